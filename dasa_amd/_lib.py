@@ -1,0 +1,97 @@
+"""ctypes binding of libdasa_hip.so (C-ABI: include/dasa_hip.h).
+
+This is the product's only path to compute: there is no CPU fallback. If the library is missing
+or cannot be loaded, `lib()` raises — callers on a GPU box therefore fail loudly instead of silently
+running something else.
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdasa_hip.so")
+
+f32p = C.c_void_p  # device pointers travel as integers
+i64 = C.c_int64
+i32 = C.c_int32
+u64 = C.c_uint64
+f32 = C.c_float
+vp = C.c_void_p
+
+ACT_NONE, ACT_RELU, ACT_GELU, ACT_TANH, ACT_SIGMOID = 0, 1, 2, 3, 4
+
+
+class GemmDesc(C.Structure):
+    _fields_ = [
+        ("M", i32), ("N", i32), ("K", i32), ("batch", i32),
+        ("opA", i32), ("opB", i32),
+        ("A", vp), ("lda", i64), ("strideA", i64),
+        ("B", vp), ("ldb", i64), ("strideB", i64),
+        ("C", vp), ("ldc", i64), ("strideC", i64),
+        ("bias", vp),
+        ("act", i32),
+        ("aux", vp), ("ld_aux", i64), ("strideAux", i64),
+        ("colscale", vp),
+        ("alpha", f32), ("beta", f32),
+    ]
+
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "dasa_version": (i32, []),
+    "dasa_build_info": (C.c_char_p, []),
+    "dasa_error_string": (C.c_char_p, [i32]),
+    "dasa_gemm_f32_workspace": (i64, [C.POINTER(GemmDesc)]),
+    "dasa_gemm_f32": (i32, [C.POINTER(GemmDesc), vp, i64, vp]),
+    "dasa_layernorm_fwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, f32, f32, u64, vp]),
+    "dasa_layernorm_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp]),
+    "dasa_bert_embed_fwd": (i32, [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, f32, f32, u64, vp]),
+    "dasa_mha_fwd": (i32, [vp, i64, vp, i64, vp, i64, vp, vp, i64, vp, i32, i32, i32, i32, i32, f32, f32, u64, vp]),
+    "dasa_mha_bwd": (i32, [vp, i64, vp, i64, vp, i64, vp, vp, i64, vp, vp, vp, i32, i32, i32, i32, i32, f32, vp]),
+    "dasa_softdot_fwd": (i32, [vp, vp, i64, vp, vp, vp, vp, i32, i32, i32, vp]),
+    "dasa_softdot_bwd": (i32, [vp, vp, i64, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp, vp]),
+    "dasa_shift_attn_fwd": (i32, [vp, vp, i64, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp]),
+    "dasa_shift_attn_bwd": (i32, [vp, vp, i64, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp, vp]),
+    "dasa_lstm_cell_fwd": (i32, [vp, vp, vp, vp, vp, i32, i32, vp]),
+    "dasa_lstm_cell_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, i32, i32, vp]),
+    "dasa_bilstm_workspace": (i64, [i32, i32]),
+    "dasa_bilstm_fwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp]),
+    "dasa_bilstm_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp]),
+    "dasa_adain_musigma_fwd": (i32, [vp, i64, vp, i64, vp, i64, vp, i32, i32, f32, vp]),
+    "dasa_reverse_valid": (i32, [vp, vp, vp, i32, i32, i32, vp]),
+    "dasa_dropout_fwd": (i32, [vp, i64, vp, i64, i32, i32, f32, u64, vp]),
+    "dasa_ada_gate_fwd": (i32, [vp, i64, vp, i64, vp, vp, i64, i32, i32, vp]),
+    "dasa_ada_gate_bwd": (i32, [vp, i64, vp, i64, vp, i64, vp, vp, i64, i32, i32, vp]),
+    "dasa_act_bwd": (i32, [vp, vp, vp, i64, i32, vp]),
+    "dasa_add2d": (i32, [vp, i64, vp, i64, vp, i64, i32, i32, vp]),
+    "dasa_copy2d": (i32, [vp, i64, vp, i64, i32, i32, vp]),
+}
+
+_LIB = None
+
+
+class DasaError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libdasa_hip.so (once). Raises DasaError if it is missing."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise DasaError(
+            f"libdasa_hip.so not found at {LIB_PATH}: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            " (there is no CPU fallback for the DASA hot path)")
+    L = C.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = L
+    return L
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = lib().dasa_error_string(rc)
+        raise DasaError(f"{what} failed: hip error {rc} ({msg.decode() if msg else '?'})")

@@ -1,0 +1,492 @@
+// BERT / LXRT building blocks for gfx950 (vilmodel.py:147-325, 443-506, 1014-1095):
+// residual+dropout+LayerNorm, embeddings gather+LN, masked multi-head attention core, plus the
+// token reversal of DicEncoder (r2rmodel.py:2326-2330), the mu/sigma AdaIN (model.py:1822-1840)
+// and a counter-RNG dropout.
+//
+// LayerNorm: one wave per row, the row held in registers (VPL float4 per lane), two-pass mean/var
+// with wave-shuffle reductions — HBM-bound, one read of x/res, one write of y.
+// MHA: one workgroup per (batch, head); K and V of that head are staged in LDS (Lk <= 128, dh = 64,
+// padded rows so the per-lane key-row reads are conflict-free); each wave owns query rows: lane j
+// scores key j (and j+64), wave-shuffle softmax, then lane d accumulates sum_j p_j V[j][d].
+#include "common.h"
+#include "../../include/dasa_hip.h"
+
+namespace {
+
+inline int cdivi(long a, long b) { return (int)((a + b - 1) / b); }
+
+// ------------------------------------------------------------------ LayerNorm
+template <int VPL>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x, const float* __restrict__ res,
+                                                     const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                     float* __restrict__ y, float* __restrict__ mean_out,
+                                                     float* __restrict__ rstd_out, float* __restrict__ xsum,
+                                                     int M, int N, float eps, float p, uint64_t seed) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const int N4 = N >> 2;
+  const float4* x4 = reinterpret_cast<const float4*>(x + (long)row * N);
+  const float4* r4 = res ? reinterpret_cast<const float4*>(res + (long)row * N) : nullptr;
+  float4 v[VPL];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = lane + 64 * i;
+    if (c < N4) {
+      float4 a = x4[c];
+      if (p > 0.f) {
+        const uint64_t base = (uint64_t)row * N + 4 * c;
+        a.x *= dasa_dropout_scale(p, seed, base + 0);
+        a.y *= dasa_dropout_scale(p, seed, base + 1);
+        a.z *= dasa_dropout_scale(p, seed, base + 2);
+        a.w *= dasa_dropout_scale(p, seed, base + 3);
+      }
+      if (r4) {
+        const float4 b = r4[c];
+        a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+      }
+      v[i] = a;
+      s += (a.x + a.y) + (a.z + a.w);
+    } else {
+      v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  const float mean = wave_sum(s) / N;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = lane + 64 * i;
+    if (c < N4) {
+      const float dx = v[i].x - mean, dy = v[i].y - mean, dz = v[i].z - mean, dw = v[i].w - mean;
+      q += (dx * dx + dy * dy) + (dz * dz + dw * dw);
+    }
+  }
+  const float var = wave_sum(q) / N;
+  const float rstd = rsqrtf(var + eps);
+  const float4* g4 = reinterpret_cast<const float4*>(gamma);
+  const float4* b4 = reinterpret_cast<const float4*>(beta);
+  float4* y4 = reinterpret_cast<float4*>(y + (long)row * N);
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = lane + 64 * i;
+    if (c < N4) {
+      if (xsum) reinterpret_cast<float4*>(xsum + (long)row * N)[c] = v[i];
+      const float4 g = g4[c], bb = b4[c];
+      float4 o;
+      o.x = (v[i].x - mean) * rstd * g.x + bb.x;
+      o.y = (v[i].y - mean) * rstd * g.y + bb.y;
+      o.z = (v[i].z - mean) * rstd * g.z + bb.z;
+      o.w = (v[i].w - mean) * rstd * g.w + bb.w;
+      y4[c] = o;
+    }
+  }
+  if (lane == 0) {
+    if (mean_out) mean_out[row] = mean;
+    if (rstd_out) rstd_out[row] = rstd;
+  }
+}
+
+// dx = rstd * (g*dy - mean(g*dy) - xhat * mean(g*dy*xhat)); dgamma += dy*xhat; dbeta += dy.
+template <int VPL>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ xsum,
+                                                     const float* __restrict__ gamma, const float* __restrict__ mean_in,
+                                                     const float* __restrict__ rstd_in, float* __restrict__ dx,
+                                                     float* __restrict__ dgamma, float* __restrict__ dbeta, int M,
+                                                     int N) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const float mean = mean_in[row], rstd = rstd_in[row];
+  const int N4 = N >> 2;
+  float4 xh[VPL], gd[VPL];
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = lane + 64 * i;
+    if (c < N4) {
+      const float4 xs = reinterpret_cast<const float4*>(xsum + (long)row * N)[c];
+      const float4 d = reinterpret_cast<const float4*>(dy + (long)row * N)[c];
+      const float4 g = reinterpret_cast<const float4*>(gamma)[c];
+      xh[i] = make_float4((xs.x - mean) * rstd, (xs.y - mean) * rstd, (xs.z - mean) * rstd, (xs.w - mean) * rstd);
+      gd[i] = make_float4(d.x * g.x, d.y * g.y, d.z * g.z, d.w * g.w);
+      s1 += gd[i].x + gd[i].y + gd[i].z + gd[i].w;
+      s2 += gd[i].x * xh[i].x + gd[i].y * xh[i].y + gd[i].z * xh[i].z + gd[i].w * xh[i].w;
+      if (dgamma) {
+        atomicAdd(dgamma + 4 * c + 0, d.x * xh[i].x);
+        atomicAdd(dgamma + 4 * c + 1, d.y * xh[i].y);
+        atomicAdd(dgamma + 4 * c + 2, d.z * xh[i].z);
+        atomicAdd(dgamma + 4 * c + 3, d.w * xh[i].w);
+      }
+      if (dbeta) {
+        atomicAdd(dbeta + 4 * c + 0, d.x);
+        atomicAdd(dbeta + 4 * c + 1, d.y);
+        atomicAdd(dbeta + 4 * c + 2, d.z);
+        atomicAdd(dbeta + 4 * c + 3, d.w);
+      }
+    }
+  }
+  const float m1 = wave_sum(s1) / N, m2 = wave_sum(s2) / N;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = lane + 64 * i;
+    if (c < N4) {
+      float4 o;
+      o.x = rstd * (gd[i].x - m1 - xh[i].x * m2);
+      o.y = rstd * (gd[i].y - m1 - xh[i].y * m2);
+      o.z = rstd * (gd[i].z - m1 - xh[i].z * m2);
+      o.w = rstd * (gd[i].w - m1 - xh[i].w * m2);
+      reinterpret_cast<float4*>(dx + (long)row * N)[c] = o;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ embeddings
+template <int VPL>
+__global__ __launch_bounds__(256) void embed_kernel(const int64_t* __restrict__ ids, const float* __restrict__ word,
+                                                    const float* __restrict__ pos, const float* __restrict__ type0,
+                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                    float* __restrict__ out, int B, int L, int H, float eps, float p,
+                                                    uint64_t seed) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= B * L) return;
+  const int t = row % L;
+  const long id = ids[row];
+  const int H4 = H >> 2;
+  const float4* w4 = reinterpret_cast<const float4*>(word + id * H);
+  const float4* p4 = reinterpret_cast<const float4*>(pos + (long)t * H);
+  const float4* t4 = reinterpret_cast<const float4*>(type0);
+  float4 v[VPL];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = lane + 64 * i;
+    if (c < H4) {
+      const float4 a = w4[c], b = p4[c], d = t4[c];
+      // (word + pos) + type, the reference's summation order (vilmodel.py:173)
+      v[i] = make_float4((a.x + b.x) + d.x, (a.y + b.y) + d.y, (a.z + b.z) + d.z, (a.w + b.w) + d.w);
+      s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+    } else {
+      v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  const float mean = wave_sum(s) / H;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = lane + 64 * i;
+    if (c < H4) {
+      const float dx = v[i].x - mean, dy = v[i].y - mean, dz = v[i].z - mean, dw = v[i].w - mean;
+      q += (dx * dx + dy * dy) + (dz * dz + dw * dw);
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(q) / H + eps);
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = lane + 64 * i;
+    if (c < H4) {
+      const float4 g = reinterpret_cast<const float4*>(gamma)[c], bb = reinterpret_cast<const float4*>(beta)[c];
+      float4 o;
+      o.x = (v[i].x - mean) * rstd * g.x + bb.x;
+      o.y = (v[i].y - mean) * rstd * g.y + bb.y;
+      o.z = (v[i].z - mean) * rstd * g.z + bb.z;
+      o.w = (v[i].w - mean) * rstd * g.w + bb.w;
+      if (p > 0.f) {
+        const uint64_t base = (uint64_t)row * H + 4 * c;
+        o.x *= dasa_dropout_scale(p, seed, base + 0);
+        o.y *= dasa_dropout_scale(p, seed, base + 1);
+        o.z *= dasa_dropout_scale(p, seed, base + 2);
+        o.w *= dasa_dropout_scale(p, seed, base + 3);
+      }
+      reinterpret_cast<float4*>(out + (long)row * H)[c] = o;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ multi-head attention
+constexpr int kDh = 64;
+constexpr int kMaxLk = 128;
+
+struct MhaArgs {
+  const float* Q; long ldq; const float* K; long ldk; const float* V; long ldv;
+  const float* mask; float* out; long ldo; float* probs;
+  int B, heads, Lq, Lk; float scale; float p; uint64_t seed;
+};
+
+// grid (B*heads, ceil(Lq/16)), 256 threads; each wave handles 4 query rows.
+__global__ __launch_bounds__(256) void mha_fwd_kernel(MhaArgs a) {
+  __shared__ float Ks[kMaxLk][kDh + 1];
+  __shared__ float Vs[kMaxLk][kDh];
+  __shared__ float qs[4][kDh];
+  __shared__ float ps[4][kMaxLk];
+  const int bh = blockIdx.x, b = bh / a.heads, h = bh % a.heads;
+  const int Lk = a.Lk;
+  for (int idx = threadIdx.x; idx < Lk * kDh; idx += 256) {
+    const int j = idx / kDh, d = idx % kDh;
+    Ks[j][d] = a.K[((long)b * Lk + j) * a.ldk + h * kDh + d];
+    Vs[j][d] = a.V[((long)b * Lk + j) * a.ldv + h * kDh + d];
+  }
+  __syncthreads();
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const float* mrow = a.mask ? a.mask + (long)b * Lk : nullptr;
+  for (int qi = 0; qi < 4; ++qi) {
+    const int i = blockIdx.y * 16 + w * 4 + qi;
+    if (i >= a.Lq) break;
+    qs[w][lane] = a.Q[((long)b * a.Lq + i) * a.ldq + h * kDh + lane];
+    __builtin_amdgcn_wave_barrier();
+    float s0 = -INFINITY, s1 = -INFINITY;
+    if (lane < Lk) {
+      float acc = 0.f;
+#pragma unroll 16
+      for (int d = 0; d < kDh; ++d) acc = fmaf(qs[w][d], Ks[lane][d], acc);
+      s0 = acc * a.scale + (mrow ? mrow[lane] : 0.f);
+    }
+    if (lane + 64 < Lk) {
+      float acc = 0.f;
+#pragma unroll 16
+      for (int d = 0; d < kDh; ++d) acc = fmaf(qs[w][d], Ks[lane + 64][d], acc);
+      s1 = acc * a.scale + (mrow ? mrow[lane + 64] : 0.f);
+    }
+    const float m = wave_max(fmaxf(s0, s1));
+    const float e0 = lane < Lk ? __expf(s0 - m) : 0.f;
+    const float e1 = lane + 64 < Lk ? __expf(s1 - m) : 0.f;
+    const float inv = 1.f / wave_sum(e0 + e1);
+    float p0 = e0 * inv, p1 = e1 * inv;
+    const long prow = (((long)b * a.heads + h) * a.Lq + i) * Lk;
+    if (a.probs) {
+      if (lane < Lk) a.probs[prow + lane] = p0;
+      if (lane + 64 < Lk) a.probs[prow + lane + 64] = p1;
+    }
+    if (a.p > 0.f) {
+      p0 *= dasa_dropout_scale(a.p, a.seed, (uint64_t)prow + lane);
+      p1 *= dasa_dropout_scale(a.p, a.seed, (uint64_t)prow + lane + 64);
+    }
+    ps[w][lane] = p0;
+    ps[w][lane + 64] = p1;
+    __builtin_amdgcn_wave_barrier();
+    float o = 0.f;
+    for (int j = 0; j < Lk; ++j) o = fmaf(ps[w][j], Vs[j][lane], o);
+    a.out[((long)b * a.Lq + i) * a.ldo + h * kDh + lane] = o;
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// Backward (no attention dropout): one workgroup per (b, h); dQ, dK, dV written (not accumulated).
+__global__ __launch_bounds__(256) void mha_bwd_kernel(MhaArgs a, const float* dO, long lddo, float* dQ, float* dK,
+                                                      float* dV) {
+  __shared__ float Ks[kMaxLk][kDh + 1];
+  __shared__ float Vs[kMaxLk][kDh + 1];
+  __shared__ float dKs[kMaxLk][kDh + 1];
+  __shared__ float dVs[kMaxLk][kDh + 1];
+  __shared__ float qs[4][kDh];
+  __shared__ float dos[4][kDh];
+  __shared__ float dss[4][kMaxLk];
+  const int bh = blockIdx.x, b = bh / a.heads, h = bh % a.heads;
+  const int Lk = a.Lk;
+  for (int idx = threadIdx.x; idx < Lk * kDh; idx += 256) {
+    const int j = idx / kDh, d = idx % kDh;
+    Ks[j][d] = a.K[((long)b * Lk + j) * a.ldk + h * kDh + d];
+    Vs[j][d] = a.V[((long)b * Lk + j) * a.ldv + h * kDh + d];
+    dKs[j][d] = 0.f;
+    dVs[j][d] = 0.f;
+  }
+  __syncthreads();
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // waves take query rows round-robin; dK/dV accumulated per wave into LDS with atomics
+  for (int i = w; i < a.Lq; i += 4) {
+    qs[w][lane] = a.Q[((long)b * a.Lq + i) * a.ldq + h * kDh + lane];
+    dos[w][lane] = dO[((long)b * a.Lq + i) * lddo + h * kDh + lane];
+    __builtin_amdgcn_wave_barrier();
+    const long prow = (((long)b * a.heads + h) * a.Lq + i) * Lk;
+    float p0 = lane < Lk ? a.probs[prow + lane] : 0.f;
+    float p1 = lane + 64 < Lk ? a.probs[prow + lane + 64] : 0.f;
+    float dp0 = 0.f, dp1 = 0.f;
+    if (lane < Lk)
+      for (int d = 0; d < kDh; ++d) dp0 = fmaf(dos[w][d], Vs[lane][d], dp0);
+    if (lane + 64 < Lk)
+      for (int d = 0; d < kDh; ++d) dp1 = fmaf(dos[w][d], Vs[lane + 64][d], dp1);
+    const float dot = wave_sum(p0 * dp0 + p1 * dp1);
+    const float ds0 = p0 * (dp0 - dot) * a.scale, ds1 = p1 * (dp1 - dot) * a.scale;
+    dss[w][lane] = ds0;
+    dss[w][lane + 64] = ds1;
+    __builtin_amdgcn_wave_barrier();
+    float dq = 0.f;
+    for (int j = 0; j < Lk; ++j) dq = fmaf(dss[w][j], Ks[j][lane], dq);
+    dQ[((long)b * a.Lq + i) * a.ldq + h * kDh + lane] = dq;
+    // dK[j][d] += ds_j * q[d]; dV[j][d] += p_j * dO[d]  (lane = d)
+    for (int j = 0; j < Lk; ++j) {
+      const float pj = j < 64 ? __shfl(p0, j, 64) : __shfl(p1, j - 64, 64);
+      atomicAdd(&dKs[j][lane], dss[w][j] * qs[w][lane]);
+      atomicAdd(&dVs[j][lane], pj * dos[w][lane]);
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < Lk * kDh; idx += 256) {
+    const int j = idx / kDh, d = idx % kDh;
+    dK[((long)b * Lk + j) * a.ldk + h * kDh + d] = dKs[j][d];
+    dV[((long)b * Lk + j) * a.ldv + h * kDh + d] = dVs[j][d];
+  }
+}
+
+// ------------------------------------------------------------------ misc
+__global__ void reverse_valid_kernel(const float* __restrict__ x, const int* __restrict__ len, float* __restrict__ out,
+                                     int B, int L, int H) {
+  const long total = (long)B * L * (H / 4);
+  for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(idx % (H / 4));
+    const long rt = idx / (H / 4);
+    const int t = (int)(rt % L), b = (int)(rt / L);
+    const int n = len[b];
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (t < n) v = reinterpret_cast<const float4*>(x + ((long)b * L + (n - 1 - t)) * H)[c];
+    reinterpret_cast<float4*>(out + ((long)b * L + t) * H)[c] = v;
+  }
+}
+
+__global__ void dropout_kernel(const float* __restrict__ x, long ldx, float* __restrict__ y, long ldy, int rows,
+                               int cols, float p, uint64_t seed) {
+  const long total = (long)rows * cols;
+  for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    const int r = (int)(idx / cols), c = (int)(idx % cols);
+    y[(long)r * ldy + c] = x[(long)r * ldx + c] * dasa_dropout_scale(p, seed, (uint64_t)idx);
+  }
+}
+
+// AdaIN mu/sigma: two rows (content, style) per wave; unbiased variance + eps, sqrt (model.py:1822-1830).
+__global__ __launch_bounds__(256) void adain_musigma_kernel(const float* __restrict__ cnt, long ldc,
+                                                            const float* __restrict__ sty, long lds,
+                                                            float* __restrict__ out, long ldo, float* __restrict__ stats,
+                                                            int M, int N, float eps) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const float* c = cnt + (long)row * ldc;
+  const float* s = sty + (long)row * lds;
+  float sc = 0.f, ss = 0.f;
+  for (int i = lane; i < N; i += 64) { sc += c[i]; ss += s[i]; }
+  const float mc = wave_sum(sc) / N, ms = wave_sum(ss) / N;
+  float vc = 0.f, vs = 0.f;
+  for (int i = lane; i < N; i += 64) {
+    const float a = c[i] - mc, b = s[i] - ms;
+    vc += a * a;
+    vs += b * b;
+  }
+  const float sdc = sqrtf(wave_sum(vc) / (N - 1) + eps), sds = sqrtf(wave_sum(vs) / (N - 1) + eps);
+  float* o = out + (long)row * ldo;
+  for (int i = lane; i < N; i += 64) o[i] = (c[i] - mc) / sdc * sds + ms;
+  if (stats && lane == 0) {
+    stats[4 * row + 0] = mc; stats[4 * row + 1] = sdc; stats[4 * row + 2] = ms; stats[4 * row + 3] = sds;
+  }
+}
+
+}  // namespace
+
+extern "C" int dasa_version(void) { return 1; }
+extern "C" const char* dasa_build_info(void) { return "libdasa_hip gfx950 (CDNA4) fp32-MFMA v1"; }
+
+#define DASA_VPL_DISPATCH(N, KERNEL, GRID, ...)                                        \
+  do {                                                                                 \
+    const int vpl = ((N) / 4 + 63) / 64;                                               \
+    switch (vpl) {                                                                     \
+      case 1: hipLaunchKernelGGL(KERNEL<1>, GRID, dim3(256), 0, st, __VA_ARGS__); break; \
+      case 2: hipLaunchKernelGGL(KERNEL<2>, GRID, dim3(256), 0, st, __VA_ARGS__); break; \
+      case 3: hipLaunchKernelGGL(KERNEL<3>, GRID, dim3(256), 0, st, __VA_ARGS__); break; \
+      case 4: hipLaunchKernelGGL(KERNEL<4>, GRID, dim3(256), 0, st, __VA_ARGS__); break; \
+      case 8: case 5: case 6: case 7:                                                  \
+        hipLaunchKernelGGL(KERNEL<8>, GRID, dim3(256), 0, st, __VA_ARGS__); break;       \
+      default: return (int)hipErrorInvalidValue;                                       \
+    }                                                                                  \
+  } while (0)
+
+extern "C" int dasa_layernorm_fwd(const float* x, const float* res, const float* gamma, const float* beta, float* y,
+                                  float* mean, float* rstd, float* xsum, int32_t M, int32_t N, float eps,
+                                  float drop_p, uint64_t seed, void* stream) {
+  if (M <= 0) return 0;
+  if ((N & 3) || N > 8192) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  DASA_VPL_DISPATCH(N, ln_fwd_kernel, dim3(cdivi(M, 4)), x, res, gamma, beta, y, mean, rstd, xsum, M, N, eps, drop_p,
+                    seed);
+  DASA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dasa_layernorm_bwd(const float* dy, const float* xsum, const float* gamma, const float* mean,
+                                  const float* rstd, float* dx, float* dgamma, float* dbeta, int32_t M, int32_t N,
+                                  void* stream) {
+  if (M <= 0) return 0;
+  if ((N & 3) || N > 8192) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  DASA_VPL_DISPATCH(N, ln_bwd_kernel, dim3(cdivi(M, 4)), dy, xsum, gamma, mean, rstd, dx, dgamma, dbeta, M, N);
+  DASA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dasa_bert_embed_fwd(const int64_t* ids, const float* word, const float* pos, const float* type0,
+                                   const float* gamma, const float* beta, float* out, int32_t B, int32_t L, int32_t H,
+                                   float eps, float drop_p, uint64_t seed, void* stream) {
+  if (B <= 0 || L <= 0) return 0;
+  if ((H & 3) || H > 8192) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  DASA_VPL_DISPATCH(H, embed_kernel, dim3(cdivi((long)B * L, 4)), ids, word, pos, type0, gamma, beta, out, B, L, H,
+                    eps, drop_p, seed);
+  DASA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dasa_mha_fwd(const float* Q, int64_t ldq, const float* K, int64_t ldk, const float* V, int64_t ldv,
+                            const float* addmask, float* out, int64_t ldo, float* probs, int32_t B, int32_t heads,
+                            int32_t Lq, int32_t Lk, int32_t dh, float scale, float drop_p, uint64_t seed,
+                            void* stream) {
+  if (B <= 0 || Lq <= 0) return 0;
+  if (dh != kDh || Lk <= 0 || Lk > kMaxLk) return (int)hipErrorInvalidValue;
+  MhaArgs a{Q, ldq, K, ldk, V, ldv, addmask, out, ldo, probs, B, heads, Lq, Lk, scale, drop_p, seed};
+  hipLaunchKernelGGL(mha_fwd_kernel, dim3(B * heads, cdivi(Lq, 16)), dim3(256), 0, (hipStream_t)stream, a);
+  DASA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dasa_mha_bwd(const float* Q, int64_t ldq, const float* K, int64_t ldk, const float* V, int64_t ldv,
+                            const float* probs, const float* dout, int64_t lddo, float* dQ, float* dK, float* dV,
+                            int32_t B, int32_t heads, int32_t Lq, int32_t Lk, int32_t dh, float scale, void* stream) {
+  if (B <= 0 || Lq <= 0) return 0;
+  if (dh != kDh || Lk <= 0 || Lk > kMaxLk || !probs) return (int)hipErrorInvalidValue;
+  MhaArgs a{Q, ldq, K, ldk, V, ldv, nullptr, nullptr, 0, const_cast<float*>(probs), B, heads, Lq, Lk, scale, 0.f, 0};
+  hipLaunchKernelGGL(mha_bwd_kernel, dim3(B * heads), dim3(256), 0, (hipStream_t)stream, a, dout, (long)lddo, dQ, dK,
+                     dV);
+  DASA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dasa_reverse_valid(const float* x, const int32_t* lengths, float* out, int32_t B, int32_t L, int32_t H,
+                                  void* stream) {
+  if (B <= 0 || L <= 0) return 0;
+  if (H & 3) return (int)hipErrorInvalidValue;
+  const long total = (long)B * L * (H / 4);
+  int grid = cdivi(total, 256);
+  if (grid > 8192) grid = 8192;
+  hipLaunchKernelGGL(reverse_valid_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, lengths, out, B, L, H);
+  DASA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dasa_dropout_fwd(const float* x, int64_t ldx, float* y, int64_t ldy, int32_t rows, int32_t cols,
+                                float p, uint64_t seed, void* stream) {
+  if (rows <= 0 || cols <= 0) return 0;
+  const long total = (long)rows * cols;
+  int grid = cdivi(total, 256);
+  if (grid > 8192) grid = 8192;
+  hipLaunchKernelGGL(dropout_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, (long)ldx, y, (long)ldy, rows,
+                     cols, p, seed);
+  DASA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dasa_adain_musigma_fwd(const float* content, int64_t ldc_, const float* style, int64_t lds, float* out,
+                                      int64_t ldo, float* stats, int32_t M, int32_t N, float eps, void* stream) {
+  if (M <= 0) return 0;
+  if (N < 2) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(adain_musigma_kernel, dim3(cdivi(M, 4)), dim3(256), 0, (hipStream_t)stream, content,
+                     (long)ldc_, style, (long)lds, out, (long)ldo, stats, M, N, eps);
+  DASA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" const char* dasa_error_string(int e) { return hipGetErrorString((hipError_t)e); }

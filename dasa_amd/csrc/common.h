@@ -1,0 +1,65 @@
+// Shared device helpers for the DASA gfx950 kernels.
+// Wave = 64 lanes on CDNA4; every reduction below is written for 64.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define DASA_WAVE 64
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+#define DASA_CHECK_LAUNCH()                                   \
+  do {                                                        \
+    hipError_t _e = hipGetLastError();                        \
+    if (_e != hipSuccess) return (int)_e;                     \
+  } while (0)
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x == 64*NW; `red` must hold NW floats.
+template <int NW>
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) s += red[i];
+  return s;
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+// Exact-erf GELU, matching vilmodel.py:125-131 (x * 0.5 * (1 + erf(x / sqrt(2)))).
+__device__ __forceinline__ float gelu_erf(float x) { return x * 0.5f * (1.f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+// Counter-based dropout RNG (splitmix64 finaliser over seed ^ index): stateless,
+// so a kernel can regenerate the same keep-mask in its backward from (seed, index).
+__device__ __forceinline__ float dasa_uniform(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (idx + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(z >> 40) * (1.0f / 16777216.0f);  // [0,1)
+}
+__device__ __forceinline__ float dasa_dropout_scale(float p, uint64_t seed, uint64_t idx) {
+  if (p <= 0.f) return 1.f;
+  return dasa_uniform(seed, idx) >= p ? 1.f / (1.f - p) : 0.f;
+}

@@ -1,0 +1,299 @@
+// fp32 GEMM on gfx950 matrix cores (v_mfma_f32_32x32x2_f32, exact f32 fma chain).
+//
+// Replaces the nn.Linear / torch.bmm calls of the reference policy (model.py SoftDot/Shift/LSTMCell
+// projections, vilmodel.py BERT/LXRT projections and FFN, agent_dg.py:1519 DGAdaChannel.a_fc).
+//
+// Structure: 256-thread workgroup = 4 waves, block tile BM x BN x 32, each wave a WM x WN sub-tile of
+// 32x32 MFMA accumulators. Operand tiles are staged k-major in LDS ([k][m], [k][n]) so that the MFMA
+// operand read (lane l: row l&31, k-half l>>5) is a lane-contiguous ds_read_b32; two LDS buffers,
+// next tile prefetched into registers while the current one feeds the MFMAs. Epilogue is fused
+// (bias, activation, gate-multiply for DGAdaChannel, column scale for env-drop, beta accumulate).
+// Split-K over gridDim.z with a deterministic fixed-order reduce for skinny (M<=64) decoder GEMMs.
+#include "common.h"
+#include "../../include/dasa_hip.h"
+
+namespace {
+
+struct GemmP {
+  int M, N, K, batch, splitk, kchunk;
+  const float* A; long lda, sA;
+  const float* B; long ldb, sB;
+  float* C; long ldc, sC;
+  const float* bias; int act;
+  const float* aux; long ld_aux, sAux;
+  const float* colscale;
+  float alpha, beta;
+  float* ws;
+};
+
+__device__ __forceinline__ float apply_act(float v, int act) {
+  switch (act) {
+    case DASA_ACT_RELU: return fmaxf(v, 0.f);
+    case DASA_ACT_GELU: return gelu_erf(v);
+    case DASA_ACT_TANH: return tanhf(v);
+    case DASA_ACT_SIGMOID: return sigmoidf_(v);
+    default: return v;
+  }
+}
+
+__device__ __forceinline__ void epilogue_store(const GemmP& p, int b, int row, int col, float acc) {
+  float v = p.alpha * acc;
+  if (p.bias) v += p.bias[col];
+  v = apply_act(v, p.act);
+  if (p.aux) v *= p.aux[(long)b * p.sAux + (long)row * p.ld_aux + col];
+  if (p.colscale) v *= p.colscale[col];
+  float* c = p.C + (long)b * p.sC + (long)row * p.ldc + col;
+  if (p.beta != 0.f) v += p.beta * (*c);
+  *c = v;
+}
+
+// Load 4 consecutive floats starting at element `e` of a row (limit = first invalid element).
+__device__ __forceinline__ float4 load4(const float* rowp, int e, int limit) {
+  if (e + 3 < limit) return *reinterpret_cast<const float4*>(rowp + e);
+  float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e + 0 < limit) r.x = rowp[e + 0];
+  if (e + 1 < limit) r.y = rowp[e + 1];
+  if (e + 2 < limit) r.z = rowp[e + 2];
+  return r;
+}
+
+constexpr int BKT = 32;
+
+// KC = operand stored with K contiguous ([rows][K]); else stored [K][rows].
+template <int ROWS, bool KC>
+struct TileLoader {
+  static constexpr int PAD = KC ? 1 : 4;
+  static constexpr int NF4 = ROWS * BKT / 4 / 256;
+  static_assert(NF4 >= 1, "tile too small");
+  float4 r[NF4];
+
+  __device__ __forceinline__ void load(const float* base, long ld, int r0, int rlimit, int k0, int klimit) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < NF4; ++i) {
+      const int q = tid + 256 * i;
+      if (KC) {
+        const int row = q / (BKT / 4), kq = q % (BKT / 4);
+        const int gr = r0 + row;
+        r[i] = (gr < rlimit) ? load4(base + (long)gr * ld, k0 + 4 * kq, klimit) : make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+        const int kr = q / (ROWS / 4), rq = q % (ROWS / 4);
+        const int gk = k0 + kr;
+        r[i] = (gk < klimit) ? load4(base + (long)gk * ld, r0 + 4 * rq, rlimit) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+  }
+  __device__ __forceinline__ void store(float (*S)[ROWS + PAD]) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < NF4; ++i) {
+      const int q = tid + 256 * i;
+      if (KC) {
+        const int row = q / (BKT / 4), kq = q % (BKT / 4);
+        S[4 * kq + 0][row] = r[i].x;
+        S[4 * kq + 1][row] = r[i].y;
+        S[4 * kq + 2][row] = r[i].z;
+        S[4 * kq + 3][row] = r[i].w;
+      } else {
+        const int kr = q / (ROWS / 4), rq = q % (ROWS / 4);
+        *reinterpret_cast<float4*>(&S[kr][4 * rq]) = r[i];
+      }
+    }
+  }
+};
+
+template <int BM, int BN, int WM, int WN, bool AKC, bool BKC>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p) {
+  constexpr int TM = WM / 32, TN = WN / 32;
+  constexpr int WAVES_N = BN / WN;
+  static_assert((BM / WM) * (BN / WN) == 4, "4 waves per block");
+  using LA = TileLoader<BM, AKC>;
+  using LB = TileLoader<BN, BKC>;
+  __shared__ float As[2][BKT][BM + LA::PAD];
+  __shared__ float Bs[2][BKT][BN + LB::PAD];
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = (wave / WAVES_N) * WM, wn = (wave % WAVES_N) * WN;
+  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+  const int b = blockIdx.z / p.splitk, split = blockIdx.z % p.splitk;
+  const int kbeg = split * p.kchunk;
+  const int kend = min(p.K, kbeg + p.kchunk);
+  const float* A = p.A + (long)b * p.sA;
+  const float* B = p.B + (long)b * p.sB;
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  LA la;
+  LB lb;
+  const int ntiles = kend > kbeg ? (kend - kbeg + BKT - 1) / BKT : 0;
+  if (ntiles > 0) {
+    la.load(A, p.lda, m0, p.M, kbeg, kend);
+    lb.load(B, p.ldb, n0, p.N, kbeg, kend);
+    la.store(As[0]);
+    lb.store(Bs[0]);
+    __syncthreads();
+  }
+  const int hl = lane >> 5, rl = lane & 31;
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    const bool more = (t + 1) < ntiles;
+    if (more) {
+      const int k0 = kbeg + (t + 1) * BKT;
+      la.load(A, p.lda, m0, p.M, k0, kend);
+      lb.load(B, p.ldb, n0, p.N, k0, kend);
+    }
+#pragma unroll
+    for (int kk = 0; kk < BKT; kk += 2) {
+      float av[TM], bv[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) av[i] = As[buf][kk + hl][wm + i * 32 + rl];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bv[j] = Bs[buf][kk + hl][wn + j * 32 + rl];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      la.store(As[buf ^ 1]);
+      lb.store(Bs[buf ^ 1]);
+    }
+    __syncthreads();
+  }
+
+  // C/D map of the 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+        const int col = n0 + wn + j * 32 + rl;
+        if (row < p.M && col < p.N) {
+          if (p.splitk > 1)
+            p.ws[(((long)split * p.batch + b) * p.M + row) * p.N + col] = acc[i][j][r];
+          else
+            epilogue_store(p, b, row, col, acc[i][j][r]);
+        }
+      }
+}
+
+__global__ void splitk_reduce_kernel(GemmP p) {
+  const long total = (long)p.batch * p.M * p.N;
+  const long slab = total;
+  for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < p.splitk; ++k) s += p.ws[k * slab + idx];
+    const int col = (int)(idx % p.N);
+    const long t = idx / p.N;
+    const int row = (int)(t % p.M);
+    const int b = (int)(t / p.M);
+    epilogue_store(p, b, row, col, s);
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+int launch_tile(const GemmP& p, int opA, int opB, hipStream_t st) {
+  dim3 grid((p.N + BN - 1) / BN, (p.M + BM - 1) / BM, p.batch * p.splitk);
+  const bool akc = (opA == 0), bkc = (opB == 1);
+  if (akc && bkc) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, true, true>), grid, dim3(256), 0, st, p);
+  else if (akc && !bkc) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, true, false>), grid, dim3(256), 0, st, p);
+  else if (!akc && bkc) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, false, true>), grid, dim3(256), 0, st, p);
+  else hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, false, false>), grid, dim3(256), 0, st, p);
+  DASA_CHECK_LAUNCH();
+  return 0;
+}
+
+inline long cdiv(long a, long b) { return (a + b - 1) / b; }
+
+}  // namespace
+
+struct Plan { int cfg, splitk, kchunk; int64_t ws; };
+
+static Plan make_plan(const dasa_gemm_desc* d) {
+  const int M = d->M, N = d->N, K = d->K, batch = d->batch < 1 ? 1 : d->batch;
+  // Tile choice (DESIGN.md "GEMM"): fill 256 CUs first, then maximise per-wave reuse.
+  auto tiles = [&](int bm, int bn) { return cdiv(M, bm) * cdiv(N, bn) * batch; };
+  Plan pl;
+  if (M <= 32) pl.cfg = 3;
+  else if (tiles(128, 128) >= 240) pl.cfg = 0;
+  else if (tiles(64, 128) >= 200) pl.cfg = 1;
+  else pl.cfg = 2;
+  const int bm = (pl.cfg == 0) ? 128 : (pl.cfg == 3 ? 32 : 64);
+  const int bn = (pl.cfg == 2) ? 64 : 128;
+  const long blocks = tiles(bm, bn);
+  int splitk = 1;
+  if (blocks < 160 && K >= 512) {
+    splitk = (int)cdiv(256, blocks);
+    const int maxs = K / 256;  // keep >= 8 K-tiles per split
+    if (splitk > maxs) splitk = maxs;
+    if (splitk > 16) splitk = 16;
+    if (splitk < 1) splitk = 1;
+  }
+  int kchunk = (int)(cdiv(cdiv(K, splitk), BKT) * BKT);
+  if (kchunk < BKT) kchunk = BKT;
+  splitk = K > 0 ? (int)cdiv(K, kchunk) : 1;
+  pl.splitk = splitk;
+  pl.kchunk = kchunk;
+  pl.ws = splitk > 1 ? (int64_t)splitk * batch * M * N * (int64_t)sizeof(float) : 0;
+  return pl;
+}
+
+extern "C" int64_t dasa_gemm_f32_workspace(const dasa_gemm_desc* d) {
+  if (!d || d->M < 0 || d->N < 0 || d->K < 0) return 0;
+  return make_plan(d).ws;
+}
+
+extern "C" int dasa_gemm_f32(const dasa_gemm_desc* d, void* ws, int64_t ws_bytes, void* stream) {
+  if (!d) return (int)hipErrorInvalidValue;
+  const int M = d->M, N = d->N, K = d->K, batch = d->batch < 1 ? 1 : d->batch;
+  if (M < 0 || N < 0 || K < 0) return (int)hipErrorInvalidValue;
+  Plan pl = make_plan(d);
+  if (pl.splitk > 1 && (ws == nullptr || ws_bytes < pl.ws)) {  // no workspace: single pass
+    pl.splitk = 1;
+    pl.kchunk = K > 0 ? (int)(cdiv(K, BKT) * BKT) : BKT;
+  }
+  if (M == 0 || N == 0) return 0;
+  // alignment contract for float4 operand loads
+  const uintptr_t am = (uintptr_t)d->A | (uintptr_t)d->B;
+  if ((am & 15) || (d->lda & 3) || (d->ldb & 3) || (batch > 1 && ((d->strideA & 3) || (d->strideB & 3))))
+    return (int)hipErrorInvalidValue;
+  if (d->opA == 0 ? d->lda < K : d->lda < M) return (int)hipErrorInvalidValue;
+  if (d->opB == 1 ? d->ldb < K : d->ldb < N) return (int)hipErrorInvalidValue;
+  if (d->ldc < N) return (int)hipErrorInvalidValue;
+
+  GemmP p;
+  p.M = M; p.N = N; p.K = K; p.batch = batch; p.splitk = pl.splitk; p.kchunk = pl.kchunk;
+  p.A = d->A; p.lda = d->lda; p.sA = d->strideA;
+  p.B = d->B; p.ldb = d->ldb; p.sB = d->strideB;
+  p.C = d->C; p.ldc = d->ldc; p.sC = d->strideC;
+  p.bias = d->bias; p.act = d->act;
+  p.aux = d->aux; p.ld_aux = d->ld_aux; p.sAux = d->strideAux;
+  p.colscale = d->colscale; p.alpha = d->alpha; p.beta = d->beta;
+  p.ws = (float*)ws;
+  hipStream_t st = (hipStream_t)stream;
+  int rc;
+  switch (pl.cfg) {
+    case 0: rc = launch_tile<128, 128, 64, 64>(p, d->opA, d->opB, st); break;
+    case 1: rc = launch_tile<64, 128, 32, 64>(p, d->opA, d->opB, st); break;
+    case 3: rc = launch_tile<32, 128, 32, 32>(p, d->opA, d->opB, st); break;
+    default: rc = launch_tile<64, 64, 32, 32>(p, d->opA, d->opB, st); break;
+  }
+  if (rc) return rc;
+  if (pl.splitk > 1) {
+    const long total = (long)batch * M * N;
+    int grid = (int)cdiv(total, 256);
+    if (grid > 4096) grid = 4096;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid), dim3(256), 0, st, p);
+    DASA_CHECK_LAUNCH();
+  }
+  return 0;
+}

@@ -1,0 +1,325 @@
+// LSTM kernels for gfx950: the decoder nn.LSTMCell (model.py:437,514) and the encoder's packed
+// bidirectional nn.LSTM (r2rmodel.py:2239-2243, 2339-2354).
+//
+// Bi-LSTM forward: the input projection for all timesteps is one MFMA GEMM (dasa_gemm_f32, done by
+// the caller); the recurrence is L dependent step launches (one per timestep, both directions in one
+// grid). For B <= 32 a step is fused: each workgroup owns 8 hidden units = 32 gate columns (i,f,g,o
+// interleaved so the cell update is workgroup-local), its 4 waves split the K=H recurrent reduction
+// with v_mfma_f32_32x32x2_f32 (batch rows padded to 32), reduce through LDS and apply the cell.
+// W_hh (2 x 16 MB) is re-read every step and stays L2/MALL-resident.
+// Packed-sequence semantics: a row is active at time t iff t < len[b]; inactive steps freeze the
+// forward state, keep the backward state at zero, and emit zero outputs (pad_packed_sequence).
+#include "common.h"
+#include "../../include/dasa_hip.h"
+
+namespace {
+
+__device__ __forceinline__ float tanh_(float x) { return tanhf(x); }
+
+// ---------------------------------------------------------------- decoder LSTMCell
+__global__ void lstm_cell_fwd_kernel(const float* __restrict__ gates, const float* __restrict__ c_prev,
+                                     float* __restrict__ h, float* __restrict__ c, float* __restrict__ act,
+                                     int B, int H) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= B * H) return;
+  const int b = idx / H, j = idx % H;
+  const float* g = gates + (long)b * 4 * H;
+  const float i = sigmoidf_(g[j]), f = sigmoidf_(g[H + j]), gg = tanh_(g[2 * H + j]), o = sigmoidf_(g[3 * H + j]);
+  const float cn = f * c_prev[idx] + i * gg;
+  c[idx] = cn;
+  h[idx] = o * tanh_(cn);
+  if (act) {
+    float* a = act + (long)b * 4 * H;
+    a[j] = i; a[H + j] = f; a[2 * H + j] = gg; a[3 * H + j] = o;
+  }
+}
+
+__global__ void lstm_cell_bwd_kernel(const float* __restrict__ act, const float* __restrict__ c_prev,
+                                     const float* __restrict__ c, const float* __restrict__ dh,
+                                     const float* __restrict__ dc, float* __restrict__ dgates,
+                                     float* __restrict__ dc_prev, int B, int H) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= B * H) return;
+  const int b = idx / H, j = idx % H;
+  const float* a = act + (long)b * 4 * H;
+  const float i = a[j], f = a[H + j], gg = a[2 * H + j], o = a[3 * H + j];
+  const float tc = tanh_(c[idx]);
+  const float dhv = dh ? dh[idx] : 0.f;
+  const float dcv = (dc ? dc[idx] : 0.f) + dhv * o * (1.f - tc * tc);
+  float* dg = dgates + (long)b * 4 * H;
+  dg[j] = dcv * gg * i * (1.f - i);
+  dg[H + j] = dcv * c_prev[idx] * f * (1.f - f);
+  dg[2 * H + j] = dcv * i * (1.f - gg * gg);
+  dg[3 * H + j] = dhv * tc * o * (1.f - o);
+  if (dc_prev) dc_prev[idx] = dcv * f;
+}
+
+// ---------------------------------------------------------------- bi-LSTM recurrence
+struct SeqArgs {
+  const float* xproj;   // [B][L][2][4H]
+  const float* whh;     // [2][4H][H]
+  const int* len;       // [B]
+  float* out;           // [B][L][2H]
+  const float* hin;     // [2][B][H]
+  float* hout;          // [2][B][H]
+  float* c;             // [2][B][H]
+  float* save_act;      // [L][2][B][4H] or NULL
+  float* save_c;        // [L][2][B][H] or NULL
+  const float* rec;     // [2][B][4H] (unfused path) or NULL
+  int B, L, H;
+};
+
+__device__ __forceinline__ void cell_apply(const SeqArgs& a, int dir, int t, int b, int u, float g0, float g1,
+                                           float g2, float g3) {
+  const int H = a.H;
+  const long sidx = ((long)dir * a.B + b) * H + u;
+  const float* xp = a.xproj + (((long)b * a.L + t) * 2 + dir) * 4 * H;
+  g0 += xp[u]; g1 += xp[H + u]; g2 += xp[2 * H + u]; g3 += xp[3 * H + u];
+  float* outp = a.out + ((long)b * a.L + t) * 2 * H + dir * H + u;
+  if (t < a.len[b]) {
+    const float i = sigmoidf_(g0), f = sigmoidf_(g1), gg = tanh_(g2), o = sigmoidf_(g3);
+    const float cn = f * a.c[sidx] + i * gg;
+    const float hn = o * tanh_(cn);
+    a.c[sidx] = cn;
+    a.hout[sidx] = hn;
+    *outp = hn;
+    if (a.save_act) {
+      float* sa = a.save_act + (((long)t * 2 + dir) * a.B + b) * 4 * H;
+      sa[u] = i; sa[H + u] = f; sa[2 * H + u] = gg; sa[3 * H + u] = o;
+      a.save_c[(((long)t * 2 + dir) * a.B + b) * H + u] = cn;
+    }
+  } else {
+    a.hout[sidx] = a.hin[sidx];
+    *outp = 0.f;
+    if (a.save_act) {
+      float* sa = a.save_act + (((long)t * 2 + dir) * a.B + b) * 4 * H;
+      sa[u] = 0.f; sa[H + u] = 0.f; sa[2 * H + u] = 0.f; sa[3 * H + u] = 0.f;
+      a.save_c[(((long)t * 2 + dir) * a.B + b) * H + u] = a.c[sidx];
+    }
+  }
+}
+
+// Fused step for B <= 32: grid (H/8, 2), 256 threads.
+__global__ __launch_bounds__(256) void bilstm_step_fused_kernel(SeqArgs a, int s) {
+  __shared__ float red[4][32][33];
+  const int dir = blockIdx.y, u0 = blockIdx.x * 8;
+  const int H = a.H, B = a.B;
+  const int t = dir == 0 ? s : a.L - 1 - s;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int hl = lane >> 5, r = lane & 31;
+  const float* hrow = a.hin + ((long)dir * B + r) * H;
+  const bool arow = r < B;
+  const int q = r & 3, unit = u0 + (r >> 2);
+  const float* wrow = a.whh + ((long)dir * 4 * H + (long)q * H + unit) * H;
+  const int kq = H / 4, k0 = w * kq;
+  floatx16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll 4
+  for (int kb = k0; kb < k0 + kq; kb += 8) {
+    const float4 av = arow ? *reinterpret_cast<const float4*>(hrow + kb + 4 * hl) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 bv = *reinterpret_cast<const float4*>(wrow + kb + 4 * hl);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, bv.x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, bv.y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, bv.z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, bv.w, acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) red[w][(i & 3) + 8 * (i >> 2) + 4 * hl][r] = acc[i];
+  __syncthreads();
+  const int b = threadIdx.x >> 3, ul = threadIdx.x & 7;
+  if (b < B) {
+    float g[4];
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) g[qq] = red[0][b][4 * ul + qq] + red[1][b][4 * ul + qq] + red[2][b][4 * ul + qq] +
+                                           red[3][b][4 * ul + qq];
+    cell_apply(a, dir, t, b, u0 + ul, g[0], g[1], g[2], g[3]);
+  }
+}
+
+// Unfused step (any B): rec = h W_hh^T computed by dasa_gemm_f32 beforehand.
+__global__ void bilstm_step_cell_kernel(SeqArgs a, int s) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  const int total = 2 * a.B * a.H;
+  if (idx >= total) return;
+  const int dir = idx / (a.B * a.H), rem = idx % (a.B * a.H), b = rem / a.H, u = rem % a.H;
+  const int t = dir == 0 ? s : a.L - 1 - s;
+  const float* rr = a.rec + ((long)dir * a.B + b) * 4 * a.H;
+  cell_apply(a, dir, t, b, u, rr[u], rr[a.H + u], rr[2 * a.H + u], rr[3 * a.H + u]);
+}
+
+__global__ void fill_kernel(float* p, long n, float v) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) p[i] = v;
+}
+__global__ void copy_kernel(const float* src, float* dst, long n) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) dst[i] = src[i];
+}
+
+// ---------------------------------------------------------------- bi-LSTM BPTT
+struct BpttArgs {
+  const float* whh;       // [2][4H][H]
+  const int* len;
+  const float* save_act;  // [L][2][B][4H]
+  const float* save_c;    // [L][2][B][H]
+  const float* dout;      // [B][L][2H]
+  float* dgates;          // [B][L][2][4H]
+  float* dh;              // [2][B][H] carry
+  float* dc;              // [2][B][H] carry
+  int B, L, H;
+};
+
+// grid (H/32, 2), 512 threads (8 waves split the 4H reduction). s = BPTT step.
+__global__ __launch_bounds__(512) void bilstm_bptt_step_kernel(BpttArgs a, int s) {
+  __shared__ float red[8][32][33];
+  const int dir = blockIdx.y, j0 = blockIdx.x * 32;
+  const int H = a.H, B = a.B, L = a.L, G4 = 4 * H;
+  const int t = dir == 0 ? (L - 1 - s) : s;
+  const int tp = dir == 0 ? t + 1 : t - 1;  // step processed just before in BPTT order
+  const bool tpv = tp >= 0 && tp < L;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int hl = lane >> 5, r = lane & 31;
+  floatx16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  if (tpv) {
+    const bool arow = r < B;
+    const float* grow = a.dgates + (((long)r * L + tp) * 2 + dir) * G4;
+    const float* W = a.whh + (long)dir * G4 * H + j0 + r;
+    const int kq = G4 / 8, k0 = w * kq;
+#pragma unroll 8
+    for (int n = k0; n < k0 + kq; n += 2) {
+      const float av = arow ? grow[n + hl] : 0.f;
+      const float bv = W[(long)(n + hl) * H];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) red[w][(i & 3) + 8 * (i >> 2) + 4 * hl][r] = acc[i];
+  __syncthreads();
+  for (int pidx = threadIdx.x; pidx < 32 * 32; pidx += 512) {
+    const int b = pidx >> 5, jl = pidx & 31, j = j0 + jl;
+    if (b >= B) continue;
+    float rec = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) rec += red[i][b][jl];
+    const long sidx = ((long)dir * B + b) * H + j;
+    float* dg = a.dgates + (((long)b * L + t) * 2 + dir) * G4;
+    if (t < a.len[b]) {
+      const float G = rec + a.dout[((long)b * L + t) * 2 * H + dir * H + j] + a.dh[sidx];
+      const float* sa = a.save_act + (((long)t * 2 + dir) * B + b) * G4;
+      const float i_ = sa[j], f_ = sa[H + j], g_ = sa[2 * H + j], o_ = sa[3 * H + j];
+      const float ct = a.save_c[(((long)t * 2 + dir) * B + b) * H + j];
+      const int tq = dir == 0 ? t - 1 : t + 1;  // previous step in forward order
+      const float cp = (tq >= 0 && tq < L) ? a.save_c[(((long)tq * 2 + dir) * B + b) * H + j] : 0.f;
+      const float tc = tanh_(ct);
+      const float dcv = a.dc[sidx] + G * o_ * (1.f - tc * tc);
+      dg[j] = dcv * g_ * i_ * (1.f - i_);
+      dg[H + j] = dcv * cp * f_ * (1.f - f_);
+      dg[2 * H + j] = dcv * i_ * (1.f - g_ * g_);
+      dg[3 * H + j] = G * tc * o_ * (1.f - o_);
+      a.dc[sidx] = dcv * f_;
+      a.dh[sidx] = 0.f;
+    } else {
+      dg[j] = 0.f; dg[H + j] = 0.f; dg[2 * H + j] = 0.f; dg[3 * H + j] = 0.f;
+      a.dh[sidx] = rec + a.dh[sidx];
+    }
+  }
+}
+
+inline int cdivi(long a, long b) { return (int)((a + b - 1) / b); }
+
+}  // namespace
+
+extern "C" int dasa_lstm_cell_fwd(const float* gates, const float* c_prev, float* h, float* c, float* act_save,
+                                  int32_t B, int32_t H, void* stream) {
+  if (B <= 0 || H <= 0) return 0;
+  hipLaunchKernelGGL(lstm_cell_fwd_kernel, dim3(cdivi((long)B * H, 256)), dim3(256), 0, (hipStream_t)stream,
+                     gates, c_prev, h, c, act_save, B, H);
+  DASA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dasa_lstm_cell_bwd(const float* act_save, const float* c_prev, const float* c, const float* dh,
+                                  const float* dc, float* dgates, float* dc_prev, int32_t B, int32_t H,
+                                  void* stream) {
+  if (B <= 0 || H <= 0) return 0;
+  hipLaunchKernelGGL(lstm_cell_bwd_kernel, dim3(cdivi((long)B * H, 256)), dim3(256), 0, (hipStream_t)stream,
+                     act_save, c_prev, c, dh, dc, dgates, dc_prev, B, H);
+  DASA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int64_t dasa_bilstm_workspace(int32_t B, int32_t H) {
+  const long base = 6L * B * H;
+  return (int64_t)((B <= 32 ? base : base + 8L * B * H) * sizeof(float));
+}
+
+extern "C" int dasa_bilstm_fwd(const float* xproj, const float* whh, const int32_t* lengths, float* out,
+                               float* h_n, float* c_n, float* save_act, float* save_c, int32_t B, int32_t L,
+                               int32_t H, float* ws, void* stream) {
+  if (B <= 0 || L <= 0) return 0;
+  if ((H % 32) || !ws || ((uintptr_t)whh & 15) || (save_act != nullptr) != (save_c != nullptr))
+    return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  const long S = 2L * B * H;
+  float* h0 = ws;
+  float* h1 = ws + S;
+  float* c = ws + 2 * S;
+  float* rec = ws + 3 * S;
+  hipLaunchKernelGGL(fill_kernel, dim3(cdivi(3 * S, 256)), dim3(256), 0, st, ws, 3 * S, 0.f);
+  DASA_CHECK_LAUNCH();
+  SeqArgs a{xproj, whh, lengths, out, h0, h1, c, save_act, save_c, nullptr, B, L, H};
+  for (int s = 0; s < L; ++s) {
+    a.hin = (s & 1) ? h1 : h0;
+    a.hout = (s & 1) ? h0 : h1;
+    if (B <= 32) {
+      hipLaunchKernelGGL(bilstm_step_fused_kernel, dim3(H / 8, 2), dim3(256), 0, st, a, s);
+      DASA_CHECK_LAUNCH();
+    } else {
+      dasa_gemm_desc d{};
+      d.M = B; d.N = 4 * H; d.K = H; d.batch = 2; d.opA = 0; d.opB = 1;
+      d.A = a.hin; d.lda = H; d.strideA = (long)B * H;
+      d.B = whh; d.ldb = H; d.strideB = 4L * H * H;
+      d.C = rec; d.ldc = 4 * H; d.strideC = 4L * B * H;
+      d.alpha = 1.f; d.beta = 0.f;
+      int rc = dasa_gemm_f32(&d, nullptr, 0, stream);
+      if (rc) return rc;
+      a.rec = rec;
+      hipLaunchKernelGGL(bilstm_step_cell_kernel, dim3(cdivi(S, 256)), dim3(256), 0, st, a, s);
+      DASA_CHECK_LAUNCH();
+    }
+  }
+  const float* hfin = (L & 1) ? h1 : h0;
+  if (h_n) {
+    hipLaunchKernelGGL(copy_kernel, dim3(cdivi(S, 256)), dim3(256), 0, st, hfin, h_n, S);
+    DASA_CHECK_LAUNCH();
+  }
+  if (c_n) {
+    hipLaunchKernelGGL(copy_kernel, dim3(cdivi(S, 256)), dim3(256), 0, st, (const float*)c, c_n, S);
+    DASA_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+extern "C" int dasa_bilstm_bwd(const float* whh, const int32_t* lengths, const float* save_act, const float* save_c,
+                               const float* dout, const float* dh_n, const float* dc_n, float* dgates, int32_t B,
+                               int32_t L, int32_t H, float* ws, void* stream) {
+  if (B <= 0 || L <= 0) return 0;
+  if ((H % 32) || !ws || B > 32 || !save_act || !save_c || !dout) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  const long S = 2L * B * H;
+  float* dh = ws;
+  float* dc = ws + S;
+  if (dh_n) hipLaunchKernelGGL(copy_kernel, dim3(cdivi(S, 256)), dim3(256), 0, st, dh_n, dh, S);
+  else hipLaunchKernelGGL(fill_kernel, dim3(cdivi(S, 256)), dim3(256), 0, st, dh, S, 0.f);
+  DASA_CHECK_LAUNCH();
+  if (dc_n) hipLaunchKernelGGL(copy_kernel, dim3(cdivi(S, 256)), dim3(256), 0, st, dc_n, dc, S);
+  else hipLaunchKernelGGL(fill_kernel, dim3(cdivi(S, 256)), dim3(256), 0, st, dc, S, 0.f);
+  DASA_CHECK_LAUNCH();
+  BpttArgs a{whh, lengths, save_act, save_c, dout, dgates, dh, dc, B, L, H};
+  for (int s = 0; s < L; ++s) {
+    hipLaunchKernelGGL(bilstm_bptt_step_kernel, dim3(H / 32, 2), dim3(512), 0, st, a, s);
+    DASA_CHECK_LAUNCH();
+  }
+  return 0;
+}

@@ -1,0 +1,387 @@
+"""Torch-facing wrappers over libdasa_hip.so.
+
+Every function here takes/returns torch tensors on the ROCm device and enqueues HIP kernels from
+libdasa_hip.so on torch's current stream (so torch.cuda.graph capture records them). There is no
+CPU path: a CPU tensor is a usage error and raises.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import ACT_NONE, ACT_RELU, ACT_GELU, ACT_TANH, ACT_SIGMOID, GemmDesc, check  # noqa: F401
+
+_ACT_IDS = {None: ACT_NONE, "none": ACT_NONE, "relu": ACT_RELU, "gelu": ACT_GELU, "tanh": ACT_TANH,
+            "sigmoid": ACT_SIGMOID}
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _p(t):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise _lib.DasaError("dasa_amd kernels need device tensors (the HIP path has no CPU fallback)")
+    return t.data_ptr()
+
+
+def _f32(t, name):
+    if t.dtype != torch.float32:
+        raise _lib.DasaError(f"{name}: expected float32, got {t.dtype}")
+    return t
+
+
+def _rows(t):
+    """(rows, ld) of a tensor viewed as a 2-D row-major matrix over its last dim (unit inner stride)."""
+    if t.stride(-1) != 1:
+        raise _lib.DasaError("inner dimension must be contiguous")
+    if t.dim() == 1:
+        return 1, t.shape[0]
+    # all leading dims must collapse with a uniform row stride
+    ld = t.stride(-2)
+    rows = 1
+    exp = ld
+    for d in range(t.dim() - 2, -1, -1):
+        if t.shape[d] != 1 and t.stride(d) != exp:
+            raise _lib.DasaError("leading dims must collapse to a single row stride")
+        exp = t.stride(d) * t.shape[d]
+        rows *= t.shape[d]
+    return rows, ld
+
+
+# ------------------------------------------------------------------------------------------ GEMM
+def gemm(A, B, C, *, M, N, K, opA=0, opB=1, lda, ldb, ldc, bias=None, act=None, aux=None, ld_aux=0,
+         colscale=None, alpha=1.0, beta=0.0, batch=1, strideA=0, strideB=0, strideC=0, strideAux=0):
+    """Raw descriptor call (see include/dasa_hip.h). A/B/C are tensors (base pointers used)."""
+    d = GemmDesc()
+    d.M, d.N, d.K, d.batch = int(M), int(N), int(K), int(batch)
+    d.opA, d.opB = int(opA), int(opB)
+    d.A, d.lda, d.strideA = _p(A), int(lda), int(strideA)
+    d.B, d.ldb, d.strideB = _p(B), int(ldb), int(strideB)
+    d.C, d.ldc, d.strideC = _p(C), int(ldc), int(strideC)
+    d.bias = _p(bias)
+    d.act = _ACT_IDS[act] if not isinstance(act, int) else act
+    d.aux, d.ld_aux, d.strideAux = _p(aux), int(ld_aux), int(strideAux)
+    d.colscale = _p(colscale)
+    d.alpha, d.beta = float(alpha), float(beta)
+    L = _lib.lib()
+    need = L.dasa_gemm_f32_workspace(ctypes.byref(d))
+    ws = None
+    if need > 0:
+        ws = torch.empty(need // 4 + 1, dtype=torch.float32, device=C.device)
+    check(L.dasa_gemm_f32(ctypes.byref(d), _p(ws), int(need), _stream()), "dasa_gemm_f32")
+
+
+def C_dev(t):
+    return t.device
+
+
+def linear(x, W, b=None, act=None, out=None, aux=None, colscale=None, beta=0.0, alpha=1.0):
+    """y = act(x @ W^T + b) [* aux] [* colscale] (+ beta*out). x [..., K] (row-strided ok), W [N, K]."""
+    _f32(x, "linear.x")
+    K = x.shape[-1]
+    N = W.shape[0]
+    assert W.shape[1] == K and W.stride(1) == 1, "W must be [N, K] with contiguous rows"
+    M, lda = _rows(x)
+    if out is None:
+        out = torch.empty(*x.shape[:-1], N, dtype=torch.float32, device=x.device)
+    Mo, ldc = _rows(out)
+    assert Mo == M and out.shape[-1] == N
+    ld_aux = 0
+    if aux is not None:
+        Ma, ld_aux = _rows(aux)
+        assert Ma == M
+    gemm(x, W, out, M=M, N=N, K=K, opA=0, opB=1, lda=lda, ldb=W.stride(0), ldc=ldc, bias=b, act=act,
+         aux=aux, ld_aux=ld_aux, colscale=colscale, alpha=alpha, beta=beta)
+    return out
+
+
+def matmul_nn(A, B, out=None, beta=0.0):
+    """out[M,N] = A[M,K] @ B[K,N] (both row-major, row-strided ok)."""
+    M, lda = _rows(A)
+    K = A.shape[-1]
+    Kb, ldb = _rows(B)
+    assert Kb == K
+    N = B.shape[-1]
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.float32, device=A.device)
+    _, ldc = _rows(out)
+    gemm(A, B, out, M=M, N=N, K=K, opA=0, opB=0, lda=lda, ldb=ldb, ldc=ldc, beta=beta)
+    return out
+
+
+def matmul_tn(A, B, out=None, beta=0.0):
+    """out[M,N] = A[K,M]^T @ B[K,N] (weight gradients: dW = dY^T X)."""
+    K, lda = _rows(A)
+    M = A.shape[-1]
+    Kb, ldb = _rows(B)
+    assert Kb == K
+    N = B.shape[-1]
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.float32, device=A.device)
+    _, ldc = _rows(out)
+    gemm(A, B, out, M=M, N=N, K=K, opA=1, opB=0, lda=lda, ldb=ldb, ldc=ldc, beta=beta)
+    return out
+
+
+def colsum(X, out=None, beta=0.0):
+    """out[N] = sum over rows of X[M,N] (bias gradients), as a 1 x M GEMM."""
+    M, ldx = _rows(X)
+    N = X.shape[-1]
+    ones = torch.ones(1, M, dtype=torch.float32, device=X.device)
+    if out is None:
+        out = torch.empty(N, dtype=torch.float32, device=X.device)
+    gemm(ones, X, out, M=1, N=N, K=M, opA=0, opB=0, lda=M, ldb=ldx, ldc=N, beta=beta)
+    return out
+
+
+# ------------------------------------------------------------------------------------ elementwise
+def act_bwd(y_or_x, dy, act):
+    dx = torch.empty_like(dy)
+    check(_lib.lib().dasa_act_bwd(_p(y_or_x.contiguous()), _p(dy.contiguous()), _p(dx), dy.numel(),
+                                  _ACT_IDS[act], _stream()), "dasa_act_bwd")
+    return dx
+
+
+def dropout(x, p, seed, out=None):
+    """Counter-RNG dropout on a [rows, cols] (row-strided) block; same seed -> same mask."""
+    rows, ldx = _rows(x)
+    cols = x.shape[-1]
+    if out is None:
+        out = torch.empty_like(x)
+    _, ldy = _rows(out)
+    check(_lib.lib().dasa_dropout_fwd(_p(x), ldx, _p(out), ldy, rows, cols, float(p), int(seed) & (2**64 - 1),
+                                      _stream()), "dasa_dropout_fwd")
+    return out
+
+
+def copy2d(x, out):
+    rows, ldx = _rows(x)
+    _, ldo = _rows(out)
+    check(_lib.lib().dasa_copy2d(_p(x), ldx, _p(out), ldo, rows, x.shape[-1], _stream()), "dasa_copy2d")
+    return out
+
+
+def ada_gate_fwd(s, f, noise, out):
+    rows, lds = _rows(s)
+    _, ldf = _rows(f)
+    _, ldo = _rows(out)
+    check(_lib.lib().dasa_ada_gate_fwd(_p(s), lds, _p(f), ldf, _p(noise), _p(out), ldo, rows, s.shape[-1],
+                                       _stream()), "dasa_ada_gate_fwd")
+    return out
+
+
+def ada_gate_bwd(dout, s, f, noise):
+    rows, lddo = _rows(dout)
+    _, lds = _rows(s)
+    _, ldf = _rows(f)
+    dz = torch.empty(rows, s.shape[-1], dtype=torch.float32, device=s.device)
+    check(_lib.lib().dasa_ada_gate_bwd(_p(dout), lddo, _p(s), lds, _p(f), ldf, _p(noise), _p(dz), s.shape[-1],
+                                       rows, s.shape[-1], _stream()), "dasa_ada_gate_bwd")
+    return dz
+
+
+# -------------------------------------------------------------------------------------- LayerNorm
+def layernorm(x, gamma, beta, eps, res=None, drop_p=0.0, seed=0, save=False):
+    M, ld = _rows(x)
+    N = x.shape[-1]
+    assert ld == N, "layernorm expects contiguous rows"
+    y = torch.empty_like(x)
+    mean = rstd = xsum = None
+    if save:
+        mean = torch.empty(M, dtype=torch.float32, device=x.device)
+        rstd = torch.empty_like(mean)
+        xsum = torch.empty_like(x)
+    check(_lib.lib().dasa_layernorm_fwd(_p(x), _p(res), _p(gamma), _p(beta), _p(y), _p(mean), _p(rstd), _p(xsum),
+                                        M, N, float(eps), float(drop_p), int(seed) & (2**64 - 1), _stream()),
+          "dasa_layernorm_fwd")
+    if save:
+        return y, (xsum, mean, rstd)
+    return y
+
+
+def layernorm_bwd(dy, saved, gamma, dgamma, dbeta):
+    xsum, mean, rstd = saved
+    M, _ = _rows(xsum)
+    N = xsum.shape[-1]
+    dx = torch.empty_like(xsum)
+    check(_lib.lib().dasa_layernorm_bwd(_p(dy.contiguous()), _p(xsum), _p(gamma), _p(mean), _p(rstd), _p(dx),
+                                        _p(dgamma), _p(dbeta), M, N, _stream()), "dasa_layernorm_bwd")
+    return dx
+
+
+def bert_embed(ids, word, pos, type0, gamma, beta, eps, drop_p=0.0, seed=0):
+    B, L = ids.shape
+    H = word.shape[1]
+    out = torch.empty(B, L, H, dtype=torch.float32, device=word.device)
+    ids = ids.contiguous().to(torch.int64)
+    check(_lib.lib().dasa_bert_embed_fwd(_p(ids), _p(word), _p(pos), _p(type0), _p(gamma), _p(beta), _p(out), B, L,
+                                         H, float(eps), float(drop_p), int(seed) & (2**64 - 1), _stream()),
+          "dasa_bert_embed_fwd")
+    return out
+
+
+def mha(Q, K, V, addmask, heads, scale, drop_p=0.0, seed=0, save_probs=False):
+    """Q [B, Lq, heads*64], K/V [B, Lk, heads*64] (row-strided ok), addmask [B, Lk] or None."""
+    B, Lq, Hd = Q.shape
+    Lk = K.shape[1]
+    dh = Hd // heads
+    out = torch.empty(B, Lq, Hd, dtype=torch.float32, device=Q.device)
+    probs = torch.empty(B, heads, Lq, Lk, dtype=torch.float32, device=Q.device) if save_probs else None
+    check(_lib.lib().dasa_mha_fwd(_p(Q), Q.stride(1), _p(K), K.stride(1), _p(V), V.stride(1),
+                                  _p(addmask.contiguous() if addmask is not None else None), _p(out), Hd, _p(probs),
+                                  B, heads, Lq, Lk, dh, float(scale), float(drop_p), int(seed) & (2**64 - 1),
+                                  _stream()), "dasa_mha_fwd")
+    return (out, probs) if save_probs else out
+
+
+def mha_bwd(Q, K, V, probs, dout, heads, scale):
+    B, Lq, Hd = Q.shape
+    Lk = K.shape[1]
+    Q, K, V, dout = Q.contiguous(), K.contiguous(), V.contiguous(), dout.contiguous()
+    dQ, dK, dV = torch.empty_like(Q), torch.empty_like(K), torch.empty_like(V)
+    check(_lib.lib().dasa_mha_bwd(_p(Q), Hd, _p(K), Hd, _p(V), Hd, _p(probs), _p(dout), Hd, _p(dQ), _p(dK), _p(dV),
+                                  B, heads, Lq, Lk, Hd // heads, float(scale), _stream()), "dasa_mha_bwd")
+    return dQ, dK, dV
+
+
+# ------------------------------------------------------------------------------ SoftDot attention
+def softdot_fwd(q, ctx, mask=None, want_scores=True, want_probs=True, want_wctx=True):
+    """q [B, D]; ctx [B, N, D] (rows may be strided, e.g. a 2176 block); mask [B, N] bool."""
+    B, N, D = ctx.shape
+    ldn = ctx.stride(1)
+    assert ctx.stride(2) == 1 and ctx.stride(0) == N * ldn
+    q = q.contiguous()
+    scores = torch.empty(B, N, dtype=torch.float32, device=q.device)
+    probs = torch.empty(B, N, dtype=torch.float32, device=q.device) if want_probs else None
+    wctx = torch.empty(B, D, dtype=torch.float32, device=q.device) if want_wctx else None
+    m = mask.to(torch.uint8).contiguous() if mask is not None else None
+    check(_lib.lib().dasa_softdot_fwd(_p(q), _p(ctx), ldn, _p(m), _p(scores), _p(probs), _p(wctx), B, N, D,
+                                      _stream()), "dasa_softdot_fwd")
+    return scores, probs, wctx
+
+
+def softdot_bwd(q, ctx, probs, dwctx=None, dscores=None, want_dctx=True):
+    B, N, D = ctx.shape
+    ldn = ctx.stride(1)
+    dq = torch.empty(B, D, dtype=torch.float32, device=q.device)
+    dctx = torch.empty(B, N, D, dtype=torch.float32, device=q.device) if want_dctx else None
+    ws = torch.empty(B * N, dtype=torch.float32, device=q.device)
+    if dctx is not None:
+        assert ldn == D, "dctx is written dense; pass a contiguous ctx for backward"
+    check(_lib.lib().dasa_softdot_bwd(_p(q.contiguous()), _p(ctx), ldn, _p(probs),
+                                      _p(dwctx.contiguous() if dwctx is not None else None),
+                                      _p(dscores.contiguous() if dscores is not None else None), _p(dq), _p(dctx), 0,
+                                      B, N, D, _p(ws), _stream()), "dasa_softdot_bwd")
+    return dq, dctx
+
+
+def shift_attn_fwd(q, ctx, shift_logits):
+    B, N, D = ctx.shape
+    assert N == 36
+    ldn = ctx.stride(1)
+    assert ctx.stride(2) == 1 and ctx.stride(0) == N * ldn
+    K = shift_logits.shape[1]
+    attn = torch.empty(B, N, dtype=torch.float32, device=q.device)
+    shifted = torch.empty_like(attn)
+    wsm = torch.empty(B, K, dtype=torch.float32, device=q.device)
+    wctx = torch.empty(B, D, dtype=torch.float32, device=q.device)
+    ws = torch.empty(B * N, dtype=torch.float32, device=q.device)
+    check(_lib.lib().dasa_shift_attn_fwd(_p(q.contiguous()), _p(ctx), ldn, _p(shift_logits.contiguous()), _p(attn),
+                                         _p(shifted), _p(wsm), _p(wctx), B, D, K, _p(ws), _stream()),
+          "dasa_shift_attn_fwd")
+    return wctx, attn, shifted, wsm
+
+
+def shift_attn_bwd(q, ctx, attn, shifted, wsm, dwctx, want_dctx=True):
+    B, N, D = ctx.shape
+    ldn = ctx.stride(1)
+    K = wsm.shape[1]
+    dq = torch.empty(B, D, dtype=torch.float32, device=q.device)
+    dctx = torch.empty(B, N, D, dtype=torch.float32, device=q.device) if want_dctx else None
+    if dctx is not None:
+        assert ldn == D, "dctx is written dense; pass a contiguous ctx for backward"
+    dz = torch.empty(B, K, dtype=torch.float32, device=q.device)
+    ws = torch.empty(B * N, dtype=torch.float32, device=q.device)
+    check(_lib.lib().dasa_shift_attn_bwd(_p(q.contiguous()), _p(ctx), ldn, _p(attn), _p(shifted), _p(wsm),
+                                         _p(dwctx.contiguous()), _p(dq), _p(dctx), _p(dz), 0, B, D, K, _p(ws),
+                                         _stream()), "dasa_shift_attn_bwd")
+    return dq, dctx, dz
+
+
+# ------------------------------------------------------------------------------------------ LSTM
+def lstm_cell_fwd(gates, c_prev, save=False):
+    B, G4 = gates.shape
+    H = G4 // 4
+    h = torch.empty(B, H, dtype=torch.float32, device=gates.device)
+    c = torch.empty_like(h)
+    act = torch.empty_like(gates) if save else None
+    check(_lib.lib().dasa_lstm_cell_fwd(_p(gates.contiguous()), _p(c_prev.contiguous()), _p(h), _p(c), _p(act), B, H,
+                                        _stream()), "dasa_lstm_cell_fwd")
+    return h, c, act
+
+
+def lstm_cell_bwd(act, c_prev, c, dh, dc):
+    B, G4 = act.shape
+    H = G4 // 4
+    dgates = torch.empty_like(act)
+    dc_prev = torch.empty(B, H, dtype=torch.float32, device=act.device)
+    check(_lib.lib().dasa_lstm_cell_bwd(_p(act), _p(c_prev.contiguous()), _p(c), _p(dh.contiguous() if dh is not None else None),
+                                        _p(dc.contiguous() if dc is not None else None), _p(dgates), _p(dc_prev), B, H,
+                                        _stream()), "dasa_lstm_cell_bwd")
+    return dgates, dc_prev
+
+
+def bilstm_fwd(xproj, whh, lengths_i32, H, save=False):
+    """xproj [B, L, 2, 4H]; whh [2, 4H, H]; lengths int32 [B] (device). Returns out [B, L, 2H],
+    h_n [2, B, H], c_n [2, B, H], saved (act, c) or None."""
+    B, L = xproj.shape[0], xproj.shape[1]
+    dev = xproj.device
+    out = torch.empty(B, L, 2 * H, dtype=torch.float32, device=dev)
+    h_n = torch.empty(2, B, H, dtype=torch.float32, device=dev)
+    c_n = torch.empty_like(h_n)
+    sa = sc = None
+    if save:
+        sa = torch.empty(L, 2, B, 4 * H, dtype=torch.float32, device=dev)
+        sc = torch.empty(L, 2, B, H, dtype=torch.float32, device=dev)
+    L_ = _lib.lib()
+    ws = torch.empty(L_.dasa_bilstm_workspace(B, H) // 4, dtype=torch.float32, device=dev)
+    check(L_.dasa_bilstm_fwd(_p(xproj.contiguous()), _p(whh), _p(lengths_i32), _p(out), _p(h_n), _p(c_n), _p(sa),
+                             _p(sc), B, L, H, _p(ws), _stream()), "dasa_bilstm_fwd")
+    return out, h_n, c_n, ((sa, sc) if save else None)
+
+
+def bilstm_bwd(whh, lengths_i32, saved, dout, dh_n, dc_n, H):
+    sa, sc = saved
+    L, _, B, _ = sa.shape
+    dev = sa.device
+    dgates = torch.empty(B, L, 2, 4 * H, dtype=torch.float32, device=dev)
+    ws = torch.empty(4 * B * H, dtype=torch.float32, device=dev)
+    check(_lib.lib().dasa_bilstm_bwd(_p(whh), _p(lengths_i32), _p(sa), _p(sc), _p(dout.contiguous()),
+                                     _p(dh_n.contiguous() if dh_n is not None else None),
+                                     _p(dc_n.contiguous() if dc_n is not None else None), _p(dgates), B, L, H, _p(ws),
+                                     _stream()), "dasa_bilstm_bwd")
+    return dgates
+
+
+def reverse_valid(x, lengths_i32):
+    B, L, H = x.shape
+    out = torch.empty_like(x)
+    check(_lib.lib().dasa_reverse_valid(_p(x.contiguous()), _p(lengths_i32), _p(out), B, L, H, _stream()),
+          "dasa_reverse_valid")
+    return out
+
+
+def adain_musigma(content, style, out=None, eps=1e-5):
+    """adaptive_instance_normalization (model.py:1832-1840) over the last dim of [..., N] blocks."""
+    M, ldc = _rows(content)
+    _, lds = _rows(style)
+    N = content.shape[-1]
+    if out is None:
+        out = torch.empty(content.shape, dtype=torch.float32, device=content.device)
+    _, ldo = _rows(out)
+    check(_lib.lib().dasa_adain_musigma_fwd(_p(content), ldc, _p(style), lds, _p(out), ldo, None, M, N, float(eps),
+                                            _stream()), "dasa_adain_musigma_fwd")
+    return out

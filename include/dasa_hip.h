@@ -1,0 +1,167 @@
+/*
+ * dasa_hip.h — C-ABI of libdasa_hip.so, the MI355X (gfx950) kernel library behind the
+ * DASA per-step navigation policy (agent_dg rollout).
+ *
+ * Conventions (every entry point):
+ *   - pointers are device pointers to fp32 (or int32/int64/uint8 where named) owned by the caller;
+ *   - no allocation and no host synchronisation inside a call, so every call is hipGraph-capturable;
+ *   - `stream` is a hipStream_t passed as void*; work is enqueued on it;
+ *   - the return value is a hipError_t (0 == hipSuccess); shape/alignment violations return
+ *     hipErrorInvalidValue (1) before anything is launched;
+ *   - row-major storage; "ld" is the row stride in elements.
+ *
+ * Each entry point names the reference code it replaces (paths relative to the DASA repo).
+ */
+#ifndef DASA_HIP_H
+#define DASA_HIP_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- library ------------------------------------------------------------------------------- */
+int dasa_version(void);                 /* ABI version, bumped on any signature change */
+const char* dasa_build_info(void);      /* "gfx950 ..." */
+const char* dasa_error_string(int err); /* hipGetErrorString of a returned code */
+
+/* ---- GEMM (MFMA f32 32x32x2) -----------------------------------------------------------------
+ * C[b] = epilogue( alpha * opA(A[b]) @ opB(B[b]) ) (+ beta * C[b])
+ *   opA: 0 = A stored [M][K] (lda >= K), 1 = A stored [K][M] (lda >= M)
+ *   opB: 0 = B stored [K][N] (ldb >= N), 1 = B stored [N][K] (ldb >= K)   (nn.Linear weight = opB 1)
+ * Epilogue order: v = alpha*acc; v += bias[n]; v = act(v); v = v*aux[m,n] (gate); v *= colscale[n];
+ *                 v += beta*C[m,n].
+ * Replaces every nn.Linear / torch.bmm on the hot path (model.py:263-313, vilmodel.py:179-309,
+ * agent_dg.py:1519 DGAdaChannel.a_fc, r2rmodel.py:2241-2251 LSTM input projections).       */
+enum dasa_act {
+  DASA_ACT_NONE = 0, DASA_ACT_RELU = 1, DASA_ACT_GELU = 2, DASA_ACT_TANH = 3, DASA_ACT_SIGMOID = 4
+};
+typedef struct dasa_gemm_desc {
+  int32_t M, N, K, batch;
+  int32_t opA, opB;
+  const float* A; int64_t lda; int64_t strideA;
+  const float* B; int64_t ldb; int64_t strideB;
+  float* C;       int64_t ldc; int64_t strideC;
+  const float* bias;       /* [N] or NULL */
+  int32_t act;             /* enum dasa_act */
+  const float* aux;        /* gate multiplier [M][ld_aux] or NULL (DGAdaChannel: sigmoid(.)*f) */
+  int64_t ld_aux; int64_t strideAux;
+  const float* colscale;   /* [N] or NULL (shared env-drop noise, agent_dg.py:780-785) */
+  float alpha, beta;
+} dasa_gemm_desc;
+/* Workspace for split-K partials (skinny-M decoder GEMMs): bytes needed for this descriptor.
+ * Passing ws == NULL (or too small) runs the GEMM without split-K instead. */
+int64_t dasa_gemm_f32_workspace(const dasa_gemm_desc* d);
+int dasa_gemm_f32(const dasa_gemm_desc* d, void* ws, int64_t ws_bytes, void* stream);
+
+/* ---- elementwise / reductions ---------------------------------------------------------------- */
+/* y = LayerNorm(dropout_p(x) + res) over N columns (eps), optionally saving mean/rstd [M] and the
+ * pre-norm sum xsum [M][N] for backward (each may be NULL; res may be NULL).
+ * vilmodel.py:239-250, 296-309 (BertSelfOutput/BertOutput), 1067-1095 (VisionEncoder).      */
+int dasa_layernorm_fwd(const float* x, const float* res, const float* gamma, const float* beta,
+                       float* y, float* mean, float* rstd, float* xsum, int32_t M, int32_t N, float eps,
+                       float drop_p, uint64_t seed, void* stream);
+/* dx = dLN/d(xsum) (= grad of both x-after-dropout and res); dgamma/dbeta accumulated (+=). */
+int dasa_layernorm_bwd(const float* dy, const float* xsum, const float* gamma, const float* mean,
+                       const float* rstd, float* dx, float* dgamma, float* dbeta,
+                       int32_t M, int32_t N, void* stream);
+
+/* BertEmbeddings.forward (vilmodel.py:161-176): word[ids] + pos[t] + type[0] -> LN -> dropout. */
+int dasa_bert_embed_fwd(const int64_t* ids, const float* word, const float* pos, const float* type0,
+                        const float* gamma, const float* beta, float* out,
+                        int32_t B, int32_t L, int32_t H, float eps, float drop_p, uint64_t seed,
+                        void* stream);
+
+/* Masked multi-head attention core (BertSelfAttention / BertOutAttention, vilmodel.py:214-236,
+ * 481-506): ctx = softmax(Q K^T * scale + addmask[b, k]) V per head; Q/K/V/out row-major with
+ * heads interleaved as [.., heads*dh]. addmask: [B][Lk] additive (-10000 for pads) or NULL. */
+int dasa_mha_fwd(const float* Q, int64_t ldq, const float* K, int64_t ldk, const float* V, int64_t ldv,
+                 const float* addmask, float* out, int64_t ldo, float* probs,
+                 int32_t B, int32_t heads, int32_t Lq, int32_t Lk, int32_t dh, float scale,
+                 float drop_p, uint64_t seed, void* stream);
+/* Backward without attention dropout (eval-equivalent); dQ/dK/dV use the ld of Q/K/V. */
+int dasa_mha_bwd(const float* Q, int64_t ldq, const float* K, int64_t ldk, const float* V, int64_t ldv,
+                 const float* probs, const float* dout, int64_t lddo,
+                 float* dQ, float* dK, float* dV, int32_t B, int32_t heads, int32_t Lq, int32_t Lk,
+                 int32_t dh, float scale, void* stream);
+
+/* ---- SoftDot / ShiftSoftDot attention (model.py:253-353) ------------------------------------
+ * q [B][D] is linear_in(h) (computed by dasa_gemm_f32); ctx [B][N][ldn] (ldn >= D, batch stride
+ * N*ldn); mask [B][N] uint8 (1 = masked -> -inf) or NULL. Outputs any of scores [B][N] (raw
+ * logits, output_prob=False), probs [B][N], wctx [B][D].                                         */
+int dasa_softdot_fwd(const float* q, const float* ctx, int64_t ldn, const uint8_t* mask,
+                     float* scores, float* probs, float* wctx,
+                     int32_t B, int32_t N, int32_t D, void* stream);
+/* Backward. dwctx [B][D] and/or dscores [B][N] (grad of raw logits); writes dq [B][D] and
+ * dctx [B][N][ldn] (dctx += if accumulate; either may be NULL). probs are the forward's saved
+ * softmax (for output_prob=False callers pass the softmax anyway; only dscores flows then).     */
+int dasa_softdot_bwd(const float* q, const float* ctx, int64_t ldn, const float* probs,
+                     const float* dwctx, const float* dscores, float* dq, float* dctx,
+                     int32_t accumulate, int32_t B, int32_t N, int32_t D, float* ws, void* stream);
+/* ShiftSoftDotAttention (model.py:318-353): 36 views as 3 elevation rows of 12 headings;
+ * a = softmax(ctx.q); w = softmax(shift_logits) over K taps; a'[r][j] = sum_k w_k a[r][(j+k-K/2) mod 12];
+ * wctx = sum_v a'_v ctx_v. Returns attn (pre-shift a), shifted a' and w for backward. */
+int dasa_shift_attn_fwd(const float* q, const float* ctx, int64_t ldn, const float* shift_logits,
+                        float* attn, float* shifted, float* wsm, float* wctx,
+                        int32_t B, int32_t D, int32_t K, float* ws, void* stream);
+int dasa_shift_attn_bwd(const float* q, const float* ctx, int64_t ldn, const float* attn,
+                        const float* shifted, const float* wsm, const float* dwctx,
+                        float* dq, float* dctx, float* dshift_logits, int32_t accumulate,
+                        int32_t B, int32_t D, int32_t K, float* ws, void* stream);
+/* Workspace for the three calls above: B*N floats (N = 36 for the shift attention). */
+
+/* ---- LSTM (model.py:437 nn.LSTMCell, r2rmodel.py:2241 nn.LSTM) ------------------------------ */
+/* gates [B][4H] = x W_ih^T + b_ih + h W_hh^T + b_hh (PyTorch order i,f,g,o) -> h, c.
+ * act_save [B][4H] holds sigmoid/tanh-activated gates for backward (may be NULL in eval). */
+int dasa_lstm_cell_fwd(const float* gates, const float* c_prev, float* h, float* c, float* act_save,
+                       int32_t B, int32_t H, void* stream);
+int dasa_lstm_cell_bwd(const float* act_save, const float* c_prev, const float* c, const float* dh,
+                       const float* dc, float* dgates, float* dc_prev, int32_t B, int32_t H, void* stream);
+
+/* Packed bidirectional single-layer LSTM recurrence (pack_padded_sequence semantics,
+ * r2rmodel.py:2339-2343). xproj [B][L][2][4H] = x W_ih^T + b_ih + b_hh for both directions;
+ * whh [2][4H][H]; lengths [B] int32 (descending not required). Writes out [B][L][2H] ([fwd,bwd]),
+ * h_n/c_n [2][B][H], and (if save != NULL) save = {act [L][2][B][4H], c [L][2][B][H]}.
+ * ws: dasa_bilstm_workspace(B, H) bytes (ping-pong state; + recurrent gates when B > 32).        */
+int64_t dasa_bilstm_workspace(int32_t B, int32_t H);
+int dasa_bilstm_fwd(const float* xproj, const float* whh, const int32_t* lengths,
+                    float* out, float* h_n, float* c_n, float* save_act, float* save_c,
+                    int32_t B, int32_t L, int32_t H, float* ws, void* stream);
+/* BPTT: dout [B][L][2H], dh_n/dc_n [2][B][H] (may be NULL) -> dgates [B][L][2][4H] (time-major
+ * grads of the pre-activation gates; zero at padded steps). B <= 32. ws: 4*B*H floats.          */
+int dasa_bilstm_bwd(const float* whh, const int32_t* lengths, const float* save_act, const float* save_c,
+                    const float* dout, const float* dh_n, const float* dc_n, float* dgates,
+                    int32_t B, int32_t L, int32_t H, float* ws, void* stream);
+
+/* ---- AdaIN mu/sigma (model.py:1822-1840, adaIn_type default) ---------------------------------
+ * out = (c - mean_c)/std_c * std_s + mean_s per row of N channels (unbiased var + eps, sqrt). */
+int dasa_adain_musigma_fwd(const float* content, int64_t ldc_, const float* style, int64_t lds,
+                           float* out, int64_t ldo, float* stats, int32_t M, int32_t N, float eps,
+                           void* stream);
+
+/* ---- training-path elementwise ------------------------------------------------------------------
+ * DGAdaChannel with saved gate (agent_dg.py:1537-1547): out = s*f*noise[c]; backward gives the grad
+ * of the a_fc pre-activation dz = dout*f*noise*s*(1-s). noise may be NULL.                        */
+int dasa_ada_gate_fwd(const float* s, int64_t lds, const float* f, int64_t ldf, const float* noise,
+                      float* out, int64_t ldo, int32_t rows, int32_t cols, void* stream);
+int dasa_ada_gate_bwd(const float* dout, int64_t lddo, const float* s, int64_t lds, const float* f,
+                      int64_t ldf, const float* noise, float* dz, int64_t ldz, int32_t rows, int32_t cols,
+                      void* stream);
+/* dx = dy * act'(.) from the activation output (relu/tanh/sigmoid) or input (gelu); n elements. */
+int dasa_act_bwd(const float* y_or_x, const float* dy, float* dx, int64_t n, int32_t act, void* stream);
+int dasa_add2d(const float* a, int64_t lda, const float* b, int64_t ldb, float* out, int64_t ldo,
+               int32_t rows, int32_t cols, void* stream);
+int dasa_copy2d(const float* x, int64_t ldx, float* out, int64_t ldo, int32_t rows, int32_t cols,
+                void* stream);
+
+/* ---- small helpers --------------------------------------------------------------------------- */
+/* Reverse the first lengths[b] rows of x [B][L][H] into out (rest zero), r2rmodel.py:2326-2330. */
+int dasa_reverse_valid(const float* x, const int32_t* lengths, float* out, int32_t B, int32_t L,
+                       int32_t H, void* stream);
+/* y[i] = x[i] * keep(seed, i) / (1-p) for a [rows][cols] block with row stride ld (in place ok). */
+int dasa_dropout_fwd(const float* x, int64_t ldx, float* y, int64_t ldy, int32_t rows, int32_t cols,
+                     float p, uint64_t seed, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DASA_HIP_H */

@@ -1,0 +1,243 @@
+"""Kernel-level parity of libdasa_hip.so against plain fp32 math on the host."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _rand(*shape, g, scale=1.0):
+    return (torch.rand(*shape, generator=g) * 2 - 1) * scale
+
+
+@pytest.mark.parametrize("M,N,K", [(1600, 768, 768), (720, 3072, 768), (20, 4096, 2240), (1040, 2048, 2048),
+                                   (37, 45, 100), (1, 1024, 1024), (33, 1, 1024), (130, 130, 36)])
+def test_linear(dev, M, N, K):
+    from dasa_amd import ops
+    g = torch.Generator().manual_seed(M * 7 + N)
+    x = _rand(M, K, g=g)
+    W = _rand(N, K, g=g, scale=0.05)
+    b = _rand(N, g=g)
+    ref = torch.nn.functional.linear(x.double(), W.double(), b.double()).float()
+    y = ops.linear(x.to(dev), W.to(dev), b.to(dev)).cpu()
+    assert (y - ref).abs().max().item() < 1e-4 * max(1.0, ref.abs().max().item())
+
+
+@pytest.mark.parametrize("act", ["relu", "gelu", "tanh", "sigmoid"])
+def test_linear_act_and_gate(dev, act):
+    from dasa_amd import ops
+    g = torch.Generator().manual_seed(3)
+    M, N, K = 300, 260, 200
+    x, W, b = _rand(M, K, g=g), _rand(N, K, g=g, scale=0.1), _rand(N, g=g)
+    aux, cs = _rand(M, N, g=g), _rand(N, g=g)
+    z = torch.nn.functional.linear(x.double(), W.double(), b.double())
+    f = {"relu": torch.relu, "gelu": lambda t: t * 0.5 * (1 + torch.erf(t / math.sqrt(2))), "tanh": torch.tanh,
+         "sigmoid": torch.sigmoid}[act]
+    ref = (f(z) * aux.double() * cs.double()).float()
+    y = ops.linear(x.to(dev), W.to(dev), b.to(dev), act=act, aux=aux.to(dev), colscale=cs.to(dev)).cpu()
+    assert (y - ref).abs().max().item() < 1e-5
+
+
+def test_gemm_layouts(dev):
+    from dasa_amd import ops
+    g = torch.Generator().manual_seed(5)
+    A, B = _rand(70, 92, g=g), _rand(92, 52, g=g)
+    ref = (A.double() @ B.double()).float()
+    assert (ops.matmul_nn(A.to(dev), B.to(dev)).cpu() - ref).abs().max() < 1e-5
+    At = A.t().contiguous()
+    assert (ops.matmul_tn(At.to(dev), B.to(dev)).cpu() - ref).abs().max() < 1e-5
+    s = ops.colsum(B.to(dev)).cpu()
+    assert (s - B.sum(0)).abs().max() < 1e-5
+    # strided rows + beta accumulate
+    big = _rand(70, 128, g=g).to(dev)
+    C0 = _rand(70, 52, g=g)
+    out = C0.clone().to(dev)
+    ops.matmul_nn(big[:, :92], B.to(dev), out=out, beta=1.0)
+    ref2 = (big[:, :92].cpu().double() @ B.double() + C0.double()).float()
+    assert (out.cpu() - ref2).abs().max() < 1e-5
+    # the float4 operand contract: unaligned row strides are rejected, not silently mis-read
+    from dasa_amd._lib import DasaError
+    with pytest.raises(DasaError):
+        ops.matmul_nn(_rand(5, 90, g=g).to(dev), _rand(90, 8, g=g).to(dev))
+
+
+def test_layernorm_and_embed(dev):
+    from dasa_amd import ops
+    g = torch.Generator().manual_seed(7)
+    x, r = _rand(123, 768, g=g), _rand(123, 768, g=g)
+    gm, bt = _rand(768, g=g), _rand(768, g=g)
+    ref = torch.nn.functional.layer_norm(x + r, (768,), gm, bt, 1e-12)
+    y = ops.layernorm(x.to(dev), gm.to(dev), bt.to(dev), 1e-12, res=r.to(dev)).cpu()
+    assert (y - ref).abs().max() < 1e-4
+    ids = torch.randint(0, 1000, (3, 17), generator=g)
+    word, pos, typ = _rand(1000, 768, g=g), _rand(512, 768, g=g), _rand(2, 768, g=g)
+    e = word[ids] + pos[:17][None] + typ[0]
+    ref = torch.nn.functional.layer_norm(e, (768,), gm, bt, 1e-12)
+    y = ops.bert_embed(ids.to(dev), word.to(dev), pos.to(dev), typ[0].to(dev), gm.to(dev), bt.to(dev), 1e-12).cpu()
+    assert (y - ref).abs().max() < 1e-4
+
+
+@pytest.mark.parametrize("Lq,Lk", [(80, 80), (80, 36), (36, 80), (5, 100)])
+def test_mha(dev, Lq, Lk):
+    from dasa_amd import ops
+    g = torch.Generator().manual_seed(Lq + Lk)
+    B, h = 3, 12
+    Q, K, V = _rand(B, Lq, 768, g=g), _rand(B, Lk, 768, g=g), _rand(B, Lk, 768, g=g)
+    m = torch.zeros(B, Lk)
+    m[1, Lk // 2:] = -10000.0
+    q4 = Q.view(B, Lq, h, 64).permute(0, 2, 1, 3)
+    k4 = K.view(B, Lk, h, 64).permute(0, 2, 1, 3)
+    v4 = V.view(B, Lk, h, 64).permute(0, 2, 1, 3)
+    s = q4 @ k4.transpose(-1, -2) / 8.0 + m[:, None, None, :]
+    p = torch.softmax(s, -1)
+    ref = (p @ v4).permute(0, 2, 1, 3).reshape(B, Lq, 768)
+    out = ops.mha(Q.to(dev), K.to(dev), V.to(dev), m.to(dev), 12, 1 / 8.0).cpu()
+    assert (out - ref).abs().max() < 1e-5
+
+
+def test_softdot_and_shift(dev):
+    from dasa_amd import ops
+    g = torch.Generator().manual_seed(11)
+    B, N, D = 5, 36, 2176
+    q, ctx = _rand(B, D, g=g, scale=0.05), torch.rand(B, N, D, generator=g)
+    mask = torch.zeros(B, N, dtype=torch.bool)
+    mask[2, 30:] = True
+    s = torch.einsum("bnd,bd->bn", ctx, q)
+    p = torch.softmax(s.masked_fill(mask, -float("inf")), 1)
+    w = torch.einsum("bn,bnd->bd", p, ctx)
+    sc, pr, wc = ops.softdot_fwd(q.to(dev), ctx.to(dev), mask.to(dev))
+    assert (sc.cpu() - s).abs().max() < 1e-4
+    assert (pr.cpu() - p).abs().max() < 1e-5
+    assert (wc.cpu() - w).abs().max() < 1e-4
+    # shift attention against the reference's conv1d formulation (model.py:337-345)
+    z = _rand(B, 5, g=g)
+    a = torch.softmax(s, 1)
+    a3 = a.view(B, 3, 12)
+    kern = torch.softmax(z, -1).unsqueeze(1)
+    a3 = torch.cat([a3[:, :, -2:], a3, a3[:, :, :2]], -1).transpose(0, 1)
+    a3 = torch.nn.functional.conv1d(a3, kern, groups=B).transpose(0, 1).reshape(B, 1, -1)
+    wref = torch.bmm(a3, ctx).squeeze(1)
+    wctx, attn, shifted, wsm = ops.shift_attn_fwd(q.to(dev), ctx.to(dev), z.to(dev))
+    assert (attn.cpu() - a).abs().max() < 1e-5
+    assert (wctx.cpu() - wref).abs().max() < 1e-4
+
+
+def test_softdot_shift_backward(dev):
+    from dasa_amd import ops
+    g = torch.Generator().manual_seed(13)
+    B, N, D = 4, 36, 2176
+    q = (_rand(B, D, g=g, scale=0.05)).requires_grad_()
+    ctx = torch.rand(B, N, D, generator=g).requires_grad_()
+    z = _rand(B, 5, g=g).requires_grad_()
+    gw = _rand(B, D, g=g)
+    s = torch.einsum("bnd,bd->bn", ctx, q)
+    a = torch.softmax(s, 1)
+    a3 = a.view(B, 3, 12)
+    kern = torch.softmax(z, -1).unsqueeze(1)
+    a3 = torch.cat([a3[:, :, -2:], a3, a3[:, :, :2]], -1).transpose(0, 1)
+    a3 = torch.nn.functional.conv1d(a3, kern, groups=B).transpose(0, 1).reshape(B, 1, -1)
+    wref = torch.bmm(a3, ctx).squeeze(1)
+    (wref * gw).sum().backward()
+    qd, cd, zd = q.detach().to(dev), ctx.detach().to(dev), z.detach().to(dev)
+    wctx, attn, shifted, wsm = ops.shift_attn_fwd(qd, cd, zd)
+    dq, dctx, dz = ops.shift_attn_bwd(qd, cd, attn, shifted, wsm, gw.to(dev))
+    assert (dq.cpu() - q.grad).abs().max() < 1e-4 * max(1, q.grad.abs().max())
+    assert (dctx.cpu() - ctx.grad).abs().max() < 1e-5
+    assert (dz.cpu() - z.grad).abs().max() < 1e-4 * max(1, z.grad.abs().max())
+    # softdot with mask: wctx grad + raw-score grad
+    mask = torch.zeros(B, N, dtype=torch.bool)
+    mask[1, 20:] = True
+    q2 = q.detach().clone().requires_grad_()
+    c2 = ctx.detach().clone().requires_grad_()
+    gs = _rand(B, N, g=g)
+    s = torch.einsum("bnd,bd->bn", c2, q2)
+    p = torch.softmax(s.masked_fill(mask, -float("inf")), 1)
+    w = torch.einsum("bn,bnd->bd", p, c2)
+    ((w * gw).sum() + (s * gs).sum()).backward()
+    _, pr, _ = ops.softdot_fwd(q2.detach().to(dev), c2.detach().to(dev), mask.to(dev))
+    dq, dctx = ops.softdot_bwd(q2.detach().to(dev), c2.detach().to(dev), pr, dwctx=gw.to(dev), dscores=gs.to(dev))
+    assert (dq.cpu() - q2.grad).abs().max() < 1e-4 * max(1, q2.grad.abs().max())
+    assert (dctx.cpu() - c2.grad).abs().max() < 1e-5 * max(1, c2.grad.abs().max())
+
+
+def test_lstm_cell(dev):
+    from dasa_amd import ops
+    g = torch.Generator().manual_seed(17)
+    B, H = 7, 1024
+    gates = _rand(B, 4 * H, g=g, scale=2).requires_grad_()
+    c0 = _rand(B, H, g=g).requires_grad_()
+    i, f, gg, o = gates.chunk(4, 1)
+    c1 = torch.sigmoid(f) * c0 + torch.sigmoid(i) * torch.tanh(gg)
+    h1 = torch.sigmoid(o) * torch.tanh(c1)
+    gh, gc = _rand(B, H, g=g), _rand(B, H, g=g)
+    ((h1 * gh).sum() + (c1 * gc).sum()).backward()
+    h, c, act = ops.lstm_cell_fwd(gates.detach().to(dev), c0.detach().to(dev), save=True)
+    assert (h.cpu() - h1).abs().max() < 1e-6 and (c.cpu() - c1).abs().max() < 1e-6
+    dg, dc0 = ops.lstm_cell_bwd(act, c0.detach().to(dev), c, gh.to(dev), gc.to(dev))
+    assert (dg.cpu() - gates.grad).abs().max() < 1e-5 and (dc0.cpu() - c0.grad).abs().max() < 1e-5
+
+
+@pytest.mark.parametrize("B,L", [(20, 80), (3, 11), (40, 9)])
+def test_bilstm(dev, B, L):
+    from dasa_amd import ops
+    torch.manual_seed(B + L)
+    H, E = 1024, 768
+    lstm = torch.nn.LSTM(E, H, 1, batch_first=True, bidirectional=True)
+    with torch.no_grad():
+        for p_ in lstm.parameters():
+            p_.uniform_(-0.05, 0.05)
+    lengths = torch.randint(1, L + 1, (B,))
+    lengths[0] = L
+    lengths, _ = lengths.sort(descending=True)
+    x = torch.randn(B, L, E) * 0.5
+    packed = torch.nn.utils.rnn.pack_padded_sequence(x, lengths.tolist(), batch_first=True)
+    out_p, (hn, cn) = lstm(packed)
+    out_ref, _ = torch.nn.utils.rnn.pad_packed_sequence(out_p, batch_first=True, total_length=L)
+    gout = torch.randn(B, L, 2 * H)
+    ghn, gcn = torch.randn(2, B, H), torch.randn(2, B, H)
+    ((out_ref * gout).sum() + (hn * ghn).sum() + (cn * gcn).sum()).backward()
+    Wih = torch.cat([lstm.weight_ih_l0, lstm.weight_ih_l0_reverse], 0).detach()
+    bias = torch.cat([lstm.bias_ih_l0 + lstm.bias_hh_l0, lstm.bias_ih_l0_reverse + lstm.bias_hh_l0_reverse]).detach()
+    whh = torch.stack([lstm.weight_hh_l0, lstm.weight_hh_l0_reverse]).detach().contiguous()
+    xd = x.to(dev)
+    xproj = ops.linear(xd.view(B * L, E), Wih.to(dev), bias.to(dev)).view(B, L, 2, 4 * H)
+    li = lengths.to(torch.int32).to(dev)
+    out, h_n, c_n, saved = ops.bilstm_fwd(xproj, whh.to(dev), li, H, save=(B <= 32))
+    assert (out.cpu() - out_ref).abs().max() < 2e-5
+    assert (h_n.cpu() - hn).abs().max() < 2e-5 and (c_n.cpu() - cn).abs().max() < 2e-5
+    if B <= 32:
+        dg = ops.bilstm_bwd(whh.to(dev), li, saved, gout.to(dev), ghn.to(dev), gcn.to(dev), H)
+        # weight grads from dgates: dW_hh[dir] = sum_t dg^T h_prev
+        dgc = dg.cpu()
+        dWih = torch.einsum("blg,ble->ge", dgc[:, :, 0], x)
+        assert (dWih - lstm.weight_ih_l0.grad).abs().max() < 1e-3 * max(1, lstm.weight_ih_l0.grad.abs().max())
+        dWih_r = torch.einsum("blg,ble->ge", dgc[:, :, 1], x)
+        assert (dWih_r - lstm.weight_ih_l0_reverse.grad).abs().max() < 1e-3 * max(1, lstm.weight_ih_l0_reverse.grad.abs().max())
+        db = dgc[:, :, 0].sum((0, 1))
+        assert (db - lstm.bias_ih_l0.grad).abs().max() < 1e-3 * max(1, lstm.bias_ih_l0.grad.abs().max())
+
+
+def test_adain_musigma_reverse_dropout(dev):
+    from dasa_amd import ops
+    g = torch.Generator().manual_seed(19)
+    c, s = torch.rand(2, 44, 2048, generator=g), torch.rand(2, 44, 2048, generator=g)
+
+    def ms(x):
+        return x.mean(-1, keepdim=True), (x.var(-1, keepdim=True) + 1e-5).sqrt()
+    mc, sc = ms(c)
+    mss, sss = ms(s)
+    ref = (c - mc) / sc * sss + mss
+    out = ops.adain_musigma(c.to(dev), s.to(dev)).cpu()
+    assert (out - ref).abs().max() < 1e-4
+    x = torch.rand(3, 7, 16, generator=g)
+    lens = torch.tensor([7, 4, 1], dtype=torch.int32)
+    r = ops.reverse_valid(x.to(dev), lens.to(dev)).cpu()
+    for b in range(3):
+        n = int(lens[b])
+        assert torch.equal(r[b, :n], x[b, :n].flip(0)) and (r[b, n:] == 0).all()
+    y = ops.dropout(torch.ones(100, 1000, device=dev), 0.4, 1234).cpu()
+    keep = (y > 0).float().mean().item()
+    assert abs(keep - 0.6) < 0.01 and torch.allclose(y[y > 0], torch.full_like(y[y > 0], 1 / 0.6))
+    y2 = ops.dropout(torch.ones(100, 1000, device=dev), 0.4, 1234).cpu()
+    assert torch.equal(y, y2)
