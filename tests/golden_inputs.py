@@ -1,0 +1,88 @@
+"""Seeded inputs shared by oracle/golden/make_golden.py (which ran the reference on them) and the
+tests (which re-create them). Fixtures store only outputs; inputs and weights regenerate from seeds.
+"""
+import numpy as np
+import torch
+
+# weight seeds per reference module (agent_dg.py:161-200)
+SEED_ENC, SEED_DEC, SEED_CRITIC, SEED_ADA = 1, 2, 3, 4
+CFG1 = dict(batch=2, vl_layers=1, la_layers=9, max_action=5, instr_len=80, kernel=5)
+
+
+def _u(rng, *shape):
+    return torch.from_numpy(rng.random(shape, dtype=np.float32))
+
+
+def _n(rng, *shape, scale=1.0):
+    return torch.from_numpy((rng.standard_normal(shape, dtype=np.float32) * scale).astype(np.float32))
+
+
+def ada_inputs():
+    rng = np.random.default_rng(100)
+    return _u(rng, 2, 10, 2048), _u(rng, 2, 10, 2048), _n(rng, 2, 10, 2048)
+
+
+def adain_inputs():
+    rng = np.random.default_rng(101)
+    return _u(rng, 2, 10, 2048), _u(rng, 2, 10, 2048)
+
+
+def shift_inputs(K):
+    rng = np.random.default_rng(102 + K)
+    return _n(rng, 3, 1024, scale=0.5), _u(rng, 3, 36, 2176), _n(rng, 3, 2176)
+
+
+def softdot_inputs():
+    rng = np.random.default_rng(110)
+    h = _n(rng, 3, 1024, scale=0.5)
+    ctx = _n(rng, 3, 12, 2048)
+    mask = torch.zeros(3, 12, dtype=torch.bool)
+    mask[1, 7:] = True
+    mask[2, 3:] = True
+    cand = _u(rng, 3, 6, 2176)
+    return h, ctx, mask, cand, _n(rng, 3, 1024), _n(rng, 3, 6)
+
+
+def decoder_inputs():
+    rng = np.random.default_rng(120)
+    B = 3
+    action = _n(rng, B, 128)
+    feature = _u(rng, B, 36, 2176)
+    cand = _u(rng, B, 6, 2176)
+    h0 = _n(rng, B, 1024, scale=0.3)
+    prev_h1 = torch.tanh(_n(rng, B, 1024))
+    c0 = _n(rng, B, 1024, scale=0.3)
+    ctx = _n(rng, B, 12, 2048, scale=0.2)
+    mask = torch.zeros(B, 12, dtype=torch.bool)
+    mask[2, 9:] = True
+    return action, feature, cand, h0, prev_h1, c0, ctx, mask
+
+
+def critic_inputs():
+    rng = np.random.default_rng(130)
+    return _n(rng, 4, 1024)
+
+
+def lxrt_inputs():
+    rng = np.random.default_rng(140)
+    lang = _n(rng, 2, 12, 768)
+    visn = _n(rng, 2, 36, 768)
+    lang_mask = torch.zeros(2, 12)
+    lang_mask[1, 8:] = -10000.0
+    return lang, lang_mask, visn, torch.zeros(2, 36)
+
+
+def encoder_inputs():
+    """DicEncoder at B=3, L=12, lengths 12/9/5 (sorted descending like _sort_batch)."""
+    rng = np.random.default_rng(150)
+    B, L = 3, 12
+    lengths = [12, 9, 5]
+    seq = np.zeros((B, L), dtype=np.int64)
+    for i, n in enumerate(lengths):
+        seq[i, 0] = 101
+        seq[i, 1:n - 1] = rng.integers(1000, 30000, size=n - 2)
+        seq[i, n - 1] = 102
+    seq = torch.from_numpy(seq)
+    mask = seq == 0
+    f = _u(rng, B, 36, 2176)
+    return seq, mask, lengths, f

@@ -1,0 +1,174 @@
+"""CPU: the oracle (oracle/policy.py) reproduces the reference's outputs recorded in tests/golden.
+
+These pin the oracle; GPU tests then compare the HIP path with the oracle (and the goldens)."""
+import numpy as np
+import pytest
+import torch
+
+from dasa_amd.synth import SynthR2RBatch, SynthWorld, init_param_dict
+from oracle import policy as O
+from oracle import schema as S
+from tests import golden_inputs as GI
+from tests.helpers import check_grads, close, golden, oracle_weights, schema_from_golden
+
+
+def test_schema_matches_reference():
+    assert S.encoder_schema(1, 9) == schema_from_golden("encoder")
+    assert S.decoder_schema() == schema_from_golden("decoder")
+    assert S.critic_schema() == schema_from_golden("critic")
+    assert S.ada_schema() == schema_from_golden("adaIn")
+
+
+def test_ada_channel_and_adain():
+    G = golden("ops")
+    P = init_param_dict(S.ada_schema(), GI.SEED_ADA)
+    for v in P.values():
+        v.requires_grad_(True)
+    f, d, g = GI.ada_inputs()
+    y = O.dg_ada_channel(f, d, P["a_fc.weight"], P["a_fc.bias"])
+    close(y, G["ada/out"], 1e-6, "ada")
+    (y * g).sum().backward()
+    assert check_grads(G, "ada/", [(k, v.grad) for k, v in P.items()]) == 2
+    c, s = GI.adain_inputs()
+    close(O.adaptive_instance_normalization(c, s), G["adain/out"], 1e-5, "adain")
+
+
+@pytest.mark.parametrize("K", [5, 3])
+def test_shift_attention(K):
+    G = golden("ops")
+    P = init_param_dict({"linear_in.weight": (2176, 1024), "linear_out.weight": (1024, 3200),
+                         "linear_shift.weight": (K, 1024), "linear_shift.bias": (K,)}, 20 + K)
+    for v in P.values():
+        v.requires_grad_(True)
+    h, ctx, gw = GI.shift_inputs(K)
+    h.requires_grad_(True)
+    ctx.requires_grad_(True)
+    wctx, attn = O.shift_softdot(h, ctx, P["linear_in.weight"], P["linear_shift.weight"], P["linear_shift.bias"], K)
+    close(wctx, G[f"shift{K}/wctx"], 1e-5, "wctx")
+    close(attn, G[f"shift{K}/attn"], 1e-6, "attn")
+    (wctx * gw).sum().backward()
+    close(h.grad, G[f"shift{K}/dh"], 1e-4, "dh")
+    n = check_grads(G, f"shift{K}/", [("ctx", ctx.grad)] + [(k, v.grad) for k, v in P.items()])
+    assert n >= 3
+
+
+def test_softdot_and_candidate():
+    G = golden("ops")
+    h, ctx, mask, cand, g1, g2 = GI.softdot_inputs()
+    P = init_param_dict({"linear_in.weight": (2048, 1024), "linear_out.weight": (1024, 3072)}, 30)
+    for v in P.values():
+        v.requires_grad_(True)
+    h1 = h.clone().requires_grad_(True)
+    ht, alpha = O.softdot(h1, ctx, P["linear_in.weight"], P["linear_out.weight"], mask=mask)
+    close(ht, G["softdot/h_tilde"], 1e-6, "h_tilde")
+    close(alpha, G["softdot/alpha"], 1e-6, "alpha")
+    (ht * g1).sum().backward()
+    close(h1.grad, G["softdot/dh"], 1e-5, "dh")
+    assert check_grads(G, "softdot/", [(k, v.grad) for k, v in P.items()]) == 2
+    Pc = init_param_dict({"linear_in.weight": (2176, 1024), "linear_out.weight": (1024, 3200)}, 31)
+    Pc["linear_in.weight"].requires_grad_(True)
+    h2 = h.clone().requires_grad_(True)
+    cand = cand.clone().requires_grad_(True)
+    _, logit = O.softdot(h2, cand, Pc["linear_in.weight"], output_tilde=False, output_prob=False)
+    close(logit, G["cand/logit"], 1e-5, "logit")
+    (logit * g2).sum().backward()
+    close(h2.grad, G["cand/dh"], 1e-5, "cand dh")
+    check_grads(G, "cand/", [("cand", cand.grad), ("linear_in.weight", Pc["linear_in.weight"].grad)])
+
+
+def test_decoder_step_and_critic():
+    G = golden("ops")
+    P = init_param_dict(S.decoder_schema(), GI.SEED_DEC)
+    for v in P.values():
+        v.requires_grad_(True)
+    action, feature, cand, h0, prev_h1, c0, ctx, mask = GI.decoder_inputs()
+    h1, c1, logit, ht = O.decoder_step(P, action, feature, cand, prev_h1, c0, ctx, mask)
+    for k, v in dict(h1=h1, c1=c1, logit=logit, h_tilde=ht).items():
+        close(v, G["dec/" + k], 2e-5, k)
+    rng = np.random.default_rng(121)
+    w = [torch.from_numpy(rng.standard_normal(t.shape).astype(np.float32)) for t in (h1, c1, logit, ht)]
+    ((h1 * w[0]).sum() + (c1 * w[1]).sum() + (logit * w[2]).sum() + (ht * w[3]).sum()).backward()
+    assert check_grads(G, "dec/", [(k, v.grad) for k, v in P.items() if v.grad is not None]) >= 10
+    C = init_param_dict(S.critic_schema(), GI.SEED_CRITIC)
+    for v in C.values():
+        v.requires_grad_(True)
+    val = O.critic(C, GI.critic_inputs())
+    close(val, G["critic/value"], 1e-6, "critic")
+    (val * torch.arange(1.0, 5.0)).sum().backward()
+    assert check_grads(G, "critic/", [(k, v.grad) for k, v in C.items()]) == 4
+
+
+def test_lxrt_layer():
+    G = golden("ops")
+    sch = {k[len("bert.addlayer.0."):]: v for k, v in S.encoder_schema(1, 0).items() if k.startswith("bert.addlayer.0.")}
+    P = init_param_dict(sch, 40)
+    P = {"x." + k: v for k, v in P.items()}
+    lang, lmask, visn, vmask = GI.lxrt_inputs()
+    lo, vo = O.lxrt_layer(P, "x", lang, lmask, visn, vmask)
+    close(lo, G["lxrt/lang"], 2e-5, "lang")
+    close(vo, G["lxrt/visn"], 2e-5, "visn")
+
+
+def test_dic_encoder():
+    G = golden("ops")
+    P = init_param_dict(S.encoder_schema(1, 9), GI.SEED_ENC)
+    for k, v in P.items():
+        v.requires_grad_(True)
+    seq, mask, lengths, f = GI.encoder_inputs()
+    ctx, dinit, ct, _, vis = O.dic_encoder(P, seq, mask, lengths, f, la_layers=9, vl_layers=1)
+    close(ctx, G["enc/ctx"], 2e-5, "ctx")
+    close(dinit, G["enc/decoder_init"], 2e-5, "decoder_init")
+    close(ct, G["enc/c_t"], 2e-5, "c_t")
+    close(vis, G["enc/vision"], 2e-5, "vision")
+    rng = np.random.default_rng(151)
+    w = [torch.from_numpy(rng.standard_normal(t.shape).astype(np.float32)) for t in (ctx, dinit, ct)]
+    ((ctx * w[0]).sum() + (dinit * w[1]).sum() + (ct * w[2]).sum()).backward()
+    assert check_grads(G, "enc/", [(k, v.grad) for k, v in P.items() if v.grad is not None]) == 12
+
+
+def test_rollout_eval_argmax():
+    G = golden("cfg1_rollout")
+    cfg = GI.CFG1
+    W = oracle_weights(cfg["vl_layers"])
+    env = SynthR2RBatch(SynthWorld(16, 0, 3), cfg["batch"], seed=7, mode="goal", instr_len=cfg["instr_len"],
+                        variable_len=True)
+    with torch.no_grad():
+        r = O.vl_rollout(W, env, "argmax", la_layers=9, vl_layers=cfg["vl_layers"], episode_len=cfg["max_action"])
+    assert r["steps"] == int(G["eval/steps"])
+    for t in range(r["steps"]):
+        close(r["logits"][t], G[f"eval/logit/{t}"], 5e-5, f"logit{t}")
+        h, c, ht = r["states"][t]
+        close(h, G[f"eval/h1/{t}"], 2e-5, f"h{t}")
+        close(c, G[f"eval/c1/{t}"], 2e-5, f"c{t}")
+        close(ht, G[f"eval/h_tilde/{t}"], 2e-5, f"h_tilde{t}")
+    assert abs(float(r["ml_loss"]) - float(G["eval/ml_loss"])) < 1e-4
+    paths = ["|".join(p) for p in r["traj"]]
+    assert paths == list(G["eval/paths"])
+
+
+def test_rollout_train_grads():
+    """accumulate_gradient('sample') with dropout 0 and argmax 'sampling' (agent_dg.py:1347-1372)."""
+    G = golden("cfg1_rollout")
+    cfg = GI.CFG1
+    saved = dict(O.DROP)
+    O.DROP.update(dec=0.0, feat=0.0, enc=0.0, bert=0.0)
+    try:
+        W = oracle_weights(cfg["vl_layers"], requires_grad=True)
+        env = SynthR2RBatch(SynthWorld(16, 0, 3), cfg["batch"], seed=8, mode="goal", instr_len=cfg["instr_len"],
+                            variable_len=True)
+        kw = dict(la_layers=9, vl_layers=cfg["vl_layers"], episode_len=cfg["max_action"], train=True)
+        r1 = O.vl_rollout(W, env, "teacher", train_ml=0.4, **kw)
+        r2 = O.vl_rollout(W, env, "sample", train_ml=None, train_rl=True, sample_fn=lambda p: p.argmax(-1), **kw)
+    finally:
+        O.DROP.update(saved)
+    loss = r1["loss"] + r2["loss"]
+    assert abs(loss.item() - float(G["train/loss"])) < 2e-5 * max(1, abs(float(G["train/loss"])))
+    assert abs(r1["ml_loss"].item() - float(G["train/ml_loss_teacher"])) < 1e-4
+    assert abs(r2["ml_loss"].item() - float(G["train/ml_loss_sample"])) < 1e-4
+    assert abs(r2["rl_loss"].item() - float(G["train/rl_loss"])) < 1e-5
+    assert r1["steps"] == int(G["train/steps_teacher"]) and r2["steps"] == int(G["train/steps_sample"])
+    loss.backward()
+    n = 0
+    for name, d in (("encoder", W.enc), ("decoder", W.dec), ("critic", W.critic), ("adaIn", W.ada)):
+        n += check_grads(G, f"train/{name}.", [(k, v.grad) for k, v in d.items()], rtol=1e-3)
+    assert n == 30
