@@ -1,0 +1,201 @@
+"""DASA agent_dg policy benchmark on MI355X (BASELINE.json metric: agent decision-steps/sec at B=20,
+36x2048 feats, maxAction=35).
+
+One "step" = one training iteration of the README auglistener loop on the GT env
+(agent_dg.py:1347-1372, 1389-1405): a teacher-forced rollout + a sampled A2C rollout, both through
+AdaIN -> DicEncoder (9 language + 3 LXRT layers + bi-LSTM) -> decoder every step, then backward,
+data-parallel gradient all-reduce (RCCL), clip and RMSprop. Episodes are synthetic 'wander' episodes
+(the teacher never stops, so the teacher rollout always runs maxAction steps); the sampled rollout
+stops when the policy says so, exactly as the reference. value = decisions / s where decisions =
+sum over rollouts of (batched steps x B), summed over all ranks.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 20] [--max-action 35] [--vl 3]
+    torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU, RCCL)
+"""
+import argparse
+import contextlib
+import io
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP32_MFMA_PEAK_TF = 157.3      # MI355X_MICROARCH.md: peak FP32 matrix (= vector) rate
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E peak (spec)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--batch", type=int, default=20)
+    p.add_argument("--max-action", type=int, default=35)
+    p.add_argument("--vl", type=int, default=3)
+    p.add_argument("--viewpoints", type=int, default=64)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-fwd", action="store_true")
+    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--profile-kernels", action="store_true", default=True)
+    return p.parse_args()
+
+
+def setup_dist(a):
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return rank, world
+
+
+def build_agent(a, rank, world):
+    from dasa_amd.r2r import param
+    param.readme_train(["--d_vl_layers", str(a.vl), "--batchSize", str(a.batch), "--maxAction", str(a.max_action)])
+    param.args.ml_weight = param.args.ml_weight_org     # train.py:233 (GT env)
+    from dasa_amd import dp
+    from dasa_amd.r2r.agent_dg import Seq2SeqAgent
+    from dasa_amd.synth import SynthR2RBatch, SynthWorld, init_params
+    world_obj = SynthWorld(a.viewpoints, feat_seed=0, graph_seed=3)
+    env = SynthR2RBatch(world_obj, a.batch, seed=1000 + rank, mode="wander", instr_len=80, lazy_features=True)
+    with contextlib.redirect_stdout(io.StringIO()):
+        agent = Seq2SeqAgent(env, "", None, a.max_action, "Dic")
+    for m, s in ((agent.encoder, 1), (agent.decoder, 2), (agent.critic, 3), (agent.adaIn, 4)):
+        init_params(m, s)        # random-init weights of the reference architecture (seeded)
+    if world > 1:
+        dp.attach(agent)         # broadcast from rank 0 + flat-bucket RCCL all-reduce in optim_step
+    return agent, env
+
+
+def train_step(agent):
+    agent.zero_grad()
+    agent.accumulate_gradient("sample")
+    n = agent.logs["viewsteps/teacher"][-1] + agent.logs["viewsteps/sample"][-1]
+    agent.optim_step()
+    return n * agent.env.batch_size
+
+
+def fwd_rollout(agent):
+    agent.feedback = "argmax"
+    for m in (agent.encoder, agent.decoder, agent.critic):
+        m.eval()
+    agent.loss = 0
+    with torch.no_grad():
+        agent.vl_rollout(train_ml=None, train_rl=False, reset=True)
+    return agent.last_rollout_steps * agent.env.batch_size
+
+
+def timed(fn, n, rank, world):
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    units = 0
+    for _ in range(n):
+        units += fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        u = torch.tensor([float(units)], device="cuda", dtype=torch.float64)
+        dist.all_reduce(u)
+        units = float(u.item())
+    return units, dt
+
+
+def kernel_profile(agent, fn):
+    """One extra (untimed) step with HIP events around every libdasa_hip launch on its stream:
+    per-kernel-family device time + algorithmic FLOPs/bytes for the roofline."""
+    from dasa_amd import prof
+    with prof.collect() as rec:
+        fn()
+    return rec.summary()
+
+
+def cpu_baseline(a):
+    """The CPU oracle (oracle/policy.py, the reference math restated in PyTorch-CPU fp32) on a bounded
+    sample of the same workload: one training iteration (teacher + sampled rollout, backward) at
+    B=20, vl=3, L=80 with maxAction=2, on the host's cores."""
+    from oracle import policy as O
+    from tests.helpers import oracle_weights
+    from dasa_amd.synth import SynthR2RBatch, SynthWorld
+    threads = max(1, min(a.cpu_threads, os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    W = oracle_weights(a.vl, requires_grad=True)
+    for d in (W.enc,):   # BERT stack is detached in the train config: no grads there
+        for k, v in d.items():
+            if k.startswith("bert."):
+                v.requires_grad_(False)
+    env = SynthR2RBatch(SynthWorld(a.viewpoints, 0, 3), a.batch, seed=1000, mode="wander", instr_len=80)
+    T = 2
+    t0 = time.perf_counter()
+    r1 = O.vl_rollout(W, env, "teacher", la_layers=9, vl_layers=a.vl, episode_len=T, train=True, train_ml=0.4)
+    r2 = O.vl_rollout(W, env, "sample", la_layers=9, vl_layers=a.vl, episode_len=T, train=True, train_rl=True)
+    (r1["loss"] + r2["loss"]).backward()
+    dt = time.perf_counter() - t0
+    dec = (r1["steps"] + r2["steps"]) * a.batch
+    return {"value": dec / dt, "unit": "agent-decisions/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/policy.py train iteration (teacher+sample rollouts, backward), B={a.batch}, "
+                      f"vl={a.vl}, L=80, maxAction={T} ({dec} decisions in {dt:.1f}s, {threads} threads, "
+                      f"{platform.processor() or platform.machine()})"}
+
+
+def main():
+    a = parse()
+    rank, world = setup_dist(a)
+    torch.manual_seed(1 + rank)
+    from dasa_amd import functional as DF
+    DF.reseed(1234 + rank)
+    agent, env = build_agent(a, rank, world)
+    for _ in range(a.warmup):
+        train_step(agent)
+    units, dt = timed(lambda: train_step(agent), a.steps, rank, world)
+    value = units / dt
+    out = {
+        "metric": "agent decision-steps/sec at B=20, 36x2048 feats, maxAction=35; 1/2/4/8 MI355X",
+        "value": round(value, 2), "unit": "agent-decisions/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(1000 * dt / a.steps, 2), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+        "config": {"workload": "cfg2 auglistener training iteration (teacher + sample rollout, backward, "
+                               "grad all-reduce, RMSprop), README flags",
+                   "global_batch": a.batch * world, "per_rank_batch": a.batch, "max_action": a.max_action,
+                   "instr_len": 80, "vl_layers": a.vl, "la_layers": 9, "parallelism": f"dp{world}"},
+    }
+    if not a.no_fwd:
+        fwd_rollout(agent)
+        fu, fdt = timed(lambda: fwd_rollout(agent), 2, rank, world)
+        out["fwd_value"] = round(fu / fdt, 2)
+        out["fwd_note"] = "eval/argmax rollout decisions/s (language stack computed once per batch: exact in eval)"
+    if a.profile_kernels:
+        summ = kernel_profile(agent, lambda: train_step(agent))
+        if rank == 0:
+            out.update(summ)
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(a)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -46,7 +46,8 @@ SIGNATURES = {
     "dasa_layernorm_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp]),
     "dasa_bert_embed_fwd": (i32, [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, f32, f32, u64, vp]),
     "dasa_mha_fwd": (i32, [vp, i64, vp, i64, vp, i64, vp, vp, i64, vp, i32, i32, i32, i32, i32, f32, f32, u64, vp]),
-    "dasa_mha_bwd": (i32, [vp, i64, vp, i64, vp, i64, vp, vp, i64, vp, vp, vp, i32, i32, i32, i32, i32, f32, vp]),
+    "dasa_mha_bwd": (i32, [vp, i64, vp, i64, vp, i64, vp, vp, i64, vp, vp, vp, i32, i32, i32, i32, i32, f32, f32, u64,
+                           vp]),
     "dasa_softdot_fwd": (i32, [vp, vp, i64, vp, vp, vp, vp, i32, i32, i32, vp]),
     "dasa_softdot_bwd": (i32, [vp, vp, i64, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp, vp]),
     "dasa_shift_attn_fwd": (i32, [vp, vp, i64, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp]),
@@ -54,16 +55,20 @@ SIGNATURES = {
     "dasa_lstm_cell_fwd": (i32, [vp, vp, vp, vp, vp, i32, i32, vp]),
     "dasa_lstm_cell_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, i32, i32, vp]),
     "dasa_bilstm_workspace": (i64, [i32, i32]),
-    "dasa_bilstm_fwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp]),
-    "dasa_bilstm_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp]),
+    "dasa_bilstm_fwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp]),
+    "dasa_bilstm_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp]),
+    "dasa_bilstm_hprev": (i32, [vp, vp, i32, i32, i32, vp]),
     "dasa_adain_musigma_fwd": (i32, [vp, i64, vp, i64, vp, i64, vp, i32, i32, f32, vp]),
     "dasa_reverse_valid": (i32, [vp, vp, vp, i32, i32, i32, vp]),
     "dasa_dropout_fwd": (i32, [vp, i64, vp, i64, i32, i32, f32, u64, vp]),
     "dasa_ada_gate_fwd": (i32, [vp, i64, vp, i64, vp, vp, i64, i32, i32, vp]),
     "dasa_ada_gate_bwd": (i32, [vp, i64, vp, i64, vp, i64, vp, vp, i64, i32, i32, vp]),
     "dasa_act_bwd": (i32, [vp, vp, vp, i64, i32, vp]),
+    "dasa_act_fwd": (i32, [vp, vp, i64, i32, vp]),
     "dasa_add2d": (i32, [vp, i64, vp, i64, vp, i64, i32, i32, vp]),
     "dasa_copy2d": (i32, [vp, i64, vp, i64, i32, i32, vp]),
+    "dasa_colscale": (i32, [vp, i64, vp, vp, i64, i32, i32, vp]),
+    "dasa_gather_rows": (i32, [vp, vp, i32, vp, vp, i32, vp, i32, vp]),
 }
 
 _LIB = None

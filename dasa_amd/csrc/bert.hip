@@ -298,11 +298,16 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(MhaArgs a, const float* dO
     const long prow = (((long)b * a.heads + h) * a.Lq + i) * Lk;
     float p0 = lane < Lk ? a.probs[prow + lane] : 0.f;
     float p1 = lane + 64 < Lk ? a.probs[prow + lane + 64] : 0.f;
+    // attention-probs dropout (train mode): the same counter-RNG mask as the forward
+    const float k0 = a.p > 0.f ? dasa_dropout_scale(a.p, a.seed, (uint64_t)prow + lane) : 1.f;
+    const float k1 = a.p > 0.f ? dasa_dropout_scale(a.p, a.seed, (uint64_t)prow + lane + 64) : 1.f;
     float dp0 = 0.f, dp1 = 0.f;
     if (lane < Lk)
       for (int d = 0; d < kDh; ++d) dp0 = fmaf(dos[w][d], Vs[lane][d], dp0);
     if (lane + 64 < Lk)
       for (int d = 0; d < kDh; ++d) dp1 = fmaf(dos[w][d], Vs[lane + 64][d], dp1);
+    dp0 *= k0;
+    dp1 *= k1;
     const float dot = wave_sum(p0 * dp0 + p1 * dp1);
     const float ds0 = p0 * (dp0 - dot) * a.scale, ds1 = p1 * (dp1 - dot) * a.scale;
     dss[w][lane] = ds0;
@@ -312,8 +317,9 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(MhaArgs a, const float* dO
     for (int j = 0; j < Lk; ++j) dq = fmaf(dss[w][j], Ks[j][lane], dq);
     dQ[((long)b * a.Lq + i) * a.ldq + h * kDh + lane] = dq;
     // dK[j][d] += ds_j * q[d]; dV[j][d] += p_j * dO[d]  (lane = d)
+    const float pd0 = p0 * k0, pd1 = p1 * k1;   // dropped probs feed dV
     for (int j = 0; j < Lk; ++j) {
-      const float pj = j < 64 ? __shfl(p0, j, 64) : __shfl(p1, j - 64, 64);
+      const float pj = j < 64 ? __shfl(pd0, j, 64) : __shfl(pd1, j - 64, 64);
       atomicAdd(&dKs[j][lane], dss[w][j] * qs[w][lane]);
       atomicAdd(&dVs[j][lane], pj * dos[w][lane]);
     }
@@ -445,10 +451,12 @@ extern "C" int dasa_mha_fwd(const float* Q, int64_t ldq, const float* K, int64_t
 
 extern "C" int dasa_mha_bwd(const float* Q, int64_t ldq, const float* K, int64_t ldk, const float* V, int64_t ldv,
                             const float* probs, const float* dout, int64_t lddo, float* dQ, float* dK, float* dV,
-                            int32_t B, int32_t heads, int32_t Lq, int32_t Lk, int32_t dh, float scale, void* stream) {
+                            int32_t B, int32_t heads, int32_t Lq, int32_t Lk, int32_t dh, float scale, float drop_p,
+                            uint64_t seed, void* stream) {
   if (B <= 0 || Lq <= 0) return 0;
   if (dh != kDh || Lk <= 0 || Lk > kMaxLk || !probs) return (int)hipErrorInvalidValue;
-  MhaArgs a{Q, ldq, K, ldk, V, ldv, nullptr, nullptr, 0, const_cast<float*>(probs), B, heads, Lq, Lk, scale, 0.f, 0};
+  MhaArgs a{Q, ldq, K, ldk, V, ldv, nullptr, nullptr, 0, const_cast<float*>(probs), B, heads, Lq, Lk, scale, drop_p,
+            seed};
   hipLaunchKernelGGL(mha_bwd_kernel, dim3(B * heads), dim3(256), 0, (hipStream_t)stream, a, dout, (long)lddo, dQ, dK,
                      dV);
   DASA_CHECK_LAUNCH();

@@ -48,8 +48,11 @@ __device__ __forceinline__ void epilogue_store(const GemmP& p, int b, int row, i
 }
 
 // Load 4 consecutive floats starting at element `e` of a row (limit = first invalid element).
+// VEC: the row base is 16-B aligned, so a whole in-range quad is one dwordx4 load.
+template <bool VEC>
 __device__ __forceinline__ float4 load4(const float* rowp, int e, int limit) {
-  if (e + 3 < limit) return *reinterpret_cast<const float4*>(rowp + e);
+  if (VEC && e + 3 < limit) return *reinterpret_cast<const float4*>(rowp + e);
+  if (!VEC && e + 3 < limit) return make_float4(rowp[e], rowp[e + 1], rowp[e + 2], rowp[e + 3]);
   float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
   if (e + 0 < limit) r.x = rowp[e + 0];
   if (e + 1 < limit) r.y = rowp[e + 1];
@@ -60,7 +63,7 @@ __device__ __forceinline__ float4 load4(const float* rowp, int e, int limit) {
 constexpr int BKT = 32;
 
 // KC = operand stored with K contiguous ([rows][K]); else stored [K][rows].
-template <int ROWS, bool KC>
+template <int ROWS, bool KC, bool VEC>
 struct TileLoader {
   static constexpr int PAD = KC ? 1 : 4;
   static constexpr int NF4 = ROWS * BKT / 4 / 256;
@@ -75,11 +78,11 @@ struct TileLoader {
       if (KC) {
         const int row = q / (BKT / 4), kq = q % (BKT / 4);
         const int gr = r0 + row;
-        r[i] = (gr < rlimit) ? load4(base + (long)gr * ld, k0 + 4 * kq, klimit) : make_float4(0.f, 0.f, 0.f, 0.f);
+        r[i] = (gr < rlimit) ? load4<VEC>(base + (long)gr * ld, k0 + 4 * kq, klimit) : make_float4(0.f, 0.f, 0.f, 0.f);
       } else {
         const int kr = q / (ROWS / 4), rq = q % (ROWS / 4);
         const int gk = k0 + kr;
-        r[i] = (gk < klimit) ? load4(base + (long)gk * ld, r0 + 4 * rq, rlimit) : make_float4(0.f, 0.f, 0.f, 0.f);
+        r[i] = (gk < klimit) ? load4<VEC>(base + (long)gk * ld, r0 + 4 * rq, rlimit) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
   }
@@ -102,13 +105,13 @@ struct TileLoader {
   }
 };
 
-template <int BM, int BN, int WM, int WN, bool AKC, bool BKC>
+template <int BM, int BN, int WM, int WN, bool AKC, bool BKC, bool VEC>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p) {
   constexpr int TM = WM / 32, TN = WN / 32;
   constexpr int WAVES_N = BN / WN;
   static_assert((BM / WM) * (BN / WN) == 4, "4 waves per block");
-  using LA = TileLoader<BM, AKC>;
-  using LB = TileLoader<BN, BKC>;
+  using LA = TileLoader<BM, AKC, VEC>;
+  using LB = TileLoader<BN, BKC, VEC>;
   __shared__ float As[2][BKT][BM + LA::PAD];
   __shared__ float Bs[2][BKT][BN + LB::PAD];
 
@@ -200,14 +203,14 @@ __global__ void splitk_reduce_kernel(GemmP p) {
   }
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, bool VEC>
 int launch_tile(const GemmP& p, int opA, int opB, hipStream_t st) {
   dim3 grid((p.N + BN - 1) / BN, (p.M + BM - 1) / BM, p.batch * p.splitk);
   const bool akc = (opA == 0), bkc = (opB == 1);
-  if (akc && bkc) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, true, true>), grid, dim3(256), 0, st, p);
-  else if (akc && !bkc) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, true, false>), grid, dim3(256), 0, st, p);
-  else if (!akc && bkc) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, false, true>), grid, dim3(256), 0, st, p);
-  else hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, false, false>), grid, dim3(256), 0, st, p);
+  if (akc && bkc) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, true, true, VEC>), grid, dim3(256), 0, st, p);
+  else if (akc && !bkc) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, true, false, VEC>), grid, dim3(256), 0, st, p);
+  else if (!akc && bkc) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, false, true, VEC>), grid, dim3(256), 0, st, p);
+  else hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, false, false, VEC>), grid, dim3(256), 0, st, p);
   DASA_CHECK_LAUNCH();
   return 0;
 }
@@ -262,10 +265,10 @@ extern "C" int dasa_gemm_f32(const dasa_gemm_desc* d, void* ws, int64_t ws_bytes
     pl.kchunk = K > 0 ? (int)(cdiv(K, BKT) * BKT) : BKT;
   }
   if (M == 0 || N == 0) return 0;
-  // alignment contract for float4 operand loads
+  // float4 operand loads need 16-B aligned rows; anything else takes the scalar-load variant
   const uintptr_t am = (uintptr_t)d->A | (uintptr_t)d->B;
-  if ((am & 15) || (d->lda & 3) || (d->ldb & 3) || (batch > 1 && ((d->strideA & 3) || (d->strideB & 3))))
-    return (int)hipErrorInvalidValue;
+  const bool vec = !((am & 15) || (d->lda & 3) || (d->ldb & 3) ||
+                     (batch > 1 && ((d->strideA & 3) || (d->strideB & 3))));
   if (d->opA == 0 ? d->lda < K : d->lda < M) return (int)hipErrorInvalidValue;
   if (d->opB == 1 ? d->ldb < K : d->ldb < N) return (int)hipErrorInvalidValue;
   if (d->ldc < N) return (int)hipErrorInvalidValue;
@@ -281,11 +284,16 @@ extern "C" int dasa_gemm_f32(const dasa_gemm_desc* d, void* ws, int64_t ws_bytes
   p.ws = (float*)ws;
   hipStream_t st = (hipStream_t)stream;
   int rc;
-  switch (pl.cfg) {
-    case 0: rc = launch_tile<128, 128, 64, 64>(p, d->opA, d->opB, st); break;
-    case 1: rc = launch_tile<64, 128, 32, 64>(p, d->opA, d->opB, st); break;
-    case 3: rc = launch_tile<32, 128, 32, 32>(p, d->opA, d->opB, st); break;
-    default: rc = launch_tile<64, 64, 32, 32>(p, d->opA, d->opB, st); break;
+  if (!vec) {
+    rc = pl.cfg == 3 ? launch_tile<32, 128, 32, 32, false>(p, d->opA, d->opB, st)
+                     : launch_tile<64, 64, 32, 32, false>(p, d->opA, d->opB, st);
+  } else {
+    switch (pl.cfg) {
+      case 0: rc = launch_tile<128, 128, 64, 64, true>(p, d->opA, d->opB, st); break;
+      case 1: rc = launch_tile<64, 128, 32, 64, true>(p, d->opA, d->opB, st); break;
+      case 3: rc = launch_tile<32, 128, 32, 32, true>(p, d->opA, d->opB, st); break;
+      default: rc = launch_tile<64, 64, 32, 32, true>(p, d->opA, d->opB, st); break;
+    }
   }
   if (rc) return rc;
   if (pl.splitk > 1) {

@@ -57,7 +57,8 @@ __global__ void lstm_cell_bwd_kernel(const float* __restrict__ act, const float*
 // ---------------------------------------------------------------- bi-LSTM recurrence
 struct SeqArgs {
   const float* xproj;   // [B][L][2][4H]
-  const float* whh;     // [2][4H][H]
+  const float* whh0;    // [4H][H] forward direction
+  const float* whh1;    // [4H][H] backward direction
   const int* len;       // [B]
   float* out;           // [B][L][2H]
   const float* hin;     // [2][B][H]
@@ -110,7 +111,7 @@ __global__ __launch_bounds__(256) void bilstm_step_fused_kernel(SeqArgs a, int s
   const float* hrow = a.hin + ((long)dir * B + r) * H;
   const bool arow = r < B;
   const int q = r & 3, unit = u0 + (r >> 2);
-  const float* wrow = a.whh + ((long)dir * 4 * H + (long)q * H + unit) * H;
+  const float* wrow = (dir ? a.whh1 : a.whh0) + ((long)q * H + unit) * H;
   const int kq = H / 4, k0 = w * kq;
   floatx16 acc;
 #pragma unroll
@@ -157,7 +158,8 @@ __global__ void copy_kernel(const float* src, float* dst, long n) {
 
 // ---------------------------------------------------------------- bi-LSTM BPTT
 struct BpttArgs {
-  const float* whh;       // [2][4H][H]
+  const float* whh0;      // [4H][H]
+  const float* whh1;
   const int* len;
   const float* save_act;  // [L][2][B][4H]
   const float* save_c;    // [L][2][B][H]
@@ -184,7 +186,7 @@ __global__ __launch_bounds__(512) void bilstm_bptt_step_kernel(BpttArgs a, int s
   if (tpv) {
     const bool arow = r < B;
     const float* grow = a.dgates + (((long)r * L + tp) * 2 + dir) * G4;
-    const float* W = a.whh + (long)dir * G4 * H + j0 + r;
+    const float* W = (dir ? a.whh1 : a.whh0) + j0 + r;
     const int kq = G4 / 8, k0 = w * kq;
 #pragma unroll 8
     for (int n = k0; n < k0 + kq; n += 2) {
@@ -226,9 +228,33 @@ __global__ __launch_bounds__(512) void bilstm_bptt_step_kernel(BpttArgs a, int s
   }
 }
 
+// hprev[dir][b][t][:] = the recurrent input of step t: fwd out[b][t-1][0:H], bwd out[b][t+1][H:2H], 0 at the ends.
+__global__ void bilstm_hprev_kernel(const float* __restrict__ out, float* __restrict__ hprev, int B, int L, int H) {
+  const long total = 2L * B * L * H;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int j = (int)(i % H);
+    long r = i / H;
+    const int t = (int)(r % L);
+    r /= L;
+    const int b = (int)(r % B), dir = (int)(r / B);
+    const int ts = dir == 0 ? t - 1 : t + 1;
+    hprev[i] = (ts >= 0 && ts < L) ? out[((long)b * L + ts) * 2 * H + dir * H + j] : 0.f;
+  }
+}
+
 inline int cdivi(long a, long b) { return (int)((a + b - 1) / b); }
 
 }  // namespace
+
+extern "C" int dasa_bilstm_hprev(const float* out, float* hprev, int32_t B, int32_t L, int32_t H, void* stream) {
+  if (B <= 0 || L <= 0) return 0;
+  long total = 2L * B * L * H;
+  int grid = cdivi(total, 256);
+  if (grid > 16384) grid = 16384;
+  hipLaunchKernelGGL(bilstm_hprev_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, out, hprev, B, L, H);
+  DASA_CHECK_LAUNCH();
+  return 0;
+}
 
 extern "C" int dasa_lstm_cell_fwd(const float* gates, const float* c_prev, float* h, float* c, float* act_save,
                                   int32_t B, int32_t H, void* stream) {
@@ -254,11 +280,12 @@ extern "C" int64_t dasa_bilstm_workspace(int32_t B, int32_t H) {
   return (int64_t)((B <= 32 ? base : base + 8L * B * H) * sizeof(float));
 }
 
-extern "C" int dasa_bilstm_fwd(const float* xproj, const float* whh, const int32_t* lengths, float* out,
-                               float* h_n, float* c_n, float* save_act, float* save_c, int32_t B, int32_t L,
-                               int32_t H, float* ws, void* stream) {
+extern "C" int dasa_bilstm_fwd(const float* xproj, const float* whh_fwd, const float* whh_bwd,
+                               const int32_t* lengths, float* out, float* h_n, float* c_n, float* save_act,
+                               float* save_c, int32_t B, int32_t L, int32_t H, float* ws, void* stream) {
   if (B <= 0 || L <= 0) return 0;
-  if ((H % 32) || !ws || ((uintptr_t)whh & 15) || (save_act != nullptr) != (save_c != nullptr))
+  if ((H % 32) || !ws || (((uintptr_t)whh_fwd | (uintptr_t)whh_bwd) & 15) ||
+      (save_act != nullptr) != (save_c != nullptr))
     return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   const long S = 2L * B * H;
@@ -268,7 +295,7 @@ extern "C" int dasa_bilstm_fwd(const float* xproj, const float* whh, const int32
   float* rec = ws + 3 * S;
   hipLaunchKernelGGL(fill_kernel, dim3(cdivi(3 * S, 256)), dim3(256), 0, st, ws, 3 * S, 0.f);
   DASA_CHECK_LAUNCH();
-  SeqArgs a{xproj, whh, lengths, out, h0, h1, c, save_act, save_c, nullptr, B, L, H};
+  SeqArgs a{xproj, whh_fwd, whh_bwd, lengths, out, h0, h1, c, save_act, save_c, nullptr, B, L, H};
   for (int s = 0; s < L; ++s) {
     a.hin = (s & 1) ? h1 : h0;
     a.hout = (s & 1) ? h0 : h1;
@@ -276,14 +303,16 @@ extern "C" int dasa_bilstm_fwd(const float* xproj, const float* whh, const int32
       hipLaunchKernelGGL(bilstm_step_fused_kernel, dim3(H / 8, 2), dim3(256), 0, st, a, s);
       DASA_CHECK_LAUNCH();
     } else {
-      dasa_gemm_desc d{};
-      d.M = B; d.N = 4 * H; d.K = H; d.batch = 2; d.opA = 0; d.opB = 1;
-      d.A = a.hin; d.lda = H; d.strideA = (long)B * H;
-      d.B = whh; d.ldb = H; d.strideB = 4L * H * H;
-      d.C = rec; d.ldc = 4 * H; d.strideC = 4L * B * H;
-      d.alpha = 1.f; d.beta = 0.f;
-      int rc = dasa_gemm_f32(&d, nullptr, 0, stream);
-      if (rc) return rc;
+      for (int dir = 0; dir < 2; ++dir) {
+        dasa_gemm_desc d{};
+        d.M = B; d.N = 4 * H; d.K = H; d.batch = 1; d.opA = 0; d.opB = 1;
+        d.A = a.hin + (long)dir * B * H; d.lda = H;
+        d.B = dir ? whh_bwd : whh_fwd; d.ldb = H;
+        d.C = rec + (long)dir * 4 * B * H; d.ldc = 4 * H;
+        d.alpha = 1.f; d.beta = 0.f;
+        int rc = dasa_gemm_f32(&d, nullptr, 0, stream);
+        if (rc) return rc;
+      }
       a.rec = rec;
       hipLaunchKernelGGL(bilstm_step_cell_kernel, dim3(cdivi(S, 256)), dim3(256), 0, st, a, s);
       DASA_CHECK_LAUNCH();
@@ -301,7 +330,8 @@ extern "C" int dasa_bilstm_fwd(const float* xproj, const float* whh, const int32
   return 0;
 }
 
-extern "C" int dasa_bilstm_bwd(const float* whh, const int32_t* lengths, const float* save_act, const float* save_c,
+extern "C" int dasa_bilstm_bwd(const float* whh_fwd, const float* whh_bwd, const int32_t* lengths,
+                               const float* save_act, const float* save_c,
                                const float* dout, const float* dh_n, const float* dc_n, float* dgates, int32_t B,
                                int32_t L, int32_t H, float* ws, void* stream) {
   if (B <= 0 || L <= 0) return 0;
@@ -316,7 +346,7 @@ extern "C" int dasa_bilstm_bwd(const float* whh, const int32_t* lengths, const f
   if (dc_n) hipLaunchKernelGGL(copy_kernel, dim3(cdivi(S, 256)), dim3(256), 0, st, dc_n, dc, S);
   else hipLaunchKernelGGL(fill_kernel, dim3(cdivi(S, 256)), dim3(256), 0, st, dc, S, 0.f);
   DASA_CHECK_LAUNCH();
-  BpttArgs a{whh, lengths, save_act, save_c, dout, dgates, dh, dc, B, L, H};
+  BpttArgs a{whh_fwd, whh_bwd, lengths, save_act, save_c, dout, dgates, dh, dc, B, L, H};
   for (int s = 0; s < L; ++s) {
     hipLaunchKernelGGL(bilstm_bptt_step_kernel, dim3(H / 32, 2), dim3(512), 0, st, a, s);
     DASA_CHECK_LAUNCH();

@@ -1,0 +1,86 @@
+"""Episode-sharded data parallelism for Seq2SeqAgent.
+
+One process per GPU; each rank runs its own environment/episode stream. Replicas start identical
+(rank-0 broadcast) and stay identical because the only exchange — one all-reduce (sum / world) of a
+flat fp32 bucket holding every gradient the step produced — happens before clip_grad_norm and
+RMSprop (agent_dg.py:1389-1405), which then run the same math on every rank. Backend "nccl" is
+RCCL on ROCm (xGMI inside a node). Parameters without a gradient anywhere (the detached BERT stack,
+unused linear_out heads) are excluded, and a parameter keeps `grad=None` iff no rank produced one,
+so the optimizer skips exactly what the single-GPU reference skips.
+"""
+import torch
+import torch.distributed as dist
+
+
+class GradSync:
+    def __init__(self, params, bucket_mb=256):
+        self.params = [p for p in params if p.requires_grad]
+        self.world = dist.get_world_size()
+        self.numel = sum(p.numel() for p in self.params)
+        dev = self.params[0].device
+        self.flat = torch.empty(self.numel, dtype=torch.float32, device=dev)
+        self.mask = torch.empty(len(self.params), dtype=torch.float32, device=dev)
+        self.bucket = max(1, int(bucket_mb * 2**20 / 4))
+
+    def __call__(self):
+        off = 0
+        has = []
+        for p in self.params:
+            n = p.numel()
+            if p.grad is not None:
+                self.flat[off:off + n].copy_(p.grad.view(-1))
+                has.append(1.0)
+            else:
+                self.flat[off:off + n].zero_()
+                has.append(0.0)
+            off += n
+        self.mask.copy_(torch.tensor(has))
+        dist.all_reduce(self.mask)
+        # bucketed so that very large models keep several collectives in flight on RCCL's channels
+        for s in range(0, self.numel, self.bucket):
+            dist.all_reduce(self.flat[s:s + self.bucket])
+        self.flat.div_(self.world)
+        m = self.mask.cpu().tolist()
+        off = 0
+        for p, any_rank in zip(self.params, m):
+            n = p.numel()
+            if any_rank > 0:
+                g = self.flat[off:off + n].view_as(p)
+                if p.grad is None:
+                    p.grad = g.clone()
+                else:
+                    p.grad.copy_(g)
+            off += n
+
+
+def broadcast_params(modules, src=0):
+    for m in modules:
+        for t in list(m.parameters()) + list(m.buffers()):
+            dist.broadcast(t.data, src)
+
+
+def _trainable(agent):
+    """Parameters that can receive gradients in this configuration."""
+    out = []
+    for m in agent.models:
+        for name, p in m.named_parameters():
+            if m is agent.encoder and name.startswith("bert."):
+                bert = agent.encoder.bert
+                lang = name.startswith("bert.embeddings") or name.startswith("bert.lalayer") or \
+                    name.startswith("bert.pooler")
+                if lang and not bert.update_lang_bert:
+                    continue
+                if not lang and not bert.update_add_layer:
+                    continue
+            out.append(p)
+    return out
+
+
+def attach(agent):
+    """Broadcast rank 0's weights and install the gradient all-reduce in agent.optim_step()."""
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return None
+    broadcast_params(agent.models)
+    sync = GradSync(_trainable(agent))
+    agent.grad_sync = sync
+    return sync

@@ -1,0 +1,406 @@
+"""Autograd wrappers: each forward/backward is a short sequence of libdasa_hip.so kernels.
+
+These are the differentiable building blocks of the reference-API modules in dasa_amd.r2r. Only
+the tensors a backward actually needs are saved, and nothing is saved when no input requires grad.
+"""
+import numpy as np
+import torch
+
+from . import ops
+
+_seed_rng = np.random.default_rng(int(torch.initial_seed()) & 0xFFFFFFFF)
+
+
+def new_seed():
+    """A fresh 63-bit seed for the counter-RNG dropout kernels."""
+    return int(_seed_rng.integers(1, 2**63 - 1))
+
+
+def reseed(seed):
+    global _seed_rng
+    _seed_rng = np.random.default_rng(seed)
+
+
+def _flat(t):
+    return t.reshape(-1, t.shape[-1])
+
+
+# ------------------------------------------------------------------------------------ Linear
+class LinearFn(torch.autograd.Function):
+    """y = act(x W^T + b) (nn.Linear + activation), one fused MFMA GEMM."""
+
+    @staticmethod
+    def forward(ctx, x, W, b, act):
+        ctx.act = act
+        ctx.has_b = b is not None
+        need = any(ctx.needs_input_grad)
+        if need and act == "gelu":
+            z = ops.linear(x, W, b)
+            y = ops.act_fwd(z, "gelu")
+            ctx.save_for_backward(x, W, z)
+        else:
+            y = ops.linear(x, W, b, act=act)
+            if need:
+                ctx.save_for_backward(x, W, y if act is not None else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, W, s = ctx.saved_tensors
+        N = W.shape[0]
+        dz = _flat(dy.contiguous())
+        if ctx.act is not None:
+            dz = ops.act_bwd(s, dz, ctx.act).view(-1, N)
+        dx = dW = db = None
+        if ctx.needs_input_grad[0]:
+            dx = ops.matmul_nn(dz, W).view(x.shape)
+        if ctx.needs_input_grad[1]:
+            dW = ops.matmul_tn(dz, _flat(x))
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = ops.colsum(dz)
+        return dx, dW, db, None
+
+
+def linear(x, W, b=None, act=None):
+    if torch.is_grad_enabled() and (x.requires_grad or W.requires_grad or (b is not None and b.requires_grad)):
+        return LinearFn.apply(x, W, b, act)
+    return ops.linear(x, W, b, act=act)
+
+
+# ----------------------------------------------------------------------------------- Dropout
+class DropoutFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, p, seed):
+        ctx.p, ctx.seed = p, seed
+        return ops.dropout(x, p, seed)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return ops.dropout(dy.contiguous(), ctx.p, ctx.seed), None, None
+
+
+def dropout(x, p, training):
+    if not training or p <= 0:
+        return x
+    return DropoutFn.apply(x, p, new_seed())
+
+
+class FeatDropFn(torch.autograd.Function):
+    """BAttnDecoderLSTM.drop_env on the RGB columns of a [.., 2176] view block (model.py:506-508, 556-557);
+    the 128 angle columns pass through."""
+
+    @staticmethod
+    def forward(ctx, feat, p, seed, n_angle):
+        ctx.p, ctx.seed, ctx.na = p, seed, n_angle
+        out = torch.empty_like(feat)
+        F = feat.shape[-1] - n_angle
+        ops.dropout(feat[..., :F], p, seed, out=out[..., :F])
+        ops.copy2d(feat[..., F:], out[..., F:])
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.contiguous()
+        dx = torch.empty_like(dy)
+        F = dy.shape[-1] - ctx.na
+        ops.dropout(dy[..., :F], ctx.p, ctx.seed, out=dx[..., :F])
+        ops.copy2d(dy[..., F:], dx[..., F:])
+        return dx, None, None, None
+
+
+def feat_drop(feat, p, training, n_angle=128):
+    if not training or p <= 0:
+        return feat
+    return FeatDropFn.apply(feat, p, new_seed(), n_angle)
+
+
+# --------------------------------------------------------------------- depth-guided AdaIN
+class AdaFeatFn(torch.autograd.Function):
+    """df = f with f[..., :F] replaced by sigmoid(a_fc(d[..., :F])) * f[..., :F] (* shared noise)
+    (agent_dg.py:728, 764-768, 780-785; DGAdaChannel.forward :1525-1547)."""
+
+    @staticmethod
+    def forward(ctx, f, d, W, b, noise, n_angle):
+        F = f.shape[-1] - n_angle
+        out = torch.empty(f.shape, dtype=torch.float32, device=f.device)
+        need = any(ctx.needs_input_grad)
+        f_rgb, d_rgb = f[..., :F], d[..., :F]
+        if need:
+            s = ops.linear(d_rgb, W, b, act="sigmoid")
+            ops.ada_gate_fwd(s, f_rgb, noise, out[..., :F])
+            ctx.save_for_backward(f, d, s, noise)
+        else:
+            ops.linear(d_rgb, W, b, act="sigmoid", out=out[..., :F], aux=f_rgb, colscale=noise)
+        ops.copy2d(f[..., F:], out[..., F:])
+        ctx.F = F
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        f, d, s, noise = ctx.saved_tensors
+        F = ctx.F
+        dy = dy.contiguous()
+        dz = ops.ada_gate_bwd(dy[..., :F], s, f[..., :F], noise)
+        dW = ops.matmul_tn(dz, d[..., :F]) if ctx.needs_input_grad[2] else None
+        db = ops.colsum(dz) if ctx.needs_input_grad[3] else None
+        return None, None, dW, db, None, None
+
+
+def ada_feature(f, d, W, b, noise=None, n_angle=128):
+    return AdaFeatFn.apply(f, d, W, b, noise, n_angle)
+
+
+# -------------------------------------------------------------------- attention heads
+class ShiftAttnFn(torch.autograd.Function):
+    """ShiftSoftDotAttention (model.py:318-353), output_tilde=False: returns weighted context."""
+
+    @staticmethod
+    def forward(ctx, h, feat, W_in, W_s, b_s):
+        q = ops.linear(h, W_in)
+        z = ops.linear(h, W_s, b_s)
+        wctx, attn, shifted, wsm = ops.shift_attn_fwd(q, feat, z)
+        if any(ctx.needs_input_grad):
+            ctx.save_for_backward(h, feat, q, attn, shifted, wsm, W_in, W_s)
+        ctx.mark_non_differentiable(attn)
+        return wctx, attn
+
+    @staticmethod
+    def backward(ctx, dwctx, _dattn):
+        h, feat, q, attn, shifted, wsm, W_in, W_s = ctx.saved_tensors
+        dq, dfeat, dz = ops.shift_attn_bwd(q, feat.contiguous(), attn, shifted, wsm, dwctx.contiguous(),
+                                           want_dctx=ctx.needs_input_grad[1])
+        dh = dWin = dWs = dbs = None
+        if ctx.needs_input_grad[0]:
+            dh = ops.matmul_nn(dq, W_in)
+            ops.matmul_nn(dz, W_s, out=dh, beta=1.0)
+        if ctx.needs_input_grad[2]:
+            dWin = ops.matmul_tn(dq, h)
+        if ctx.needs_input_grad[3]:
+            dWs = ops.matmul_tn(dz, h)
+        if ctx.needs_input_grad[4]:
+            dbs = ops.colsum(dz)
+        return dh, dfeat, dWin, dWs, dbs
+
+
+class SoftDotTildeFn(torch.autograd.Function):
+    """SoftDotAttention with output_tilde=True (model.py:268-296): tanh(W_out [wctx, h]), alpha."""
+
+    @staticmethod
+    def forward(ctx, h, c, mask, W_in, W_out):
+        q = ops.linear(h, W_in)
+        _, probs, wctx = ops.softdot_fwd(q, c, mask)
+        B, D = wctx.shape
+        cat = torch.empty(B, D + h.shape[1], dtype=torch.float32, device=h.device)
+        ops.copy2d(wctx, cat[:, :D])
+        ops.copy2d(h, cat[:, D:])
+        y = ops.linear(cat, W_out, act="tanh")
+        if any(ctx.needs_input_grad):
+            ctx.save_for_backward(h, c, q, probs, cat, y, W_in, W_out)
+        ctx.mark_non_differentiable(probs)
+        return y, probs
+
+    @staticmethod
+    def backward(ctx, dy, _dalpha):
+        h, c, q, probs, cat, y, W_in, W_out = ctx.saved_tensors
+        dz = ops.act_bwd(y, dy.contiguous(), "tanh")
+        D = c.shape[2]
+        dh = dc = dWin = dWout = None
+        if ctx.needs_input_grad[4]:
+            dWout = ops.matmul_tn(dz, cat)
+        dcat = ops.matmul_nn(dz, W_out)
+        dq, dc = ops.softdot_bwd(q, c.contiguous(), probs, dwctx=dcat[:, :D].contiguous(),
+                                 want_dctx=ctx.needs_input_grad[1])
+        if ctx.needs_input_grad[0]:
+            dh = dcat[:, D:].contiguous()
+            ops.matmul_nn(dq, W_in, out=dh, beta=1.0)
+        if ctx.needs_input_grad[3]:
+            dWin = ops.matmul_tn(dq, h)
+        return dh, dc, None, dWin, dWout
+
+
+class CandLogitFn(torch.autograd.Function):
+    """SoftDotAttention with output_prob=False, output_tilde=False: the raw candidate logits
+    (model.py:276-280, 289-290; used as the policy logits at model.py:559)."""
+
+    @staticmethod
+    def forward(ctx, h, cand, W_in):
+        q = ops.linear(h, W_in)
+        scores, _, _ = ops.softdot_fwd(q, cand, None, want_probs=False, want_wctx=False)
+        if any(ctx.needs_input_grad):
+            ctx.save_for_backward(h, cand, q, scores, W_in)
+        return scores
+
+    @staticmethod
+    def backward(ctx, dlogit):
+        h, cand, q, scores, W_in = ctx.saved_tensors
+        # ds = dscores exactly when no dwctx flows (probs operand unused)
+        dq, dcand = ops.softdot_bwd(q, cand.contiguous(), scores, dscores=dlogit.contiguous(),
+                                    want_dctx=ctx.needs_input_grad[1])
+        dh = ops.matmul_nn(dq, W_in) if ctx.needs_input_grad[0] else None
+        dW = ops.matmul_tn(dq, h) if ctx.needs_input_grad[2] else None
+        return dh, dcand, dW
+
+
+# ----------------------------------------------------------------------------------- LSTM
+class LSTMCellFn(torch.autograd.Function):
+    """nn.LSTMCell on the concatenated input [a_emb, attn_feat] (model.py:513-514)."""
+
+    @staticmethod
+    def forward(ctx, a_emb, x2, h, c, W_ih, W_hh, b_ih, b_hh):
+        B, E = a_emb.shape
+        xcat = torch.empty(B, E + x2.shape[1], dtype=torch.float32, device=a_emb.device)
+        ops.copy2d(a_emb, xcat[:, :E])
+        ops.copy2d(x2, xcat[:, E:])
+        gates = ops.linear(xcat, W_ih, b_ih)
+        ops.linear(h, W_hh, b_hh, out=gates, beta=1.0)
+        need = any(ctx.needs_input_grad)
+        h1, c1, act = ops.lstm_cell_fwd(gates, c, save=need)
+        if need:
+            ctx.save_for_backward(xcat, h, c, c1, act, W_ih, W_hh)
+        ctx.E = E
+        return h1, c1
+
+    @staticmethod
+    def backward(ctx, dh1, dc1):
+        xcat, h, c, c1, act, W_ih, W_hh = ctx.saved_tensors
+        dgates, dc_prev = ops.lstm_cell_bwd(act, c, c1, dh1, dc1)
+        E = ctx.E
+        n = ctx.needs_input_grad
+        da = dx2 = dh = dW_ih = dW_hh = db = None
+        if n[0] or n[1]:
+            dxcat = ops.matmul_nn(dgates, W_ih)
+            da = dxcat[:, :E].contiguous() if n[0] else None
+            dx2 = dxcat[:, E:].contiguous() if n[1] else None
+        if n[2]:
+            dh = ops.matmul_nn(dgates, W_hh)
+        if n[4]:
+            dW_ih = ops.matmul_tn(dgates, xcat)
+        if n[5]:
+            dW_hh = ops.matmul_tn(dgates, h)
+        if n[6] or n[7]:
+            db = ops.colsum(dgates)
+        return da, dx2, dh, (dc_prev if n[3] else None), dW_ih, dW_hh, db, db
+
+
+class BiLSTMFn(torch.autograd.Function):
+    """Packed single-layer bidirectional nn.LSTM (r2rmodel.py:2339-2343, pack/pad_packed semantics)."""
+
+    @staticmethod
+    def forward(ctx, x, lengths_i32, W_ih_f, W_hh_f, b_ih_f, b_hh_f, W_ih_b, W_hh_b, b_ih_b, b_hh_b):
+        B, L, E = x.shape
+        H = W_hh_f.shape[1]
+        x2 = x.reshape(B * L, E)
+        xproj = torch.empty(B, L, 2, 4 * H, dtype=torch.float32, device=x.device)
+        bf = ops.add2d(b_ih_f.view(1, -1), b_hh_f.view(1, -1)).view(-1)
+        bb = ops.add2d(b_ih_b.view(1, -1), b_hh_b.view(1, -1)).view(-1)
+        ops.linear(x2, W_ih_f, bf, out=xproj[:, :, 0, :])
+        ops.linear(x2, W_ih_b, bb, out=xproj[:, :, 1, :])
+        need = any(ctx.needs_input_grad)
+        out, h_n, c_n, saved = ops.bilstm_fwd(xproj, W_hh_f, W_hh_b, lengths_i32, H, save=need and B <= 32)
+        if need:
+            if B > 32:
+                raise NotImplementedError("bi-LSTM backward is implemented for B <= 32 per rank")
+            ctx.save_for_backward(x, lengths_i32, out, saved[0], saved[1], W_ih_f, W_hh_f, W_ih_b, W_hh_b)
+        ctx.H = H
+        return out, h_n, c_n
+
+    @staticmethod
+    def backward(ctx, dout, dh_n, dc_n):
+        x, lens, out, sa, sc, W_ih_f, W_hh_f, W_ih_b, W_hh_b = ctx.saved_tensors
+        H = ctx.H
+        B, L, E = x.shape
+        if dout is None:
+            dout = torch.zeros_like(out)
+        dgates = ops.bilstm_bwd(W_hh_f, W_hh_b, lens, (sa, sc), dout, dh_n, dc_n, H)
+        hprev = ops.bilstm_hprev(out, H)
+        x2 = x.reshape(B * L, E)
+        n = ctx.needs_input_grad
+        grads = [None] * 10
+        dx = None
+        for d, (iw, ihh, ibi, ibh, Wih) in enumerate(((2, 3, 4, 5, W_ih_f), (6, 7, 8, 9, W_ih_b))):
+            dg = dgates[:, :, d, :]          # [B, L, 4H] rows of stride 8H
+            if n[iw]:
+                grads[iw] = ops.matmul_tn(dg, x2)
+            if n[ihh]:
+                grads[ihh] = ops.matmul_tn(dg, hprev[d].reshape(B * L, H))
+            if n[ibi] or n[ibh]:
+                db = ops.colsum(dg)
+                grads[ibi] = db if n[ibi] else None
+                grads[ibh] = db if n[ibh] else None
+            if n[0]:
+                if dx is None:
+                    dx = ops.matmul_nn(dg, Wih)
+                else:
+                    ops.matmul_nn(dg, Wih, out=dx, beta=1.0)
+        grads[0] = dx.view(B, L, E) if dx is not None else None
+        return tuple(grads)
+
+
+# --------------------------------------------------------------------------- BERT blocks
+class LayerNormFn(torch.autograd.Function):
+    """LayerNorm(dropout(x) + res) (BertSelfOutput/BertOutput, vilmodel.py:239-250, 296-309)."""
+
+    @staticmethod
+    def forward(ctx, x, res, gamma, beta, eps, p, seed):
+        need = any(ctx.needs_input_grad)
+        x = x.contiguous()
+        if need:
+            y, saved = ops.layernorm(x, gamma, beta, eps, res=res.contiguous() if res is not None else None,
+                                     drop_p=p, seed=seed, save=True)
+            ctx.save_for_backward(gamma, *saved)
+        else:
+            y = ops.layernorm(x, gamma, beta, eps, res=res.contiguous() if res is not None else None, drop_p=p,
+                              seed=seed)
+        ctx.p, ctx.seed, ctx.has_res = p, seed, res is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        gamma, xsum, mean, rstd = ctx.saved_tensors
+        n = ctx.needs_input_grad
+        dgamma = torch.zeros_like(gamma) if n[2] else None
+        dbeta = torch.zeros_like(gamma) if n[3] else None
+        dxs = ops.layernorm_bwd(dy, (xsum, mean, rstd), gamma, dgamma, dbeta)
+        dx = None
+        if n[0]:
+            dx = ops.dropout(dxs, ctx.p, ctx.seed) if ctx.p > 0 else dxs
+        dres = dxs if (ctx.has_res and n[1]) else None
+        return dx, dres, dgamma, dbeta, None, None, None
+
+
+def layer_norm(x, gamma, beta, eps, res=None, p=0.0, training=False):
+    seed = new_seed() if (training and p > 0) else 0
+    p = p if training else 0.0
+    if torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in (x, res, gamma, beta)):
+        return LayerNormFn.apply(x, res, gamma, beta, eps, p, seed)
+    return ops.layernorm(x.contiguous(), gamma, beta, eps, res=res.contiguous() if res is not None else None,
+                         drop_p=p, seed=seed)
+
+
+class MHAFn(torch.autograd.Function):
+    """softmax(Q K^T / sqrt(dh) + mask) V per head (vilmodel.py:214-236, 481-506)."""
+
+    @staticmethod
+    def forward(ctx, Q, K, V, addmask, heads, scale, p, seed):
+        need = any(ctx.needs_input_grad)
+        if need:
+            out, probs = ops.mha(Q, K, V, addmask, heads, scale, p, seed, save_probs=True)
+            ctx.save_for_backward(Q, K, V, probs)
+        else:
+            out = ops.mha(Q, K, V, addmask, heads, scale, p, seed)
+        ctx.heads, ctx.scale, ctx.p, ctx.seed = heads, scale, p, seed
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        Q, K, V, probs = ctx.saved_tensors
+        dQ, dK, dV = ops.mha_bwd(Q, K, V, probs, dout, ctx.heads, ctx.scale, ctx.p, ctx.seed)
+        return dQ, dK, dV, None, None, None, None, None
+
+
+def mha(Q, K, V, addmask, heads, scale, p=0.0, training=False):
+    seed = new_seed() if (training and p > 0) else 0
+    p = p if training else 0.0
+    if torch.is_grad_enabled() and (Q.requires_grad or K.requires_grad or V.requires_grad):
+        return MHAFn.apply(Q, K, V, addmask, heads, scale, p, seed)
+    return ops.mha(Q, K, V, addmask, heads, scale, p, seed)

@@ -9,7 +9,26 @@ import ctypes
 import torch
 
 from . import _lib
-from ._lib import ACT_NONE, ACT_RELU, ACT_GELU, ACT_TANH, ACT_SIGMOID, GemmDesc, check  # noqa: F401
+from . import prof
+from ._lib import ACT_NONE, ACT_RELU, ACT_GELU, ACT_TANH, ACT_SIGMOID, GemmDesc  # noqa: F401
+
+
+def check(rc, what, family=None, flops=0.0, nbytes=0.0, _ev=None):
+    _lib.check(rc, what)
+
+
+def _call(what, family, fn, *a, flops=0.0, nbytes=0.0):
+    """Launch through the C-ABI; under prof.collect() bracket it with HIP events on the stream."""
+    if prof.active():
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        rc = fn(*a)
+        e1.record()
+        prof.record(family, e0, e1, flops, nbytes)
+    else:
+        rc = fn(*a)
+    _lib.check(rc, what)
 
 _ACT_IDS = {None: ACT_NONE, "none": ACT_NONE, "relu": ACT_RELU, "gelu": ACT_GELU, "tanh": ACT_TANH,
             "sigmoid": ACT_SIGMOID}
@@ -71,11 +90,9 @@ def gemm(A, B, C, *, M, N, K, opA=0, opB=1, lda, ldb, ldc, bias=None, act=None, 
     ws = None
     if need > 0:
         ws = torch.empty(need // 4 + 1, dtype=torch.float32, device=C.device)
-    check(L.dasa_gemm_f32(ctypes.byref(d), _p(ws), int(need), _stream()), "dasa_gemm_f32")
-
-
-def C_dev(t):
-    return t.device
+    b = max(1, int(batch))
+    _call("dasa_gemm_f32", "gemm", L.dasa_gemm_f32, ctypes.byref(d), _p(ws), int(need), _stream(),
+          flops=2.0 * M * N * K * b, nbytes=4.0 * b * (M * K + K * N + M * N))
 
 
 def linear(x, W, b=None, act=None, out=None, aux=None, colscale=None, beta=0.0, alpha=1.0):
@@ -138,10 +155,27 @@ def colsum(X, out=None, beta=0.0):
 
 
 # ------------------------------------------------------------------------------------ elementwise
+def act_fwd(x, act):
+    x = x.contiguous()
+    y = torch.empty_like(x)
+    _call("dasa_act_fwd", "elementwise", _lib.lib().dasa_act_fwd, _p(x), _p(y), x.numel(), _ACT_IDS[act], _stream())
+    return y
+
+
+def add2d(a, b, out=None):
+    rows, lda = _rows(a)
+    _, ldb = _rows(b)
+    if out is None:
+        out = torch.empty(a.shape, dtype=torch.float32, device=a.device)
+    _, ldo = _rows(out)
+    _call("dasa_add2d", "elementwise", _lib.lib().dasa_add2d, _p(a), lda, _p(b), ldb, _p(out), ldo, rows, a.shape[-1], _stream())
+    return out
+
+
 def act_bwd(y_or_x, dy, act):
     dx = torch.empty_like(dy)
-    check(_lib.lib().dasa_act_bwd(_p(y_or_x.contiguous()), _p(dy.contiguous()), _p(dx), dy.numel(),
-                                  _ACT_IDS[act], _stream()), "dasa_act_bwd")
+    _call("dasa_act_bwd", "elementwise", _lib.lib().dasa_act_bwd, _p(y_or_x.contiguous()), _p(dy.contiguous()), _p(dx), dy.numel(),
+                                  _ACT_IDS[act], _stream())
     return dx
 
 
@@ -152,15 +186,22 @@ def dropout(x, p, seed, out=None):
     if out is None:
         out = torch.empty_like(x)
     _, ldy = _rows(out)
-    check(_lib.lib().dasa_dropout_fwd(_p(x), ldx, _p(out), ldy, rows, cols, float(p), int(seed) & (2**64 - 1),
-                                      _stream()), "dasa_dropout_fwd")
+    _call("dasa_dropout_fwd", "elementwise", _lib.lib().dasa_dropout_fwd, _p(x), ldx, _p(out), ldy, rows, cols, float(p), int(seed) & (2**64 - 1),
+                                      _stream())
     return out
 
 
 def copy2d(x, out):
     rows, ldx = _rows(x)
     _, ldo = _rows(out)
-    check(_lib.lib().dasa_copy2d(_p(x), ldx, _p(out), ldo, rows, x.shape[-1], _stream()), "dasa_copy2d")
+    _call("dasa_copy2d", "elementwise", _lib.lib().dasa_copy2d, _p(x), ldx, _p(out), ldo, rows, x.shape[-1], _stream())
+    return out
+
+
+def colscale(x, scale, out):
+    rows, ldx = _rows(x)
+    _, ldo = _rows(out)
+    _call("dasa_colscale", "elementwise", _lib.lib().dasa_colscale, _p(x), ldx, _p(scale.contiguous()), _p(out), ldo, rows, x.shape[-1], _stream())
     return out
 
 
@@ -168,8 +209,8 @@ def ada_gate_fwd(s, f, noise, out):
     rows, lds = _rows(s)
     _, ldf = _rows(f)
     _, ldo = _rows(out)
-    check(_lib.lib().dasa_ada_gate_fwd(_p(s), lds, _p(f), ldf, _p(noise), _p(out), ldo, rows, s.shape[-1],
-                                       _stream()), "dasa_ada_gate_fwd")
+    _call("dasa_ada_gate_fwd", "ada_gate", _lib.lib().dasa_ada_gate_fwd, _p(s), lds, _p(f), ldf, _p(noise), _p(out), ldo, rows, s.shape[-1],
+                                       _stream())
     return out
 
 
@@ -178,8 +219,8 @@ def ada_gate_bwd(dout, s, f, noise):
     _, lds = _rows(s)
     _, ldf = _rows(f)
     dz = torch.empty(rows, s.shape[-1], dtype=torch.float32, device=s.device)
-    check(_lib.lib().dasa_ada_gate_bwd(_p(dout), lddo, _p(s), lds, _p(f), ldf, _p(noise), _p(dz), s.shape[-1],
-                                       rows, s.shape[-1], _stream()), "dasa_ada_gate_bwd")
+    _call("dasa_ada_gate_bwd", "ada_gate", _lib.lib().dasa_ada_gate_bwd, _p(dout), lddo, _p(s), lds, _p(f), ldf, _p(noise), _p(dz), s.shape[-1],
+                                       rows, s.shape[-1], _stream())
     return dz
 
 
@@ -194,9 +235,9 @@ def layernorm(x, gamma, beta, eps, res=None, drop_p=0.0, seed=0, save=False):
         mean = torch.empty(M, dtype=torch.float32, device=x.device)
         rstd = torch.empty_like(mean)
         xsum = torch.empty_like(x)
-    check(_lib.lib().dasa_layernorm_fwd(_p(x), _p(res), _p(gamma), _p(beta), _p(y), _p(mean), _p(rstd), _p(xsum),
-                                        M, N, float(eps), float(drop_p), int(seed) & (2**64 - 1), _stream()),
-          "dasa_layernorm_fwd")
+    _call("dasa_layernorm_fwd", "layernorm", _lib.lib().dasa_layernorm_fwd, _p(x), _p(res), _p(gamma), _p(beta),
+          _p(y), _p(mean), _p(rstd), _p(xsum), M, N, float(eps), float(drop_p), int(seed) & (2**64 - 1), _stream(),
+          nbytes=4.0 * M * N * (3 if res is not None else 2))
     if save:
         return y, (xsum, mean, rstd)
     return y
@@ -207,8 +248,8 @@ def layernorm_bwd(dy, saved, gamma, dgamma, dbeta):
     M, _ = _rows(xsum)
     N = xsum.shape[-1]
     dx = torch.empty_like(xsum)
-    check(_lib.lib().dasa_layernorm_bwd(_p(dy.contiguous()), _p(xsum), _p(gamma), _p(mean), _p(rstd), _p(dx),
-                                        _p(dgamma), _p(dbeta), M, N, _stream()), "dasa_layernorm_bwd")
+    _call("dasa_layernorm_bwd", "elementwise", _lib.lib().dasa_layernorm_bwd, _p(dy.contiguous()), _p(xsum), _p(gamma), _p(mean), _p(rstd), _p(dx),
+                                        _p(dgamma), _p(dbeta), M, N, _stream())
     return dx
 
 
@@ -217,9 +258,9 @@ def bert_embed(ids, word, pos, type0, gamma, beta, eps, drop_p=0.0, seed=0):
     H = word.shape[1]
     out = torch.empty(B, L, H, dtype=torch.float32, device=word.device)
     ids = ids.contiguous().to(torch.int64)
-    check(_lib.lib().dasa_bert_embed_fwd(_p(ids), _p(word), _p(pos), _p(type0), _p(gamma), _p(beta), _p(out), B, L,
-                                         H, float(eps), float(drop_p), int(seed) & (2**64 - 1), _stream()),
-          "dasa_bert_embed_fwd")
+    _call("dasa_bert_embed_fwd", "embed", _lib.lib().dasa_bert_embed_fwd, _p(ids), _p(word), _p(pos), _p(type0),
+          _p(gamma), _p(beta), _p(out), B, L, H, float(eps), float(drop_p), int(seed) & (2**64 - 1), _stream(),
+          nbytes=4.0 * 3 * B * L * H)
     return out
 
 
@@ -230,20 +271,21 @@ def mha(Q, K, V, addmask, heads, scale, drop_p=0.0, seed=0, save_probs=False):
     dh = Hd // heads
     out = torch.empty(B, Lq, Hd, dtype=torch.float32, device=Q.device)
     probs = torch.empty(B, heads, Lq, Lk, dtype=torch.float32, device=Q.device) if save_probs else None
-    check(_lib.lib().dasa_mha_fwd(_p(Q), Q.stride(1), _p(K), K.stride(1), _p(V), V.stride(1),
-                                  _p(addmask.contiguous() if addmask is not None else None), _p(out), Hd, _p(probs),
-                                  B, heads, Lq, Lk, dh, float(scale), float(drop_p), int(seed) & (2**64 - 1),
-                                  _stream()), "dasa_mha_fwd")
+    _call("dasa_mha_fwd", "mha", _lib.lib().dasa_mha_fwd, _p(Q), Q.stride(1), _p(K), K.stride(1), _p(V), V.stride(1),
+          _p(addmask.contiguous() if addmask is not None else None), _p(out), Hd, _p(probs),
+          B, heads, Lq, Lk, dh, float(scale), float(drop_p), int(seed) & (2**64 - 1), _stream(),
+          flops=4.0 * B * Lq * Lk * Hd, nbytes=4.0 * B * (2 * Lq + 2 * Lk) * Hd)
     return (out, probs) if save_probs else out
 
 
-def mha_bwd(Q, K, V, probs, dout, heads, scale):
+def mha_bwd(Q, K, V, probs, dout, heads, scale, drop_p=0.0, seed=0):
     B, Lq, Hd = Q.shape
     Lk = K.shape[1]
     Q, K, V, dout = Q.contiguous(), K.contiguous(), V.contiguous(), dout.contiguous()
     dQ, dK, dV = torch.empty_like(Q), torch.empty_like(K), torch.empty_like(V)
-    check(_lib.lib().dasa_mha_bwd(_p(Q), Hd, _p(K), Hd, _p(V), Hd, _p(probs), _p(dout), Hd, _p(dQ), _p(dK), _p(dV),
-                                  B, heads, Lq, Lk, Hd // heads, float(scale), _stream()), "dasa_mha_bwd")
+    _call("dasa_mha_bwd", "elementwise", _lib.lib().dasa_mha_bwd, _p(Q), Hd, _p(K), Hd, _p(V), Hd, _p(probs), _p(dout), Hd, _p(dQ), _p(dK), _p(dV),
+                                  B, heads, Lq, Lk, Hd // heads, float(scale), float(drop_p), int(seed) & (2**64 - 1),
+                                  _stream())
     return dQ, dK, dV
 
 
@@ -258,8 +300,9 @@ def softdot_fwd(q, ctx, mask=None, want_scores=True, want_probs=True, want_wctx=
     probs = torch.empty(B, N, dtype=torch.float32, device=q.device) if want_probs else None
     wctx = torch.empty(B, D, dtype=torch.float32, device=q.device) if want_wctx else None
     m = mask.to(torch.uint8).contiguous() if mask is not None else None
-    check(_lib.lib().dasa_softdot_fwd(_p(q), _p(ctx), ldn, _p(m), _p(scores), _p(probs), _p(wctx), B, N, D,
-                                      _stream()), "dasa_softdot_fwd")
+    _call("dasa_softdot_fwd", "softdot", _lib.lib().dasa_softdot_fwd, _p(q), _p(ctx), ldn, _p(m), _p(scores), _p(probs),
+          _p(wctx), B, N, D, _stream(),
+          nbytes=4.0 * B * (N * D + D + (D if wctx is not None else 0) + 2 * N))
     return scores, probs, wctx
 
 
@@ -271,10 +314,11 @@ def softdot_bwd(q, ctx, probs, dwctx=None, dscores=None, want_dctx=True):
     ws = torch.empty(B * N, dtype=torch.float32, device=q.device)
     if dctx is not None:
         assert ldn == D, "dctx is written dense; pass a contiguous ctx for backward"
-    check(_lib.lib().dasa_softdot_bwd(_p(q.contiguous()), _p(ctx), ldn, _p(probs),
-                                      _p(dwctx.contiguous() if dwctx is not None else None),
-                                      _p(dscores.contiguous() if dscores is not None else None), _p(dq), _p(dctx), 0,
-                                      B, N, D, _p(ws), _stream()), "dasa_softdot_bwd")
+    _call("dasa_softdot_bwd", "softdot_bwd", _lib.lib().dasa_softdot_bwd, _p(q.contiguous()), _p(ctx), ldn, _p(probs),
+          _p(dwctx.contiguous() if dwctx is not None else None),
+          _p(dscores.contiguous() if dscores is not None else None), _p(dq), _p(dctx), 0,
+          B, N, D, _p(ws), _stream(),
+          nbytes=4.0 * B * (N * D * (2 if dwctx is not None else 1) + (N * D if dctx is not None else 0) + 3 * D))
     return dq, dctx
 
 
@@ -289,9 +333,9 @@ def shift_attn_fwd(q, ctx, shift_logits):
     wsm = torch.empty(B, K, dtype=torch.float32, device=q.device)
     wctx = torch.empty(B, D, dtype=torch.float32, device=q.device)
     ws = torch.empty(B * N, dtype=torch.float32, device=q.device)
-    check(_lib.lib().dasa_shift_attn_fwd(_p(q.contiguous()), _p(ctx), ldn, _p(shift_logits.contiguous()), _p(attn),
-                                         _p(shifted), _p(wsm), _p(wctx), B, D, K, _p(ws), _stream()),
-          "dasa_shift_attn_fwd")
+    _call("dasa_shift_attn_fwd", "shift_attn", _lib.lib().dasa_shift_attn_fwd, _p(q.contiguous()), _p(ctx), ldn,
+          _p(shift_logits.contiguous()), _p(attn), _p(shifted), _p(wsm), _p(wctx), B, D, K, _p(ws), _stream(),
+          nbytes=4.0 * B * (N * D + 2 * D))
     return wctx, attn, shifted, wsm
 
 
@@ -305,9 +349,9 @@ def shift_attn_bwd(q, ctx, attn, shifted, wsm, dwctx, want_dctx=True):
         assert ldn == D, "dctx is written dense; pass a contiguous ctx for backward"
     dz = torch.empty(B, K, dtype=torch.float32, device=q.device)
     ws = torch.empty(B * N, dtype=torch.float32, device=q.device)
-    check(_lib.lib().dasa_shift_attn_bwd(_p(q.contiguous()), _p(ctx), ldn, _p(attn), _p(shifted), _p(wsm),
-                                         _p(dwctx.contiguous()), _p(dq), _p(dctx), _p(dz), 0, B, D, K, _p(ws),
-                                         _stream()), "dasa_shift_attn_bwd")
+    _call("dasa_shift_attn_bwd", "shift_attn_bwd", _lib.lib().dasa_shift_attn_bwd, _p(q.contiguous()), _p(ctx), ldn,
+          _p(attn), _p(shifted), _p(wsm), _p(dwctx.contiguous()), _p(dq), _p(dctx), _p(dz), 0, B, D, K, _p(ws),
+          _stream(), nbytes=4.0 * B * (N * D * (3 if dctx is not None else 2) + 3 * D))
     return dq, dctx, dz
 
 
@@ -318,8 +362,8 @@ def lstm_cell_fwd(gates, c_prev, save=False):
     h = torch.empty(B, H, dtype=torch.float32, device=gates.device)
     c = torch.empty_like(h)
     act = torch.empty_like(gates) if save else None
-    check(_lib.lib().dasa_lstm_cell_fwd(_p(gates.contiguous()), _p(c_prev.contiguous()), _p(h), _p(c), _p(act), B, H,
-                                        _stream()), "dasa_lstm_cell_fwd")
+    _call("dasa_lstm_cell_fwd", "lstm_cell", _lib.lib().dasa_lstm_cell_fwd, _p(gates.contiguous()), _p(c_prev.contiguous()), _p(h), _p(c), _p(act), B, H,
+                                        _stream())
     return h, c, act
 
 
@@ -328,14 +372,14 @@ def lstm_cell_bwd(act, c_prev, c, dh, dc):
     H = G4 // 4
     dgates = torch.empty_like(act)
     dc_prev = torch.empty(B, H, dtype=torch.float32, device=act.device)
-    check(_lib.lib().dasa_lstm_cell_bwd(_p(act), _p(c_prev.contiguous()), _p(c), _p(dh.contiguous() if dh is not None else None),
+    _call("dasa_lstm_cell_bwd", "lstm_cell", _lib.lib().dasa_lstm_cell_bwd, _p(act), _p(c_prev.contiguous()), _p(c), _p(dh.contiguous() if dh is not None else None),
                                         _p(dc.contiguous() if dc is not None else None), _p(dgates), _p(dc_prev), B, H,
-                                        _stream()), "dasa_lstm_cell_bwd")
+                                        _stream())
     return dgates, dc_prev
 
 
-def bilstm_fwd(xproj, whh, lengths_i32, H, save=False):
-    """xproj [B, L, 2, 4H]; whh [2, 4H, H]; lengths int32 [B] (device). Returns out [B, L, 2H],
+def bilstm_fwd(xproj, whh_f, whh_b, lengths_i32, H, save=False):
+    """xproj [B, L, 2, 4H]; whh_f/whh_b [4H, H]; lengths int32 [B] (device). Returns out [B, L, 2H],
     h_n [2, B, H], c_n [2, B, H], saved (act, c) or None."""
     B, L = xproj.shape[0], xproj.shape[1]
     dev = xproj.device
@@ -348,29 +392,37 @@ def bilstm_fwd(xproj, whh, lengths_i32, H, save=False):
         sc = torch.empty(L, 2, B, H, dtype=torch.float32, device=dev)
     L_ = _lib.lib()
     ws = torch.empty(L_.dasa_bilstm_workspace(B, H) // 4, dtype=torch.float32, device=dev)
-    check(L_.dasa_bilstm_fwd(_p(xproj.contiguous()), _p(whh), _p(lengths_i32), _p(out), _p(h_n), _p(c_n), _p(sa),
-                             _p(sc), B, L, H, _p(ws), _stream()), "dasa_bilstm_fwd")
+    _call("dasa_bilstm_fwd", "bilstm", L_.dasa_bilstm_fwd, _p(xproj.contiguous()), _p(whh_f.contiguous()),
+          _p(whh_b.contiguous()), _p(lengths_i32), _p(out), _p(h_n), _p(c_n), _p(sa), _p(sc), B, L, H, _p(ws), _stream(),
+          flops=2.0 * 2 * L * B * 4 * H * H, nbytes=4.0 * L * 2 * 4 * H * H)
     return out, h_n, c_n, ((sa, sc) if save else None)
 
 
-def bilstm_bwd(whh, lengths_i32, saved, dout, dh_n, dc_n, H):
+def bilstm_bwd(whh_f, whh_b, lengths_i32, saved, dout, dh_n, dc_n, H):
     sa, sc = saved
     L, _, B, _ = sa.shape
     dev = sa.device
     dgates = torch.empty(B, L, 2, 4 * H, dtype=torch.float32, device=dev)
     ws = torch.empty(4 * B * H, dtype=torch.float32, device=dev)
-    check(_lib.lib().dasa_bilstm_bwd(_p(whh), _p(lengths_i32), _p(sa), _p(sc), _p(dout.contiguous()),
-                                     _p(dh_n.contiguous() if dh_n is not None else None),
-                                     _p(dc_n.contiguous() if dc_n is not None else None), _p(dgates), B, L, H, _p(ws),
-                                     _stream()), "dasa_bilstm_bwd")
+    _call("dasa_bilstm_bwd", "bilstm_bptt", _lib.lib().dasa_bilstm_bwd, _p(whh_f.contiguous()), _p(whh_b.contiguous()),
+          _p(lengths_i32), _p(sa), _p(sc), _p(dout.contiguous()),
+          _p(dh_n.contiguous() if dh_n is not None else None),
+          _p(dc_n.contiguous() if dc_n is not None else None), _p(dgates), B, L, H, _p(ws), _stream(),
+          flops=2.0 * 2 * L * B * 4 * H * H, nbytes=4.0 * L * 2 * 4 * H * H)
     return dgates
+
+
+def bilstm_hprev(out, H):
+    B, L, _ = out.shape
+    hprev = torch.empty(2, B, L, H, dtype=torch.float32, device=out.device)
+    _call("dasa_bilstm_hprev", "elementwise", _lib.lib().dasa_bilstm_hprev, _p(out.contiguous()), _p(hprev), B, L, H, _stream())
+    return hprev
 
 
 def reverse_valid(x, lengths_i32):
     B, L, H = x.shape
     out = torch.empty_like(x)
-    check(_lib.lib().dasa_reverse_valid(_p(x.contiguous()), _p(lengths_i32), _p(out), B, L, H, _stream()),
-          "dasa_reverse_valid")
+    _call("dasa_reverse_valid", "elementwise", _lib.lib().dasa_reverse_valid, _p(x.contiguous()), _p(lengths_i32), _p(out), B, L, H, _stream())
     return out
 
 
@@ -382,6 +434,16 @@ def adain_musigma(content, style, out=None, eps=1e-5):
     if out is None:
         out = torch.empty(content.shape, dtype=torch.float32, device=content.device)
     _, ldo = _rows(out)
-    check(_lib.lib().dasa_adain_musigma_fwd(_p(content), ldc, _p(style), lds, _p(out), ldo, None, M, N, float(eps),
-                                            _stream()), "dasa_adain_musigma_fwd")
+    _call("dasa_adain_musigma_fwd", "elementwise", _lib.lib().dasa_adain_musigma_fwd, _p(content), ldc, _p(style), lds, _p(out), ldo, None, M, N, float(eps),
+                                            _stream())
+    return out
+
+
+def gather_rows(ta, ia, tb, ib, out):
+    """out[r] = [ta[ia[r]] | tb[ib[r]]] (zeros for negative indices); ta [Na, Fa], tb [Nb, Fb]."""
+    R = ia.numel()
+    Fa = ta.shape[-1]
+    Fb = tb.shape[-1] if tb is not None else out.shape[-1] - Fa
+    _call("dasa_gather_rows", "gather", _lib.lib().dasa_gather_rows, _p(ta), _p(ia), Fa, _p(tb), _p(ib), Fb, _p(out),
+          R, _stream(), nbytes=8.0 * R * (Fa + Fb))
     return out

@@ -1,0 +1,84 @@
+"""Per-kernel-family device timing with HIP events (torch.cuda.Event on the launch stream) plus the
+algorithmic FLOPs / bytes of each launch, for bench.py's roofline report. Off unless collect() is
+active, so the timed region of the benchmark carries no instrumentation."""
+import contextlib
+from collections import defaultdict
+
+import torch
+
+_REC = None
+
+# family -> (roofline bound, kernel name prefix in rocprof)
+FAMILIES = {
+    "gemm": ("mfma", "gemm_f32_kernel"),
+    "bilstm": ("mfma", "bilstm_step_fused_kernel"),
+    "bilstm_bptt": ("mfma", "bilstm_bptt_step_kernel"),
+    "shift_attn": ("hbm", "scores_kernel+apply_fwd_kernel"),
+    "shift_attn_bwd": ("hbm", "scores_kernel+apply_bwd_kernel"),
+    "softdot": ("hbm", "scores_kernel+apply_fwd_kernel"),
+    "softdot_bwd": ("hbm", "scores_kernel+apply_bwd_kernel"),
+    "mha": ("hbm", "mha_fwd_kernel"),
+    "layernorm": ("hbm", "ln_fwd_kernel"),
+    "embed": ("hbm", "embed_kernel"),
+    "ada_gate": ("hbm", "ada_gate_*_kernel"),
+    "gather": ("hbm", "gather_rows_kernel"),
+    "elementwise": ("hbm", "various"),
+    "lstm_cell": ("hbm", "lstm_cell_*_kernel"),
+}
+
+
+class _Recorder:
+    def __init__(self):
+        self.items = []
+
+    def summary(self, peak_tf=157.3, peak_gbs=8000.0):
+        torch.cuda.synchronize()
+        fam = defaultdict(lambda: {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0})
+        for name, e0, e1, flops, nbytes in self.items:
+            f = fam[name]
+            f["launches"] += 1
+            f["ms"] += e0.elapsed_time(e1)
+            f["flops"] += flops
+            f["bytes"] += nbytes
+        total = sum(f["ms"] for f in fam.values()) or 1.0
+        kernels = {}
+        for name, f in sorted(fam.items(), key=lambda kv: -kv[1]["ms"]):
+            bound = FAMILIES.get(name, ("hbm", ""))[0]
+            s = f["ms"] / 1e3
+            ent = {"launches": f["launches"], "device_ms": round(f["ms"], 3), "share": round(f["ms"] / total, 4),
+                   "avg_launch_us": round(1e3 * f["ms"] / f["launches"], 2), "bound": bound}
+            if bound == "mfma":
+                ach = f["flops"] / s / 1e12 if s > 0 else 0.0
+                ent.update(achieved=round(ach, 2), peak=peak_tf, unit="TFLOP/s", frac=round(ach / peak_tf, 4))
+            else:
+                ach = f["bytes"] / s / 1e9 if s > 0 else 0.0
+                ent.update(achieved=round(ach, 1), peak=peak_gbs, unit="GB/s", frac=round(ach / peak_gbs, 4))
+            kernels[name] = ent
+        dom_name = max(fam.items(), key=lambda kv: kv[1]["ms"])[0]
+        d = kernels[dom_name]
+        roof = {"kernel": dom_name, "bound": d["bound"], "achieved": d["achieved"], "peak": d["peak"],
+                "unit": d["unit"], "frac": d["frac"], "traffic": None,
+                "per_launch": {"avg_us": d["avg_launch_us"],
+                               "alg_" + ("flops" if d["bound"] == "mfma" else "bytes"):
+                                   (fam[dom_name]["flops"] if d["bound"] == "mfma" else fam[dom_name]["bytes"])
+                                   / fam[dom_name]["launches"]}}
+        return {"roofline": roof, "kernels": kernels, "profiled_device_ms": round(total, 2)}
+
+
+def active():
+    return _REC is not None
+
+
+def record(name, e0, e1, flops, nbytes):
+    _REC.items.append((name, e0, e1, float(flops), float(nbytes)))
+
+
+@contextlib.contextmanager
+def collect():
+    global _REC
+    rec = _Recorder()
+    _REC = rec
+    try:
+        yield rec
+    finally:
+        _REC = None

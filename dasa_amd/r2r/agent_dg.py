@@ -1,0 +1,673 @@
+"""Seq2SeqAgent / DGAdaChannel of r2r_src/agent_dg.py on the MI355X kernels.
+
+Same constructor, methods, attributes, `logs` keys and checkpoint schema as the reference
+(agent_dg.py:102-1510), so r2r_src/train.py drives it unchanged. The per-step policy math runs in
+libdasa_hip.so; the host loop keeps the reference's semantics (per-row env stepping, rewards, A2C).
+Deliberate differences, none observable by train.py:
+  * `.item()` logging syncs are deferred to the end of the rollout (same values, same order);
+  * if the env offers `device_input_feat(perm_obs)` the panorama blocks are gathered on the device
+    instead of numpy-assembled and copied (identical tensors);
+  * eval rollouts compute the (input-independent, detached) 9-layer language stack once per batch;
+  * data-parallel training: optim_step() all-reduces gradients over the default process group.
+"""
+import json
+import math
+import os
+import random
+import sys
+from collections import defaultdict
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import functional as DF
+from .. import ops
+from . import model
+from . import utils
+from .param import args
+from .r2rmodel import DicEncoder
+
+FEATURE_SIZE = 2048
+FEATURE_ALL_SIZE = 2176
+
+
+def _device():
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+class BaseAgent(object):
+    """agent_dg.py:31-100."""
+
+    def __init__(self, env, results_path):
+        self.env = env
+        self.results_path = results_path
+        random.seed(1)
+        self.results = {}
+        self.losses = []
+
+    def write_results(self):
+        output = [{"instr_id": k, "trajectory": v} for k, v in self.results.items()]
+        with open(self.results_path, "w") as f:
+            json.dump(output, f)
+
+    def get_results(self):
+        return [{"instr_id": k, "trajectory": v} for k, v in self.results.items()]
+
+    def rollout(self, **kwargs):
+        raise NotImplementedError
+
+    @staticmethod
+    def get_agent(name):
+        return globals()[name + "Agent"]
+
+    def test(self, iters=None, **kwargs):
+        args.is_test = True
+        self.env.reset_epoch(shuffle=(iters is not None))
+        self.losses = []
+        self.results = {}
+        looped = False
+        self.loss = 0
+        if iters is not None:
+            for _ in range(iters):
+                for traj in self.vl_rollout(**kwargs):
+                    self.loss = 0
+                    self.results[traj["instr_id"]] = traj["path"]
+        else:
+            while True:
+                for traj in self.vl_rollout(**kwargs):
+                    if traj["instr_id"] in self.results:
+                        looped = True
+                    else:
+                        self.loss = 0
+                        self.results[traj["instr_id"]] = traj["path"]
+                if looped:
+                    break
+        args.is_test = False
+
+
+class DGAdaChannel(nn.Module):
+    """agent_dg.py:1513-1547: a = sigmoid(a_fc(d)) (ab_type 'a'), out = a * f (+ b_fc(d) for 'ab'/'b').
+    ab_type 'a' + a_type 'sigmoid' (the README configuration) is one fused GEMM + gate epilogue."""
+
+    def __init__(self, channel, eps=1e-6):
+        super().__init__()
+        if args.ab_type in ["ab", "a"]:
+            self.a_fc = nn.Linear(channel, channel)
+        if args.ab_type in ["ab", "b"]:
+            self.b_fc = nn.Linear(channel, channel)
+        self.eps = eps
+
+    def fused_ok(self):
+        return args.ab_type == "a" and args.a_type == "sigmoid"
+
+    def forward(self, f_t, d_t):
+        if self.fused_ok():
+            s = DF.linear(d_t, self.a_fc.weight, self.a_fc.bias, "sigmoid")
+            return s * f_t
+        a, b = 1, 0
+        if args.ab_type in ["ab", "a"]:
+            a = DF.linear(d_t, self.a_fc.weight, self.a_fc.bias)
+        if args.ab_type in ["ab", "b"]:
+            b = DF.linear(d_t, self.b_fc.weight, self.b_fc.bias)
+        if args.a_type == "sigmoid":
+            a = torch.sigmoid(a)
+        elif args.a_type == "gumbel_sigmoid":
+            raise NotImplementedError("gumbel_sigmoid AdaIN is not in any DASA configuration")
+        return a * f_t + b
+
+    def feature(self, f_full, d_full, noise=None):
+        """df = f_full with its RGB columns replaced by forward(f, d) (* noise): one fused kernel chain."""
+        if self.fused_ok():
+            return DF.ada_feature(f_full, d_full, self.a_fc.weight, self.a_fc.bias, noise, args.angle_feat_size)
+        out = f_full.clone()
+        out[..., :-args.angle_feat_size] = self.forward(f_full[..., :-args.angle_feat_size],
+                                                        d_full[..., :-args.angle_feat_size])
+        if noise is not None:
+            out[..., :-args.angle_feat_size] *= noise
+        return out
+
+
+class Seq2SeqAgent(BaseAgent):
+    """agent_dg.py:102-1510 (encoder_type 'Dic' — the DASA configuration)."""
+
+    env_actions = {
+        "left": (0, -1, 0), "right": (0, 1, 0), "up": (0, 0, 1), "down": (0, 0, -1),
+        "forward": (1, 0, 0), "<end>": (0, 0, 0), "<start>": (0, 0, 0), "<ignore>": (0, 0, 0),
+    }
+
+    def __init__(self, env, results_path, tok, episode_len=20, encoder_type="EncoderLSTM"):
+        super().__init__(env, results_path)
+        self.tok = tok
+        self.episode_len = episode_len
+        self.feature_size = self.env.feature_size
+        self.encoder_type = encoder_type
+        self.device = _device()
+        if encoder_type in ("EncoderLSTM", "DicEncoder", "CEncoder"):
+            raise NotImplementedError("encoder_type %r is not the DASA (Dic) agent" % encoder_type)
+        self.encoder = DicEncoder(FEATURE_ALL_SIZE, args.d_enc_hidden_size, args.d_hidden_size, args.d_dropout_ratio,
+                                  args.d_bidirectional, args.d_transformer_update, args.d_bert_n_layers,
+                                  args.d_reverse_input, args.d_top_lstm, args.d_vl_layers, args.d_la_layers,
+                                  args.d_bert_type, update_add_layer=args.d_update_add_layer).to(self.device)
+        if args.pretrain_model_name is not None:
+            self._load_pretrained_bert(args.pretrain_model_name)
+        self.decoder = model.BAttnDecoderLSTM(args.aemb, args.d_hidden_size, args.dropout,
+                                              feature_size=self.feature_size + args.angle_feat_size,
+                                              pred_back=args.pred_back).to(self.device)
+        self.critic = model.Critic().to(self.device)
+        if args.adaIn_type in ("channel", "rgb_channel"):
+            self.adaIn = DGAdaChannel(args.feature_size).to(self.device)
+        elif args.adaIn_type in ("default", "none"):
+            self.adaIn = None
+        else:
+            raise NotImplementedError("adaIn_type %r is outside the DASA configurations" % args.adaIn_type)
+
+        self.encoder_optimizer = args.optimizer(self.encoder.parameters(), lr=args.lr, weight_decay=args.weight_decay)
+        self.decoder_optimizer = args.optimizer(self.decoder.parameters(), lr=args.lr, weight_decay=args.weight_decay)
+        self.critic_optimizer = args.optimizer(self.critic.parameters(), lr=args.lr, weight_decay=args.weight_decay)
+
+        def lr_lambda(it):   # agent_dg.py:219-227
+            if args.warm_steps > 0 and it < args.warm_steps:
+                return (1.0 + it) / args.warm_steps
+            if it < args.decay_start:
+                return 1.0
+            return args.lr_decay ** ((it - args.decay_start) // args.decay_intervals)
+
+        if args.use_lr_scheduler:
+            self.decoder_lr_scheduler = torch.optim.lr_scheduler.LambdaLR(self.decoder_optimizer, lr_lambda)
+            self.critic_lr_scheduler = torch.optim.lr_scheduler.LambdaLR(self.critic_optimizer, lr_lambda)
+        else:
+            self.decoder_lr_scheduler = None
+            self.critic_lr_scheduler = None
+        if args.adaIn_type not in ("default", "none"):
+            self.adaIn_optimizer = args.optimizer(self.adaIn.parameters(), lr=args.lr)
+            self.adaIn_lr_scheduler = torch.optim.lr_scheduler.LambdaLR(self.adaIn_optimizer, lr_lambda)
+            self.models = (self.encoder, self.decoder, self.critic, self.adaIn)
+            self.optimizers = (self.encoder_optimizer, self.decoder_optimizer, self.critic_optimizer,
+                               self.adaIn_optimizer)
+        else:
+            self.models = (self.encoder, self.decoder, self.critic)
+            self.optimizers = (self.encoder_optimizer, self.decoder_optimizer, self.critic_optimizer)
+        self.losses = []
+        self.criterion = nn.CrossEntropyLoss(ignore_index=args.ignoreid, reduction="sum")
+        self.logs = defaultdict(list)
+        self.sample_fn = None        # test hook: probs -> actions, replaces Categorical sampling
+        self.grad_sync = None        # data-parallel hook set by dasa_amd.dp
+
+    def _load_pretrained_bert(self, path):
+        """--pretrain_model_name: load `bert.*` weights from a local state dict file (safe loader)."""
+        fn = os.path.join(path, "pytorch_model.bin") if os.path.isdir(path) else path
+        sd = torch.load(fn, map_location="cpu", weights_only=True)
+        sd = sd.get("state_dict", sd)
+        bert_sd = {k[len("bert."):]: v for k, v in sd.items() if k.startswith("bert.")}
+        self.encoder.bert.load_state_dict(bert_sd, strict=False)
+
+    # ------------------------------------------------------------------ observation -> tensors
+    def _sort_batch(self, obs):
+        """agent_dg.py:262-284."""
+        seq_tensor = np.array([ob["instr_encoding"] for ob in obs])
+        seq_lengths = np.argmax(seq_tensor == utils.padding_idx, axis=1)
+        seq_lengths[seq_lengths == 0] = seq_tensor.shape[1]
+        seq_tensor = torch.from_numpy(seq_tensor)
+        seq_lengths = torch.from_numpy(seq_lengths)
+        seq_lengths, perm_idx = seq_lengths.sort(0, True)
+        sorted_tensor = seq_tensor[perm_idx]
+        mask = (sorted_tensor == utils.padding_idx)[:, :seq_lengths[0]]
+        progresses = torch.Tensor([ob["progress"] for ob in obs])[perm_idx].float().to(self.device)
+        return (sorted_tensor.long().to(self.device), mask.bool().to(self.device), list(seq_lengths),
+                list(perm_idx), progresses)
+
+    def _to_dev(self, arr):
+        return torch.from_numpy(arr).pin_memory().to(self.device, non_blocking=True)
+
+    def _feature_variable(self, obs):
+        features = np.empty((len(obs), args.views, self.feature_size + args.angle_feat_size), dtype=np.float32)
+        for i, ob in enumerate(obs):
+            features[i] = ob["feature"]
+        return self._to_dev(features)
+
+    def _dfeature_variable(self, obs):
+        dfeatures = np.empty((len(obs), args.views, self.feature_size + args.angle_feat_size), dtype=np.float32)
+        for i, ob in enumerate(obs):
+            dfeatures[i] = ob["dfeature"]
+        return self._to_dev(dfeatures)
+
+    def _candidate_variable(self, obs):
+        candidate_leng = [len(ob["candidate"]) + 1 for ob in obs]
+        cf = np.zeros((len(obs), max(candidate_leng), self.feature_size + args.angle_feat_size), dtype=np.float32)
+        cd = np.zeros_like(cf)
+        for i, ob in enumerate(obs):
+            for j, c in enumerate(ob["candidate"]):
+                cf[i, j] = c["feature"]
+                cd[i, j] = c["dfeature"]
+        return self._to_dev(cf), self._to_dev(cd), candidate_leng
+
+    def get_input_feat(self, obs):
+        """agent_dg.py:313-323; device-side gather when the env provides one."""
+        if hasattr(self.env, "device_input_feat"):
+            return self.env.device_input_feat(obs, self.device)
+        input_a_t = np.zeros((len(obs), args.angle_feat_size), np.float32)
+        for i, ob in enumerate(obs):
+            input_a_t[i] = utils.angle_feature(ob["heading"], ob["elevation"])
+        input_a_t = self._to_dev(input_a_t)
+        f_t = self._feature_variable(obs)
+        d_t = self._dfeature_variable(obs)
+        cf, cd, leng = self._candidate_variable(obs)
+        return input_a_t, f_t, d_t, cf, cd, leng
+
+    def _teacher_action(self, obs, ended):
+        a = np.zeros(len(obs), dtype=np.int64)
+        for i, ob in enumerate(obs):
+            if ended[i]:
+                a[i] = args.ignoreid
+            else:
+                for k, candidate in enumerate(ob["candidate"]):
+                    if candidate["viewpointId"] == ob["teacher"]:
+                        a[i] = k
+                        break
+                else:
+                    assert ob["teacher"] == ob["viewpoint"]
+                    a[i] = len(ob["candidate"])
+        return torch.from_numpy(a).to(self.device)
+
+    def _back_teacher_action(self, obs, ended):
+        a = np.zeros(len(obs), dtype=np.int64)
+        for i, ob in enumerate(obs):
+            for k, candidate in enumerate(ob["candidate"]):
+                if candidate["viewpointId"] == ob["back_teacher"]:
+                    a[i] = k
+                    break
+            else:
+                assert ob["back_teacher"] == ob["viewpoint"]
+                a[i] = len(ob["candidate"])
+        return torch.from_numpy(a).to(self.device)
+
+    def make_equiv_action(self, a_t, perm_obs, perm_idx=None, traj=None):
+        """agent_dg.py:358-391."""
+        def take_action(i, idx, name):
+            if type(name) is int:
+                self.env.env.sims[idx].makeAction(name, 0, 0)
+            else:
+                self.env.env.sims[idx].makeAction(*self.env_actions[name])
+            state = self.env.env.sims[idx].getState()
+            if traj is not None:
+                traj[i]["path"].append((state.location.viewpointId, state.heading, state.elevation))
+        if perm_idx is None:
+            perm_idx = range(len(perm_obs))
+        for i, idx in enumerate(perm_idx):
+            action = a_t[i]
+            if action != -1:
+                select_candidate = perm_obs[i]["candidate"][action]
+                src_point = perm_obs[i]["viewIndex"]
+                trg_point = select_candidate["pointId"]
+                src_level = src_point // 12
+                trg_level = trg_point // 12
+                while src_level < trg_level:
+                    take_action(i, idx, "up")
+                    src_level += 1
+                while src_level > trg_level:
+                    take_action(i, idx, "down")
+                    src_level -= 1
+                while self.env.env.sims[idx].getState().viewIndex != trg_point:
+                    take_action(i, idx, "right")
+                assert select_candidate["viewpointId"] == \
+                    self.env.env.sims[idx].getState().navigableLocations[select_candidate["idx"]].viewpointId
+                take_action(i, idx, select_candidate["idx"])
+
+    # ------------------------------------------------------------------ the rollout
+    def _noise_mult(self, x, noise):
+        """x[..., :-angle] *= noise, out of place (shared env-drop mask, agent_dg.py:731-736, 780-785)."""
+        out = torch.empty_like(x)
+        ops.colscale(x[..., :-args.angle_feat_size], noise, out[..., :-args.angle_feat_size])
+        ops.copy2d(x[..., -args.angle_feat_size:], out[..., -args.angle_feat_size:])
+        return out
+
+    def vl_rollout(self, train_ml=None, train_rl=True, reset=True, speaker=None):
+        """agent_dg.py:633-1033."""
+        if self.feedback == "teacher" or self.feedback == "argmax":
+            train_rl = False
+        obs = np.array(self.env.reset()) if reset else np.array(self.env._get_obs())
+        batch_size = len(obs)
+        noise = None
+        if speaker is not None:
+            noise = self.decoder.drop_env(torch.ones(self.feature_size, device=self.device))
+            batch = self.env.batch.copy()
+            speaker.env = self.env
+            insts = speaker.infer_batch(featdropmask=noise)
+            inst_lengths = np.argmax(insts == self.tok.tokenizer.pad_token_id, axis=1)
+            inst_lengths[inst_lengths == 0] = insts.shape[1]
+            for i, (datum, inst) in enumerate(zip(batch, insts)):
+                inst = inst[:inst_lengths[i]]
+                if inst[-1] == speaker.tok.word_to_index["<EOS>"]:
+                    inst = inst[:-1]
+                datum.pop("instructions")
+                datum.pop("instr_encoding")
+                datum["instructions"] = speaker.tok.decode_sentence(inst)
+                datum["instr_encoding"] = self.tok.encode_sentence(datum["instructions"])
+            obs = np.array(self.env.reset(batch))
+        elif args.consistent_drop:
+            noise = self.decoder.drop_env(torch.ones(self.feature_size, device=self.device))
+
+        seq, seq_mask, seq_lengths, perm_idx, progresses = self._sort_batch(obs)
+        perm_obs = obs[perm_idx]
+        ctx_mask = seq_mask
+        lens_dev = torch.as_tensor([int(x) for x in seq_lengths], dtype=torch.int32).to(self.device)
+        if not args.include_vision:
+            raise NotImplementedError("include_vision=False is not the DASA configuration")
+
+        last_dist = np.zeros(batch_size, np.float32)
+        for i, ob in enumerate(perm_obs):
+            last_dist[i] = ob["distance"]
+        traj = [{"instr_id": ob["instr_id"], "path": [(ob["viewpoint"], ob["heading"], ob["elevation"])]}
+                for ob in perm_obs]
+        visited = [set() for _ in perm_obs]
+        ended = np.array([False] * batch_size)
+        rewards, hidden_states, policy_log_probs, masks, entropys = [], [], [], [], []
+        deferred = defaultdict(list)     # logs whose .item() is taken after the loop
+        ml_loss = 0.0
+        total_forth_loss = 0.0
+        total_back_loss = 0.0
+        consistent_drop = args.consistent_drop or (speaker is not None)
+        if args.decoder_consistent_drop:
+            self.decoder.init_noise((seq.shape[0], args.d_enc_hidden_size))
+        self.encoder.cache_language(not self.encoder.training)
+        angle = args.angle_feat_size
+        h_t = c_t = h1 = ctx = None
+        for t in range(self.episode_len):
+            input_a_t, f_t, d_t, candidate_feat, candidate_dfeat, candidate_leng = self.get_input_feat(perm_obs)
+            stage = args.env_drop_stage
+            use_noise = consistent_drop and noise is not None
+            all_img_feats = f_t                  # the raw panorama (agent_dg.py:730)
+            df_t = f_t                           # df_t = f_t.clone() (agent_dg.py:728), copied lazily below
+            if use_noise and stage == "before_adain":     # agent_dg.py:731-736
+                candidate_feat = self._noise_mult(candidate_feat, noise)
+                f_t = self._noise_mult(f_t, noise)
+                if args.depth_drop:
+                    candidate_dfeat = self._noise_mult(candidate_dfeat, noise)
+                    df_t = f_t
+            after = use_noise and stage == "after_adain"
+            if args.adaIn_type in ("channel", "rgb_channel"):            # agent_dg.py:748-768
+                style_v = f_t if args.adaIn_type == "rgb_channel" else d_t
+                style_c = candidate_feat if args.adaIn_type == "rgb_channel" else candidate_dfeat
+                # df_t's angle columns are df_t's own (== f_t's); its RGB columns are replaced
+                df_t = self.adaIn.feature(f_t, style_v, noise if (after and args.depth_drop) else None)
+                candidate_feat = self.adaIn.feature(candidate_feat, style_c, noise if after else None)
+                if after:
+                    f_t = self._noise_mult(f_t, noise)
+            elif args.adaIn_type == "default":                             # agent_dg.py:774-777
+                f_t = f_t.clone()
+                model.adaptive_instance_normalization(f_t[..., :-angle], d_t[..., :-angle], out=f_t[..., :-angle])
+                candidate_feat = candidate_feat.clone()
+                model.adaptive_instance_normalization(candidate_feat[..., :-angle], candidate_dfeat[..., :-angle],
+                                                      out=candidate_feat[..., :-angle])
+                if after:                                                  # agent_dg.py:780-785
+                    candidate_feat = self._noise_mult(candidate_feat, noise)
+                    f_t = self._noise_mult(f_t, noise)
+                    if args.depth_drop:
+                        df_t = self._noise_mult(df_t, noise)
+            elif after:
+                candidate_feat = self._noise_mult(candidate_feat, noise)
+                f_t = self._noise_mult(f_t, noise)
+                if args.depth_drop:
+                    df_t = self._noise_mult(df_t, noise)
+            img = f_t if args.use_dropout_vision else all_img_feats
+            ctx, en_ht, en_ct, _, ctx_v = self.encoder(seq, mask=seq_mask, lengths=lens_dev, f_t_all=img)
+            if args.ctx_v:
+                df_t = df_t + ctx_v
+            if t == 0:
+                h_t, c_t, logit, h1, aux_outputs = self.decoder(input_a_t, df_t, candidate_feat, en_ht, en_ht, en_ct,
+                                                                ctx, ctx_mask, already_dropfeat=consistent_drop)
+            else:
+                h_t, c_t, logit, h1, aux_outputs = self.decoder(input_a_t, df_t, candidate_feat, h_t, h1, c_t, ctx,
+                                                                ctx_mask, already_dropfeat=consistent_drop)
+            hidden_states.append(h_t)
+            candidate_mask = utils.length2mask(candidate_leng, device=self.device)
+            if args.submit:
+                cm = candidate_mask.cpu()
+                for ob_id, ob in enumerate(perm_obs):
+                    visited[ob_id].add(ob["viewpoint"])
+                    for c_id, c in enumerate(ob["candidate"]):
+                        if c["viewpointId"] in visited[ob_id]:
+                            cm[ob_id][c_id] = 1
+                candidate_mask = cm.to(self.device)
+            logit = logit.masked_fill(candidate_mask, -float("inf"))
+            target = self._teacher_action(perm_obs, ended)
+            forth_loss = self.criterion(logit, target)
+            total_forth_loss += forth_loss
+            if args.pred_back:
+                back_logit = aux_outputs["back_logit"].masked_fill(candidate_mask, -float("inf"))
+                total_back_loss += self.criterion(back_logit, self._back_teacher_action(perm_obs, ended))
+            if self.feedback == "teacher":
+                a_t = target
+            elif self.feedback == "argmax":
+                _, a_t = logit.max(1)
+                a_t = a_t.detach()
+                policy_log_probs.append(F.log_softmax(logit, 1).gather(1, a_t.unsqueeze(1)))
+            elif self.feedback == "sample":
+                probs = F.softmax(logit, 1)
+                c = torch.distributions.Categorical(probs)
+                ent = c.entropy()
+                deferred["entropy"].append(ent.sum().detach())
+                entropys.append(ent)
+                a_t = (self.sample_fn(probs) if self.sample_fn is not None else c.sample()).detach()
+                policy_log_probs.append(c.log_prob(a_t))
+            else:
+                sys.exit("Invalid feedback option")
+            cpu_a_t = a_t.cpu().numpy().copy()      # the step's one device->host sync
+            for i, next_id in enumerate(cpu_a_t):
+                if next_id == (candidate_leng[i] - 1) or next_id == args.ignoreid:
+                    cpu_a_t[i] = -1
+            self.make_equiv_action(cpu_a_t, perm_obs, perm_idx, traj)
+            obs = np.array(self.env._get_obs())
+            perm_obs = obs[perm_idx]
+            dist = np.zeros(batch_size, np.float32)
+            reward = np.zeros(batch_size, np.float32)
+            mask = np.ones(batch_size, np.float32)
+            for i, ob in enumerate(perm_obs):
+                dist[i] = ob["distance"]
+                if ended[i]:
+                    reward[i] = 0.0
+                    mask[i] = 0.0
+                else:
+                    action_idx = cpu_a_t[i]
+                    if action_idx == -1:
+                        reward[i] = 2.0 if dist[i] < 3 else -2.0
+                    else:
+                        reward[i] = -(dist[i] - last_dist[i])
+                        if reward[i] > 0:
+                            reward[i] = 1
+                        elif reward[i] < 0:
+                            reward[i] = -1
+                        else:
+                            raise NameError("The action doesn't change the move")
+            rewards.append(reward)
+            masks.append(mask)
+            last_dist[:] = dist
+            ended[:] = np.logical_or(ended, (cpu_a_t == -1))
+            if ended.all():
+                break
+
+        if train_rl:
+            input_a_t, f_t, d_t, candidate_feat, candidate_dfeat, candidate_leng = self.get_input_feat(perm_obs)
+            if speaker is not None:
+                candidate_feat = self._noise_mult(candidate_feat, noise)
+                f_t = self._noise_mult(f_t, noise)
+            last_h_, _, _, _, _ = self.decoder(input_a_t, f_t, candidate_feat, h_t, h1, c_t, ctx, ctx_mask,
+                                               speaker is not None)
+            rl_loss = 0.0
+            last_value__ = self.critic(last_h_).detach().view(-1).cpu().numpy()
+            discount_reward = np.zeros(batch_size, np.float32)
+            for i in range(batch_size):
+                if not ended[i]:
+                    discount_reward[i] = last_value__[i]
+            length = len(rewards)
+            total = 0
+            for t in range(length - 1, -1, -1):
+                discount_reward = discount_reward * args.gamma + rewards[t]
+                mask_ = torch.from_numpy(masks[t]).to(self.device)
+                r_ = torch.from_numpy(discount_reward.copy()).to(self.device)
+                v_ = self.critic(hidden_states[t])
+                a_ = (r_ - v_).detach()
+                rl_loss += (-policy_log_probs[t].view(-1) * a_ * mask_).sum()
+                rl_loss += (((r_ - v_) ** 2) * mask_).sum() * 0.5
+                if self.feedback == "sample":
+                    rl_loss += (-0.01 * entropys[t] * mask_).sum()
+                deferred["critic_loss"].append((((r_ - v_) ** 2) * mask_).sum().detach())
+                total = total + np.sum(masks[t])
+            self.logs["total"].append(total)
+            if args.normalize_loss == "total":
+                rl_loss /= total
+            elif args.normalize_loss == "batch":
+                rl_loss /= batch_size
+            else:
+                assert args.normalize_loss == "none"
+            self.loss += rl_loss
+            deferred["normalized_rl_loss"].append(rl_loss.detach())
+
+        ml_loss += total_forth_loss
+        deferred["forth_loss"].append(total_forth_loss.detach())
+        if args.pred_back:
+            ml_loss += args.back_weight * total_back_loss
+            deferred["back_loss"].append(args.back_weight * total_back_loss.detach())
+        self.logs["viewsteps/{}".format(self.feedback)].append(len(rewards))
+        if train_ml is not None:
+            self.loss += ml_loss * train_ml / batch_size
+            deferred["normalized_supervised_loss"].append((ml_loss * train_ml / batch_size).detach())
+        deferred["ml_loss"].append(ml_loss.detach())
+        # flush the deferred scalars with one host sync, in the reference's key order
+        keys = [k for k in ("entropy", "critic_loss", "total", "normalized_rl_loss", "forth_loss", "back_loss",
+                            "normalized_supervised_loss", "ml_loss") if k in deferred]
+        flat = [v for k in keys for v in deferred[k]]
+        if flat:
+            vals = torch.stack([v.float().reshape(()) for v in flat]).cpu().tolist()
+            i = 0
+            for k in keys:
+                for _ in deferred[k]:
+                    self.logs[k].append(vals[i])
+                    i += 1
+        if type(self.loss) is int:
+            self.losses.append(0.0)
+        else:
+            self.losses.append(float(self.loss.item()) / self.episode_len)
+        self.last_rollout_steps = len(rewards)
+        return traj
+
+    # ------------------------------------------------------------------ training API
+    def test(self, use_dropout=False, feedback="argmax", allow_cheat=False, iters=None):
+        self.feedback = feedback
+        for m in (self.encoder, self.decoder, self.critic):
+            m.train() if use_dropout else m.eval()
+        with torch.no_grad():
+            super().test(iters)
+
+    def zero_grad(self):
+        self.loss = 0.0
+        self.losses = []
+        for m, opt in zip(self.models, self.optimizers):
+            m.train()
+            opt.zero_grad()
+
+    def accumulate_gradient(self, feedback="teacher", **kwargs):
+        """agent_dg.py:1347-1384."""
+        if args.schedule_ratio == -1:
+            if feedback == "teacher":
+                self.feedback = "teacher"
+                self.vl_rollout(train_ml=args.teacher_weight, train_rl=False, **kwargs)
+            elif feedback == "sample":
+                self.feedback = "teacher"
+                self.vl_rollout(train_ml=args.ml_weight, train_rl=False, **kwargs)
+                self.feedback = "sample"
+                self.vl_rollout(train_ml=None, train_rl=True, **kwargs)
+            else:
+                assert False
+        else:
+            feedback = random.choices(["sample", "teacher"], [args.schedule_ratio, 1 - args.schedule_ratio], k=1)[0]
+            if feedback == "teacher":
+                self.feedback = "teacher"
+                self.vl_rollout(train_ml=args.teacher_weight, train_rl=False, **kwargs)
+            else:
+                self.feedback = "sample"
+                self.vl_rollout(train_ml=None, train_rl=True, **kwargs)
+
+    def optim_step(self, **kwargs):
+        """agent_dg.py:1389-1405 (+ data-parallel gradient all-reduce before clipping)."""
+        self.loss.backward()
+        if self.grad_sync is not None:
+            self.grad_sync()
+        torch.nn.utils.clip_grad_norm_(self.encoder.parameters(), 40.0)
+        torch.nn.utils.clip_grad_norm_(self.decoder.parameters(), 40.0)
+        self.encoder_optimizer.step()
+        self.decoder_optimizer.step()
+        self.critic_optimizer.step()
+        if args.adaIn_type not in ("default", "none"):
+            self.adaIn_optimizer.step()
+        if args.use_lr_scheduler:
+            self.decoder_lr_scheduler.step()
+            self.critic_lr_scheduler.step()
+            if args.adaIn_type not in ("default", "none"):
+                self.adaIn_lr_scheduler.step()
+
+    def train(self, n_iters, feedback="teacher", **kwargs):
+        """agent_dg.py:1407-1464."""
+        self.feedback = feedback
+        for m in (self.encoder, self.decoder, self.critic):
+            m.train()
+        self.losses = []
+        for _ in range(1, n_iters + 1):
+            self.encoder_optimizer.zero_grad()
+            self.decoder_optimizer.zero_grad()
+            self.critic_optimizer.zero_grad()
+            self.loss = 0
+            if args.schedule_ratio == -1:
+                if feedback == "teacher":
+                    self.feedback = "teacher"
+                    self.vl_rollout(train_ml=args.teacher_weight, train_rl=False, **kwargs)
+                elif feedback == "sample":
+                    if args.ml_weight != 0:
+                        self.feedback = "teacher"
+                        self.vl_rollout(train_ml=args.ml_weight, train_rl=False, **kwargs)
+                    self.feedback = "sample"
+                    self.vl_rollout(train_ml=None, train_rl=True, **kwargs)
+                else:
+                    assert False
+            else:
+                fb = random.choices(["sample", "teacher"], [args.schedule_ratio, 1 - args.schedule_ratio], k=1)[0]
+                self.feedback = fb
+                self.vl_rollout(train_ml=args.teacher_weight if fb == "teacher" else None, train_rl=fb == "sample",
+                                **kwargs)
+            self.optim_step()
+
+    def save(self, epoch, path):
+        """agent_dg.py:1466-1487 (same checkpoint schema)."""
+        the_dir, _ = os.path.split(path)
+        if the_dir:
+            os.makedirs(the_dir, exist_ok=True)
+        states = {}
+        items = [("encoder", self.encoder, self.encoder_optimizer), ("decoder", self.decoder, self.decoder_optimizer),
+                 ("critic", self.critic, self.critic_optimizer)]
+        if args.adaIn_type not in ("default", "none"):
+            items.append(("adaIn", self.adaIn, self.adaIn_optimizer))
+        for name, m, opt in items:
+            states[name] = {"epoch": epoch + 1, "state_dict": m.state_dict(), "optimizer": opt.state_dict()}
+        torch.save(states, path)
+
+    def load(self, path):
+        """agent_dg.py:1489-1510."""
+        states = torch.load(path, map_location=self.device, weights_only=True)
+
+        def recover_state(name, m, opt):
+            state = m.state_dict()
+            if set(state.keys()) != set(states[name]["state_dict"].keys()):
+                print("NOTICE: DIFFERENT KEYS IN THE LISTEREN")
+            state.update(states[name]["state_dict"])
+            m.load_state_dict(state)
+            if args.loadOptim:
+                opt.load_state_dict(states[name]["optimizer"])
+        items = [("encoder", self.encoder, self.encoder_optimizer), ("decoder", self.decoder, self.decoder_optimizer),
+                 ("critic", self.critic, self.critic_optimizer)]
+        if args.adaIn_type not in ("default", "none"):
+            items.append(("adaIn", self.adaIn, self.adaIn_optimizer))
+        for it in items:
+            recover_state(*it)
+        return states["encoder"]["epoch"] - 1

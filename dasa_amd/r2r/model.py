@@ -1,0 +1,169 @@
+"""Policy heads of r2r_src/model.py on the MI355X kernels: SoftDotAttention, ShiftSoftDotAttention,
+BAttnDecoderLSTM, Critic and the mu/sigma AdaIN.
+
+Parameters are held in the same nn.Linear / nn.LSTMCell containers as the reference, so state_dict keys
+and shapes are identical; forward() never calls those containers — it runs the HIP
+kernels through dasa_amd.functional. Removed by design (no caller observes them): the in-place dropout
+on the caller's `feature` / `cand_feat` (model.py:508, 557) — the dropped copies are local here.
+"""
+import torch
+import torch.nn as nn
+
+from .. import functional as DF
+from .. import ops
+from .param import args
+
+
+class SoftDotAttention(nn.Module):
+    """model.py:253-296."""
+
+    def __init__(self, query_dim, ctx_dim):
+        super().__init__()
+        self.linear_in = nn.Linear(query_dim, ctx_dim, bias=False)
+        self.sm = nn.Softmax(dim=1)
+        self.linear_out = nn.Linear(query_dim + ctx_dim, query_dim, bias=False)
+        self.tanh = nn.Tanh()
+
+    def forward(self, h, context, mask=None, output_tilde=True, output_prob=True):
+        if output_tilde and output_prob:
+            return DF.SoftDotTildeFn.apply(h, context, mask, self.linear_in.weight, self.linear_out.weight)
+        if not output_tilde and not output_prob and mask is None:
+            logit = DF.CandLogitFn.apply(h, context, self.linear_in.weight)
+            q = ops.linear(h.detach(), self.linear_in.weight.detach())
+            wctx = ops.softdot_fwd(q, context.detach(), None)[2]     # unused by the decoder (model.py:559)
+            return wctx, logit
+        # general combination (not on the README path)
+        q = DF.linear(h, self.linear_in.weight)
+        scores = torch.einsum("bnd,bd->bn", context, q)
+        if mask is not None:
+            scores = scores.masked_fill(mask.bool(), -float("inf"))
+        p = torch.softmax(scores, 1)
+        wctx = torch.einsum("bn,bnd->bd", p, context)
+        attn = p if output_prob else scores
+        if output_tilde:
+            return DF.linear(torch.cat((wctx, h), 1), self.linear_out.weight, None, "tanh"), attn
+        return wctx, attn
+
+    def logits(self, h, cand):
+        """Raw candidate scores (output_tilde=False, output_prob=False) without the unused wctx."""
+        return DF.CandLogitFn.apply(h, cand, self.linear_in.weight)
+
+
+class ShiftSoftDotAttention(nn.Module):
+    """model.py:300-353: soft attention over the 36 views followed by a learned K-tap circular shift
+    along each of the 3 elevation rows."""
+
+    def __init__(self, query_dim, ctx_dim, kernel_size=3):
+        super().__init__()
+        self.linear_in = nn.Linear(query_dim, ctx_dim, bias=False)
+        self.linear_shift = nn.Linear(query_dim, kernel_size)
+        self.sm = nn.Softmax(dim=1)
+        self.linear_out = nn.Linear(query_dim + ctx_dim, query_dim, bias=False)
+        self.tanh = nn.Tanh()
+        self.kernel_size = kernel_size
+        self.padding_size = kernel_size // 2
+
+    def forward(self, h, context, mask=None, output_tilde=True, output_prob=True):
+        if mask is not None:
+            raise NotImplementedError("masked shift attention is not used by the reference decoder")
+        if context.shape[1] != 36:
+            raise ValueError("ShiftSoftDotAttention expects the 36-view panorama (3 x 12)")
+        wctx, attn = DF.ShiftAttnFn.apply(h, context.contiguous(), self.linear_in.weight, self.linear_shift.weight,
+                                          self.linear_shift.bias)
+        if not output_prob:
+            attn = torch.einsum("bnd,bd->bn", context, ops.linear(h.detach(), self.linear_in.weight.detach()))
+        if output_tilde:
+            return DF.linear(torch.cat((wctx, h), 1), self.linear_out.weight, None, "tanh"), attn
+        return wctx, attn
+
+
+class BAttnDecoderLSTM(nn.Module):
+    """model.py:422-574 (use_shift / pred_back / decoder_consistent_drop supported; pred_pm is not)."""
+
+    def __init__(self, embedding_size, hidden_size, dropout_ratio, feature_size=2048 + 4, pred_back=False):
+        super().__init__()
+        self.embedding_size = embedding_size
+        self.feature_size = feature_size
+        self.hidden_size = hidden_size
+        self.embedding = nn.Sequential(nn.Linear(args.angle_feat_size, self.embedding_size), nn.Tanh())
+        self.drop = nn.Dropout(p=dropout_ratio)
+        self.drop_env = nn.Dropout(p=args.featdropout)
+        self.lstm = nn.LSTMCell(embedding_size + feature_size, hidden_size)
+        if args.use_shift:
+            self.feat_att_layer = ShiftSoftDotAttention(hidden_size, feature_size, args.shift_kernel_size)
+        else:
+            self.feat_att_layer = SoftDotAttention(hidden_size, feature_size)
+        self.attention_layer = SoftDotAttention(hidden_size, hidden_size * 2)
+        self.candidate_att_layer = SoftDotAttention(hidden_size, feature_size)
+        self.pred_back = pred_back
+        if self.pred_back:
+            self.back_candidate_att_layer = SoftDotAttention(hidden_size, feature_size)
+        self.pred_pm = args.pred_pm
+        if self.pred_pm:
+            raise NotImplementedError("--pred_pm progress monitor is outside the DASA hot path")
+        self.input_noise = None
+        self.output_noise = None
+
+    def init_noise(self, shape):
+        dev = self.lstm.weight_hh.device
+        self.input_noise = self.drop(torch.ones(shape, device=dev))
+        self.output_noise = self.drop(torch.ones(shape, device=dev))
+
+    def forward(self, action, feature, cand_feat, h_0, prev_h1, c_0, ctx, ctx_mask=None, already_dropfeat=False):
+        training = self.training
+        p, pf = self.drop.p, self.drop_env.p
+        angle = args.angle_feat_size
+        aux_outputs = {}
+        a_emb = DF.linear(action, self.embedding[0].weight, self.embedding[0].bias, "tanh")
+        a_emb = DF.dropout(a_emb, p, training)
+        if not already_dropfeat:
+            feature = DF.feat_drop(feature, pf, training, angle)
+        prev_h1_drop = DF.dropout(prev_h1, p, training)
+        attn_feat, _ = self.feat_att_layer(prev_h1_drop, feature, output_tilde=False)
+        h_1, c_1 = DF.LSTMCellFn.apply(a_emb, attn_feat, prev_h1, c_0, self.lstm.weight_ih, self.lstm.weight_hh,
+                                       self.lstm.bias_ih, self.lstm.bias_hh)
+        if args.decoder_consistent_drop:
+            h_1_drop = h_1 * self.input_noise
+        else:
+            h_1_drop = DF.dropout(h_1, p, training)
+        h_tilde, alpha = self.attention_layer(h_1_drop, ctx, ctx_mask)
+        if args.decoder_consistent_drop:
+            h_tilde_drop = h_tilde * self.output_noise
+        else:
+            h_tilde_drop = DF.dropout(h_tilde, p, training)
+        if not already_dropfeat:
+            cand_feat = DF.feat_drop(cand_feat, pf, training, angle)
+        logit = self.candidate_att_layer.logits(h_tilde_drop, cand_feat)
+        if self.pred_back:
+            q = prev_h1 if args.back_input == "pre" else h_tilde_drop
+            aux_outputs["back_logit"] = self.back_candidate_att_layer.logits(q, cand_feat)
+        return h_1, c_1, logit, h_tilde, aux_outputs
+
+
+class Critic(nn.Module):
+    """model.py:970-982."""
+
+    def __init__(self):
+        super().__init__()
+        self.dim = args.critic_dim
+        self.state2value = nn.Sequential(nn.Linear(self.dim, self.dim), nn.ReLU(), nn.Dropout(args.dropout),
+                                         nn.Linear(self.dim, 1))
+
+    def forward(self, state):
+        l0, drop, l3 = self.state2value[0], self.state2value[2], self.state2value[3]
+        x = DF.linear(state, l0.weight, l0.bias, "relu")
+        x = DF.dropout(x, drop.p, self.training)
+        return DF.linear(x, l3.weight, l3.bias).squeeze()
+
+
+def calc_mean_std(feat, eps=1e-5, dim=-1):
+    """model.py:1822-1830 (returned for API parity; the fused kernel below does not need it)."""
+    assert feat.dim() == 3
+    var = feat.var(dim=dim, keepdim=True) + eps
+    return feat.mean(dim=dim, keepdim=True), var.sqrt()
+
+
+def adaptive_instance_normalization(content_feat, style_feat, out=None):
+    """model.py:1832-1840, one wave per row (two wave-shuffle reductions per operand) on gfx950."""
+    assert content_feat.size() == style_feat.size()
+    return ops.adain_musigma(content_feat, style_feat, out=out)

@@ -1,0 +1,118 @@
+"""DicEncoder of r2r_src/r2rmodel.py:2199-2365 on the MI355X kernels.
+
+DicModel (language stack + vision encoder + LXRT layers) -> reverse the valid tokens -> packed
+bidirectional LSTM (one MFMA GEMM for the input projection of all timesteps, one fused recurrence
+kernel per timestep) -> decoder init projections. `cache_language(True)` lets callers that run many
+steps on the same instruction batch (eval rollouts) compute the 9 language layers once — exact, since
+that stack is input-independent of the panorama and detached (vilmodel.py:1377-1378).
+"""
+import torch
+import torch.nn as nn
+
+from .. import functional as DF
+from .. import ops
+from .param import args
+from .vilmodel import BertConfig, DicModel
+
+
+class ReverseFn(torch.autograd.Function):
+    """r2rmodel.py:2326-2330 token reversal; a permutation, so its backward is the same reversal."""
+
+    @staticmethod
+    def forward(ctx, x, lens_i32):
+        ctx.save_for_backward(lens_i32)
+        return ops.reverse_valid(x, lens_i32)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (lens,) = ctx.saved_tensors
+        return ops.reverse_valid(dy.contiguous(), lens), None
+
+
+class DicEncoder(nn.Module):
+    lstm_num_layers = 1
+
+    def __init__(self, vision_size, hidden_size, dec_hidden_size, dropout_ratio, bidirectional, update,
+                 bert_n_layers, reverse_input, top_lstm, vl_layers, la_layers, bert_type="small",
+                 update_add_layer=True):
+        super().__init__()
+        if not (bidirectional and top_lstm and bert_n_layers == 1):
+            raise NotImplementedError("DicEncoder is built for the DASA configuration: bidirectional top LSTM, "
+                                      "bert_n_layers=1")
+        self.hidden_size = hidden_size
+        self.dec_hidden_size = dec_hidden_size
+        self.dropout_ratio = dropout_ratio
+        self.drop = nn.Dropout(p=dropout_ratio)
+        self.update = update
+        self.bert_n_layers = bert_n_layers
+        self.reverse_input = reverse_input
+        self.top_lstm = top_lstm
+        self.bert_type = bert_type
+        self.vl_layers = vl_layers
+        self.la_layers = la_layers
+        self.config = BertConfig.from_pretrained("bert-large-uncased" if bert_type == "large" else "bert-base-uncased")
+        self.config.img_feature_dim = vision_size
+        self.config.img_feature_type = ""
+        self.config.update_lang_bert = update
+        self.config.update_add_layer = update_add_layer
+        self.config.vl_layers = vl_layers
+        self.config.la_layers = la_layers
+        self.bert = DicModel(self.config)
+        self.transformer_hidden_size = self.config.hidden_size
+        self.lstm = nn.LSTM(self.transformer_hidden_size * bert_n_layers, hidden_size, 1, batch_first=True,
+                            bidirectional=bidirectional)
+        self.num_directions = 2
+        self.linear_n_in = hidden_size * self.num_directions
+        self.encoder2decoder_ht = nn.Linear(self.linear_n_in, dec_hidden_size)
+        self.encoder2decoder_ct = nn.Linear(self.linear_n_in, dec_hidden_size)
+        self.encoder_lstm2decoder_ht = nn.Linear(hidden_size * self.num_directions, dec_hidden_size)
+        self.encoder_lstm2decoder_ct = nn.Linear(hidden_size * self.num_directions, dec_hidden_size)
+        if args.ctx_v:
+            self.ctx_v_to_v = nn.Linear(self.transformer_hidden_size, 2048 + args.angle_feat_size)
+        self._lang_cache_on = False
+        self._lang_cache = None
+
+    # ------------------------------------------------------------------ language-stack cache
+    def cache_language(self, on=True):
+        self._lang_cache_on = on
+        self._lang_cache = None
+
+    def _language(self, ids, att_mask):
+        bert = self.bert
+        trainable = bert.update_lang_bert and torch.is_grad_enabled()
+        if self._lang_cache_on and not trainable and not bert.training:
+            key = (ids.data_ptr(), tuple(ids.shape), ids._version, att_mask.data_ptr())
+            if self._lang_cache is None or self._lang_cache[0] != key:
+                ext = ((1.0 - att_mask.float()) * -10000.0).unsqueeze(1).unsqueeze(2)
+                with torch.no_grad():
+                    self._lang_cache = (key, bert.language(ids, ext))
+            return self._lang_cache[1]
+        return None
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, inputs, mask, lengths, f_t_all=None):
+        B = inputs.size(0)
+        L = mask.size(1)
+        att_mask = ~mask
+        ids = inputs[:, :L]
+        text = self._language(ids, att_mask)
+        embeds, pooled, vision_outputs = self.bert(ids, None, att_mask, img_feats=f_t_all, text_embeds=text)
+        if not self.config.update_add_layer:
+            embeds = embeds.detach()
+        lens = lengths if torch.is_tensor(lengths) else torch.as_tensor(list(lengths))
+        lens_i32 = lens.to(device=embeds.device, dtype=torch.int32)
+        if self.reverse_input:
+            embeds = ReverseFn.apply(embeds.contiguous(), lens_i32)
+        l = self.lstm
+        out, h_n, c_n = DF.BiLSTMFn.apply(embeds.contiguous(), lens_i32, l.weight_ih_l0, l.weight_hh_l0, l.bias_ih_l0,
+                                          l.bias_hh_l0, l.weight_ih_l0_reverse, l.weight_hh_l0_reverse,
+                                          l.bias_ih_l0_reverse, l.bias_hh_l0_reverse)
+        h_t = torch.cat((h_n[1], h_n[0]), 1)          # (enc_h_t[-1], enc_h_t[-2]) = [bwd, fwd]
+        c_t = torch.cat((c_n[1], c_n[0]), 1)
+        decoder_init = DF.linear(h_t, self.encoder_lstm2decoder_ht.weight, self.encoder_lstm2decoder_ht.bias, "tanh")
+        if self.hidden_size * self.num_directions != self.dec_hidden_size:
+            c_t = DF.linear(c_t, self.encoder_lstm2decoder_ct.weight, self.encoder_lstm2decoder_ct.bias)
+        ctx = DF.dropout(out, self.drop.p, self.training)
+        if args.ctx_v:
+            vision_outputs = DF.linear(vision_outputs, self.ctx_v_to_v.weight, self.ctx_v_to_v.bias)
+        return ctx, decoder_init, c_t, mask, vision_outputs

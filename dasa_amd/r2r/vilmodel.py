@@ -1,0 +1,333 @@
+"""BERT / LXMERT blocks of r2r_src/vilmodel.py used by DicModel, on the MI355X kernels.
+
+Same module tree and parameter names as the reference (so `bert.*` checkpoints load unchanged);
+forward() runs fused HIP kernels: MFMA GEMMs with bias/GELU epilogues (dasa_gemm_f32), a fused
+dropout+residual+LayerNorm (dasa_layernorm_fwd) and a per-(batch, head) LDS-resident masked
+attention core (dasa_mha_fwd). Attention masks arrive in the reference's additive extended form
+[B, 1, 1, L] (0 / -10000).
+"""
+import math
+
+import torch
+import torch.nn as nn
+
+from .. import functional as DF
+from .. import ops
+from .param import args
+
+BertLayerNorm = nn.LayerNorm   # vilmodel.py:141-145 (apex is bypassed there too)
+
+
+class BertConfig:
+    """bert-base-uncased hyper-parameters (the values BertConfig.from_pretrained('bert-base-uncased')
+    yields, r2rmodel.py:2229), built locally: no network."""
+
+    _BASE = dict(vocab_size=30522, hidden_size=768, num_hidden_layers=12, num_attention_heads=12,
+                 intermediate_size=3072, hidden_act="gelu", hidden_dropout_prob=0.1,
+                 attention_probs_dropout_prob=0.1, max_position_embeddings=512, type_vocab_size=2,
+                 initializer_range=0.02, layer_norm_eps=1e-12, output_attentions=False,
+                 output_hidden_states=False)
+
+    def __init__(self, **kw):
+        for k, v in dict(self._BASE, **kw).items():
+            setattr(self, k, v)
+
+    @classmethod
+    def from_pretrained(cls, name="bert-base-uncased", **kw):
+        if "large" in str(name):
+            kw = dict(dict(hidden_size=1024, num_hidden_layers=24, num_attention_heads=16, intermediate_size=4096), **kw)
+        return cls(**kw)
+
+
+def gelu(x):
+    """vilmodel.py:125-131 (exact erf form) on the device."""
+    return ops.act_fwd(x, "gelu")
+
+
+def _addmask(mask, B):
+    """[B,1,1,L] additive -> [B, L] contiguous (or None)."""
+    if mask is None:
+        return None
+    return mask.reshape(B, -1).contiguous().float()
+
+
+def _lin(x, m, act=None):
+    return DF.linear(x, m.weight, m.bias, act)
+
+
+class BertEmbeddings(nn.Module):
+    """vilmodel.py:147-176: word + position + token_type(0) -> LayerNorm -> dropout, one kernel."""
+
+    def __init__(self, config):
+        super().__init__()
+        self.word_embeddings = nn.Embedding(config.vocab_size, config.hidden_size, padding_idx=0)
+        self.position_embeddings = nn.Embedding(config.max_position_embeddings, config.hidden_size)
+        self.token_type_embeddings = nn.Embedding(config.type_vocab_size, config.hidden_size)
+        self.LayerNorm = BertLayerNorm(config.hidden_size, eps=config.layer_norm_eps)
+        self.dropout = nn.Dropout(config.hidden_dropout_prob)
+
+    def forward(self, input_ids, token_type_ids=None, position_ids=None):
+        if position_ids is not None or (token_type_ids is not None and bool((token_type_ids != 0).any())):
+            raise NotImplementedError("explicit position ids / non-zero token types are not on the DASA path")
+        p = self.dropout.p if self.training else 0.0
+        return ops.bert_embed(input_ids, self.word_embeddings.weight, self.position_embeddings.weight,
+                              self.token_type_embeddings.weight[0], self.LayerNorm.weight, self.LayerNorm.bias,
+                              self.LayerNorm.eps, p, DF.new_seed() if p > 0 else 0)
+
+
+class BertSelfAttention(nn.Module):
+    """vilmodel.py:179-236."""
+
+    def __init__(self, config):
+        super().__init__()
+        if config.hidden_size % config.num_attention_heads != 0:
+            raise ValueError("hidden size not a multiple of heads")
+        self.output_attentions = config.output_attentions
+        self.num_attention_heads = config.num_attention_heads
+        self.attention_head_size = int(config.hidden_size / config.num_attention_heads)
+        self.all_head_size = self.num_attention_heads * self.attention_head_size
+        self.query = nn.Linear(config.hidden_size, self.all_head_size)
+        self.key = nn.Linear(config.hidden_size, self.all_head_size)
+        self.value = nn.Linear(config.hidden_size, self.all_head_size)
+        self.dropout = nn.Dropout(config.attention_probs_dropout_prob)
+
+    def forward(self, hidden_states, attention_mask, head_mask=None):
+        if head_mask is not None:
+            raise NotImplementedError("head_mask")
+        q, k, v = _lin(hidden_states, self.query), _lin(hidden_states, self.key), _lin(hidden_states, self.value)
+        ctx = DF.mha(q, k, v, _addmask(attention_mask, q.shape[0]), self.num_attention_heads,
+                     1.0 / math.sqrt(self.attention_head_size), self.dropout.p, self.training)
+        return (ctx,)
+
+
+class BertSelfOutput(nn.Module):
+    """vilmodel.py:239-250: LayerNorm(dropout(dense(h)) + input) — dropout+residual+LN fused."""
+
+    def __init__(self, config):
+        super().__init__()
+        self.dense = nn.Linear(config.hidden_size, config.hidden_size)
+        self.LayerNorm = BertLayerNorm(config.hidden_size, eps=config.layer_norm_eps)
+        self.dropout = nn.Dropout(config.hidden_dropout_prob)
+
+    def forward(self, hidden_states, input_tensor):
+        return DF.layer_norm(_lin(hidden_states, self.dense), self.LayerNorm.weight, self.LayerNorm.bias,
+                             self.LayerNorm.eps, res=input_tensor, p=self.dropout.p, training=self.training)
+
+
+class BertAttention(nn.Module):
+    """vilmodel.py:253-280."""
+
+    def __init__(self, config):
+        super().__init__()
+        self.self = BertSelfAttention(config)
+        self.output = BertSelfOutput(config)
+
+    def forward(self, input_tensor, attention_mask, head_mask=None):
+        s = self.self(input_tensor, attention_mask, head_mask)
+        return (self.output(s[0], input_tensor),) + s[1:]
+
+
+class BertIntermediate(nn.Module):
+    """vilmodel.py:283-293: GELU fused into the GEMM epilogue."""
+
+    def __init__(self, config):
+        super().__init__()
+        self.dense = nn.Linear(config.hidden_size, config.intermediate_size)
+        if config.hidden_act != "gelu":
+            raise NotImplementedError("only the gelu BERT configuration is on the DASA path")
+
+    def forward(self, hidden_states):
+        return _lin(hidden_states, self.dense, "gelu")
+
+
+class BertOutput(nn.Module):
+    """vilmodel.py:296-309."""
+
+    def __init__(self, config):
+        super().__init__()
+        self.dense = nn.Linear(config.intermediate_size, config.hidden_size)
+        self.LayerNorm = BertLayerNorm(config.hidden_size, eps=config.layer_norm_eps)
+        self.dropout = nn.Dropout(config.hidden_dropout_prob)
+
+    def forward(self, hidden_states, input_tensor):
+        return DF.layer_norm(_lin(hidden_states, self.dense), self.LayerNorm.weight, self.LayerNorm.bias,
+                             self.LayerNorm.eps, res=input_tensor, p=self.dropout.p, training=self.training)
+
+
+class BertLayer(nn.Module):
+    """vilmodel.py:312-325."""
+
+    def __init__(self, config):
+        super().__init__()
+        self.attention = BertAttention(config)
+        self.intermediate = BertIntermediate(config)
+        self.output = BertOutput(config)
+
+    def forward(self, hidden_states, attention_mask, head_mask=None):
+        a = self.attention(hidden_states, attention_mask, head_mask)
+        return (self.output(self.intermediate(a[0]), a[0]),) + a[1:]
+
+
+class BertPooler(nn.Module):
+    """vilmodel.py:360-372."""
+
+    def __init__(self, config):
+        super().__init__()
+        self.dense = nn.Linear(config.hidden_size, config.hidden_size)
+        self.activation = nn.Tanh()
+
+    def forward(self, hidden_states):
+        return _lin(hidden_states[:, 0], self.dense, "tanh")
+
+
+class BertOutAttention(nn.Module):
+    """vilmodel.py:455-506: attention of `hidden_states` (queries) over `context` (keys/values)."""
+
+    def __init__(self, config, ctx_dim=None):
+        super().__init__()
+        self.num_attention_heads = config.num_attention_heads
+        self.attention_head_size = int(config.hidden_size / config.num_attention_heads)
+        self.all_head_size = self.num_attention_heads * self.attention_head_size
+        ctx_dim = config.hidden_size if ctx_dim is None else ctx_dim
+        self.query = nn.Linear(config.hidden_size, self.all_head_size)
+        self.key = nn.Linear(ctx_dim, self.all_head_size)
+        self.value = nn.Linear(ctx_dim, self.all_head_size)
+        self.dropout = nn.Dropout(config.attention_probs_dropout_prob)
+
+    def forward(self, hidden_states, context, attention_mask=None):
+        q, k, v = _lin(hidden_states, self.query), _lin(context, self.key), _lin(context, self.value)
+        return DF.mha(q, k, v, _addmask(attention_mask, q.shape[0]), self.num_attention_heads,
+                      1.0 / math.sqrt(self.attention_head_size), self.dropout.p, self.training)
+
+
+class BertXAttention(nn.Module):
+    """vilmodel.py:443-452."""
+
+    def __init__(self, config, ctx_dim=None):
+        super().__init__()
+        self.att = BertOutAttention(config, ctx_dim=ctx_dim)
+        self.output = BertSelfOutput(config)
+
+    def forward(self, input_tensor, ctx_tensor, ctx_att_mask=None):
+        return self.output(self.att(input_tensor, ctx_tensor, ctx_att_mask), input_tensor)
+
+
+class LXRTXLayer(nn.Module):
+    """vilmodel.py:1014-1064: cross attention (ONE shared visual_attention for both directions),
+    then self attention and FFN on each stream."""
+
+    def __init__(self, config):
+        super().__init__()
+        self.lang_self_att = BertAttention(config)
+        self.lang_inter = BertIntermediate(config)
+        self.lang_output = BertOutput(config)
+        self.visn_self_att = BertAttention(config)
+        self.visn_inter = BertIntermediate(config)
+        self.visn_output = BertOutput(config)
+        self.visual_attention = BertXAttention(config)
+
+    def cross_att(self, lang_input, lang_attention_mask, visn_input, visn_attention_mask):
+        lang_att = self.visual_attention(lang_input, visn_input, ctx_att_mask=visn_attention_mask)
+        visn_att = self.visual_attention(visn_input, lang_input, ctx_att_mask=lang_attention_mask)
+        return lang_att, visn_att
+
+    def self_att(self, lang_input, lang_attention_mask, visn_input, visn_attention_mask):
+        return self.lang_self_att(lang_input, lang_attention_mask), self.visn_self_att(visn_input, visn_attention_mask)
+
+    def output_fc(self, lang_input, visn_input):
+        lang = self.lang_output(self.lang_inter(lang_input), lang_input)
+        visn = self.visn_output(self.visn_inter(visn_input), visn_input)
+        return lang, visn
+
+    def forward(self, lang_feats, lang_attention_mask, visn_feats, visn_attention_mask):
+        la, va = self.cross_att(lang_feats, lang_attention_mask, visn_feats, visn_attention_mask)
+        la, va = self.self_att(la, lang_attention_mask, va, visn_attention_mask)
+        return self.output_fc(la[0], va[0])
+
+
+class VisionEncoder(nn.Module):
+    """vilmodel.py:1067-1095: dropout(LayerNorm(visn_fc(f)))."""
+
+    def __init__(self, vision_size, config):
+        super().__init__()
+        self.visn_fc = nn.Linear(vision_size, config.hidden_size)
+        self.visn_layer_norm = BertLayerNorm(config.hidden_size, eps=1e-12)
+        self.dropout = nn.Dropout(config.hidden_dropout_prob)
+
+    def forward(self, visn_input):
+        x = _lin(visn_input, self.visn_fc)
+        x = DF.layer_norm(x, self.visn_layer_norm.weight, self.visn_layer_norm.bias, self.visn_layer_norm.eps)
+        return DF.dropout(x, self.dropout.p, self.training)
+
+
+class DicModel(nn.Module):
+    """vilmodel.py:1245-1423. `text_embeds` (extra, optional) short-circuits the language stack with a
+    cached output — exact whenever the stack is not being trained, since it does not see the image."""
+
+    def __init__(self, config):
+        super().__init__()
+        self.config = config
+        self.embeddings = BertEmbeddings(config)
+        self.pooler = BertPooler(config)
+        self.img_dim = config.img_feature_dim
+        self.img_feature_type = config.img_feature_type
+        self.vl_layers = config.vl_layers
+        self.la_layers = config.la_layers
+        self.update_lang_bert = config.update_lang_bert
+        self.update_add_layer = config.update_add_layer
+        self.lalayer = nn.ModuleList([BertLayer(config) for _ in range(self.la_layers)])
+        self.addlayer = nn.ModuleList([LXRTXLayer(config) for _ in range(self.vl_layers)])
+        self.vision_encoder = VisionEncoder(self.config.img_feature_dim, self.config)
+        if args.d_v_layers > 0:
+            self.vlayer = nn.ModuleList([BertLayer(config) for _ in range(args.d_v_layers)])
+        self.init_weights()
+
+    def init_weights(self):
+        std = getattr(self.config, "initializer_range", 0.02)
+        for m in self.modules():
+            if isinstance(m, (nn.Linear, nn.Embedding)):
+                m.weight.data.normal_(0.0, std)
+                if isinstance(m, nn.Linear) and m.bias is not None:
+                    m.bias.data.zero_()
+            elif isinstance(m, nn.LayerNorm):
+                m.weight.data.fill_(1.0)
+                m.bias.data.zero_()
+
+    def language(self, input_ids, ext_mask):
+        """Embeddings + the la_layers language BertLayers (vilmodel.py:1366-1372)."""
+        x = self.embeddings(input_ids)
+        for layer in self.lalayer:
+            x = layer(x, ext_mask)[0]
+        return x
+
+    def forward(self, input_ids, token_type_ids=None, attention_mask=None, position_ids=None, head_mask=None,
+                img_feats=None, text_embeds=None):
+        if head_mask is not None or position_ids is not None:
+            raise NotImplementedError("head_mask / position_ids")
+        if attention_mask is None:
+            attention_mask = torch.ones_like(input_ids)
+        ext = ((1.0 - attention_mask.float()) * -10000.0).unsqueeze(1).unsqueeze(2)
+        if text_embeds is None:
+            with torch.set_grad_enabled(torch.is_grad_enabled() and self.update_lang_bert):
+                text_embeds = self.language(input_ids, ext)
+        if not self.update_lang_bert:
+            text_embeds = text_embeds.detach()
+        visn_output = None
+        if img_feats is not None:
+            with torch.set_grad_enabled(torch.is_grad_enabled() and self.update_add_layer):
+                B, V = img_feats.shape[0], img_feats.shape[1]
+                img_mask = torch.zeros(B, 1, 1, V, dtype=torch.float32, device=img_feats.device)
+                lang = text_embeds
+                visn = self.vision_encoder(img_feats)
+                if args.d_v_layers > 0:
+                    for layer in self.vlayer:
+                        visn = layer(visn, img_mask)[0]
+                for layer in self.addlayer:
+                    lang, visn = layer(lang, ext, visn, img_mask)
+            if not self.update_add_layer:
+                lang, visn = lang.detach(), visn.detach()
+            sequence_output = lang
+        else:
+            sequence_output = text_embeds
+        pooled_output = self.pooler(sequence_output)
+        return sequence_output, pooled_output, visn_output if img_feats is None else visn

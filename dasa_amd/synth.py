@@ -273,7 +273,7 @@ class SynthR2RBatch:
     """
 
     def __init__(self, world, batch_size, seed=7, mode="goal", instr_len=80, variable_len=False,
-                 angle_feat_size=ANGLE_FEAT_SIZE):
+                 angle_feat_size=ANGLE_FEAT_SIZE, lazy_features=False):
         self.world = world
         self.batch_size = batch_size
         self.rng = np.random.default_rng(seed)
@@ -287,6 +287,10 @@ class SynthR2RBatch:
         self.batch = []
         self._episode = 0
         self.virtual_goal = np.array([100.0, 100.0, 100.0])
+        # lazy_features: obs dicts carry pool indices instead of the [36, 2176] arrays; the agent then
+        # assembles the tensors on the device (device_input_feat), as a device-resident feature store would.
+        self.lazy_features = lazy_features
+        self._store = None
 
     # -- episodes
     def _new_batch(self):
@@ -333,6 +337,11 @@ class SynthR2RBatch:
         for k, (u, point, dh, de) in enumerate(w.neighbors[v]):
             ang = angle_feature(view_heading(point) - base_heading + dh, view_elevation(point) + de,
                                 self.angle_feat_size)
+            if self.lazy_features:
+                out.append({"viewpointId": w.ids[u], "pointId": point, "idx": k + 1, "angle": ang,
+                            "heading": view_heading(point) - base_heading + dh,
+                            "elevation": view_elevation(point) + de, "scanId": "synth"})
+                continue
             out.append({
                 "heading": view_heading(point) - base_heading + dh,
                 "elevation": view_elevation(point) + de,
@@ -369,6 +378,7 @@ class SynthR2RBatch:
             v = sim.vp
             base = st.viewIndex
             ang = self.angle_feature[base]
+            lazy = self.lazy_features
             obs.append({
                 "instr_id": item["instr_id"],
                 "scan": "synth",
@@ -376,8 +386,8 @@ class SynthR2RBatch:
                 "viewIndex": base,
                 "heading": st.heading,
                 "elevation": st.elevation,
-                "feature": np.concatenate((w.rgb[v], ang), -1),
-                "dfeature": np.concatenate((w.depth[v], ang), -1),
+                "feature": None if lazy else np.concatenate((w.rgb[v], ang), -1),
+                "dfeature": None if lazy else np.concatenate((w.depth[v], ang), -1),
                 "candidate": self._candidates(v, base),
                 "navigableLocations": st.navigableLocations,
                 "instructions": item["instructions"],
@@ -392,3 +402,68 @@ class SynthR2RBatch:
                 "_vp_index": v,
             })
         return obs
+
+
+class DeviceFeatureStore:
+    """Device-resident RGB/depth pools + the 36x36 angle table; assembles the agent's input tensors with
+    one libdasa_hip gather launch per block (dasa_gather_rows)."""
+
+    def __init__(self, world, device, angle_feat_size=ANGLE_FEAT_SIZE):
+        import torch
+        P = world.P
+        self.device = device
+        self.rgb = torch.from_numpy(world.rgb.reshape(P * NUM_VIEWS, FEATURE_SIZE)).to(device)
+        self.depth = torch.from_numpy(world.depth.reshape(P * NUM_VIEWS, FEATURE_SIZE)).to(device)
+        self.angles = torch.from_numpy(angle_table(angle_feat_size).reshape(NUM_VIEWS * NUM_VIEWS, -1)).to(device)
+        self.A = angle_feat_size
+
+    def input_feat(self, obs):
+        import torch
+        from . import ops
+        B = len(obs)
+        A = self.A
+        leng = [len(ob["candidate"]) + 1 for ob in obs]
+        C = max(leng)
+        vp = np.array([ob["_vp_index"] for ob in obs], np.int64)
+        view = np.array([ob["viewIndex"] for ob in obs], np.int64)
+        r36 = np.arange(NUM_VIEWS)
+        ia_v = (vp[:, None] * NUM_VIEWS + r36[None]).astype(np.int32).reshape(-1)
+        ib_v = (view[:, None] * NUM_VIEWS + r36[None]).astype(np.int32).reshape(-1)
+        ia_c = np.full((B, C), -1, np.int32)
+        ib_c = np.full((B, C), -1, np.int32)
+        cang = np.zeros((B, C, A), np.float32)
+        a_t = np.zeros((B, A), np.float32)
+        for i, ob in enumerate(obs):
+            a_t[i] = angle_feature(ob["heading"], ob["elevation"], A)
+            for j, c in enumerate(ob["candidate"]):
+                ia_c[i, j] = vp[i] * NUM_VIEWS + c["pointId"]
+                ib_c[i, j] = i * C + j
+                cang[i, j] = c["angle"] if "angle" in c else c["feature"][-A:]
+        ints = torch.from_numpy(np.concatenate([ia_v, ib_v, ia_c.reshape(-1), ib_c.reshape(-1)])).pin_memory()
+        flts = torch.from_numpy(np.concatenate([a_t.reshape(-1), cang.reshape(-1)])).pin_memory()
+        ints = ints.to(self.device, non_blocking=True)
+        flts = flts.to(self.device, non_blocking=True)
+        n = B * NUM_VIEWS
+        ia_v_d, ib_v_d = ints[:n], ints[n:2 * n]
+        ia_c_d, ib_c_d = ints[2 * n:2 * n + B * C], ints[2 * n + B * C:]
+        a_t_d = flts[:B * A].view(B, A)
+        cang_d = flts[B * A:].view(B * C, A)
+        F = FEATURE_SIZE + A
+        f_t = torch.empty(B, NUM_VIEWS, F, dtype=torch.float32, device=self.device)
+        d_t = torch.empty_like(f_t)
+        cf = torch.empty(B, C, F, dtype=torch.float32, device=self.device)
+        cd = torch.empty_like(cf)
+        ops.gather_rows(self.rgb, ia_v_d, self.angles, ib_v_d, f_t)
+        ops.gather_rows(self.depth, ia_v_d, self.angles, ib_v_d, d_t)
+        ops.gather_rows(self.rgb, ia_c_d, cang_d, ib_c_d, cf)
+        ops.gather_rows(self.depth, ia_c_d, cang_d, ib_c_d, cd)
+        return a_t_d, f_t, d_t, cf, cd, leng
+
+
+def _device_input_feat(self, obs, device):
+    if self._store is None or self._store.device != device:
+        self._store = DeviceFeatureStore(self.world, device, self.angle_feat_size)
+    return self._store.input_feat(obs)
+
+
+SynthR2RBatch.device_input_feat = _device_input_feat

@@ -30,6 +30,7 @@ const char* dasa_error_string(int err); /* hipGetErrorString of a returned code 
  *   opB: 0 = B stored [K][N] (ldb >= N), 1 = B stored [N][K] (ldb >= K)   (nn.Linear weight = opB 1)
  * Epilogue order: v = alpha*acc; v += bias[n]; v = act(v); v = v*aux[m,n] (gate); v *= colscale[n];
  *                 v += beta*C[m,n].
+ * 16-B aligned operands with ld % 4 == 0 stream with dwordx4 loads; others take a scalar-load variant.
  * Replaces every nn.Linear / torch.bmm on the hot path (model.py:263-313, vilmodel.py:179-309,
  * agent_dg.py:1519 DGAdaChannel.a_fc, r2rmodel.py:2241-2251 LSTM input projections).       */
 enum dasa_act {
@@ -78,11 +79,12 @@ int dasa_mha_fwd(const float* Q, int64_t ldq, const float* K, int64_t ldk, const
                  const float* addmask, float* out, int64_t ldo, float* probs,
                  int32_t B, int32_t heads, int32_t Lq, int32_t Lk, int32_t dh, float scale,
                  float drop_p, uint64_t seed, void* stream);
-/* Backward without attention dropout (eval-equivalent); dQ/dK/dV use the ld of Q/K/V. */
+/* Backward; probs are the forward's saved pre-dropout softmax [B][heads][Lq][Lk], the dropout mask
+ * is regenerated from (drop_p, seed). dQ/dK/dV are written with the ld of Q/K/V. */
 int dasa_mha_bwd(const float* Q, int64_t ldq, const float* K, int64_t ldk, const float* V, int64_t ldv,
                  const float* probs, const float* dout, int64_t lddo,
                  float* dQ, float* dK, float* dV, int32_t B, int32_t heads, int32_t Lq, int32_t Lk,
-                 int32_t dh, float scale, void* stream);
+                 int32_t dh, float scale, float drop_p, uint64_t seed, void* stream);
 
 /* ---- SoftDot / ShiftSoftDot attention (model.py:253-353) ------------------------------------
  * q [B][D] is linear_in(h) (computed by dasa_gemm_f32); ctx [B][N][ldn] (ldn >= D, batch stride
@@ -119,18 +121,23 @@ int dasa_lstm_cell_bwd(const float* act_save, const float* c_prev, const float* 
 
 /* Packed bidirectional single-layer LSTM recurrence (pack_padded_sequence semantics,
  * r2rmodel.py:2339-2343). xproj [B][L][2][4H] = x W_ih^T + b_ih + b_hh for both directions;
- * whh [2][4H][H]; lengths [B] int32 (descending not required). Writes out [B][L][2H] ([fwd,bwd]),
+ * whh_fwd/whh_bwd [4H][H] (weight_hh_l0 / weight_hh_l0_reverse); lengths [B] int32 (any order).
+ * Writes out [B][L][2H] ([fwd,bwd]),
  * h_n/c_n [2][B][H], and (if save != NULL) save = {act [L][2][B][4H], c [L][2][B][H]}.
  * ws: dasa_bilstm_workspace(B, H) bytes (ping-pong state; + recurrent gates when B > 32).        */
 int64_t dasa_bilstm_workspace(int32_t B, int32_t H);
-int dasa_bilstm_fwd(const float* xproj, const float* whh, const int32_t* lengths,
-                    float* out, float* h_n, float* c_n, float* save_act, float* save_c,
-                    int32_t B, int32_t L, int32_t H, float* ws, void* stream);
+int dasa_bilstm_fwd(const float* xproj, const float* whh_fwd, const float* whh_bwd,
+                    const int32_t* lengths, float* out, float* h_n, float* c_n, float* save_act,
+                    float* save_c, int32_t B, int32_t L, int32_t H, float* ws, void* stream);
 /* BPTT: dout [B][L][2H], dh_n/dc_n [2][B][H] (may be NULL) -> dgates [B][L][2][4H] (time-major
  * grads of the pre-activation gates; zero at padded steps). B <= 32. ws: 4*B*H floats.          */
-int dasa_bilstm_bwd(const float* whh, const int32_t* lengths, const float* save_act, const float* save_c,
+int dasa_bilstm_bwd(const float* whh_fwd, const float* whh_bwd, const int32_t* lengths,
+                    const float* save_act, const float* save_c,
                     const float* dout, const float* dh_n, const float* dc_n, float* dgates,
                     int32_t B, int32_t L, int32_t H, float* ws, void* stream);
+/* hprev [2][B][L][H]: the recurrent input each step saw (fwd: out[b][t-1][:H], bwd: out[b][t+1][H:]),
+ * zero at the sequence ends — the right operand of dW_hh = sum_t dgates_t^T hprev_t.            */
+int dasa_bilstm_hprev(const float* out, float* hprev, int32_t B, int32_t L, int32_t H, void* stream);
 
 /* ---- AdaIN mu/sigma (model.py:1822-1840, adaIn_type default) ---------------------------------
  * out = (c - mean_c)/std_c * std_s + mean_s per row of N channels (unbiased var + eps, sqrt). */
@@ -146,12 +153,22 @@ int dasa_ada_gate_fwd(const float* s, int64_t lds, const float* f, int64_t ldf, 
 int dasa_ada_gate_bwd(const float* dout, int64_t lddo, const float* s, int64_t lds, const float* f,
                       int64_t ldf, const float* noise, float* dz, int64_t ldz, int32_t rows, int32_t cols,
                       void* stream);
+int dasa_act_fwd(const float* x, float* y, int64_t n, int32_t act, void* stream);
 /* dx = dy * act'(.) from the activation output (relu/tanh/sigmoid) or input (gelu); n elements. */
 int dasa_act_bwd(const float* y_or_x, const float* dy, float* dx, int64_t n, int32_t act, void* stream);
 int dasa_add2d(const float* a, int64_t lda, const float* b, int64_t ldb, float* out, int64_t ldo,
                int32_t rows, int32_t cols, void* stream);
 int dasa_copy2d(const float* x, int64_t ldx, float* out, int64_t ldo, int32_t rows, int32_t cols,
                 void* stream);
+/* out = x * scale[col] (shared env-drop noise on the RGB columns, agent_dg.py:731-736, 780-785). */
+int dasa_colscale(const float* x, int64_t ldx, const float* scale, float* out, int64_t ldo, int32_t rows,
+                  int32_t cols, void* stream);
+
+/* ---- observation pipeline (agent_dg.py:286-323, env.py:317-360 on a device-resident store) -----
+ * out[r] = [ta[ia[r]] (Fa floats; zeros if ia[r] < 0) | tb[ib[r]] (Fb floats; zeros if ib == NULL or
+ * ib[r] < 0)]: panorama blocks [B][36][2048+128] and candidate blocks [B][C][2176] in one gather.  */
+int dasa_gather_rows(const float* ta, const int32_t* ia, int32_t Fa, const float* tb, const int32_t* ib,
+                     int32_t Fb, float* out, int32_t R, void* stream);
 
 /* ---- small helpers --------------------------------------------------------------------------- */
 /* Reverse the first lengths[b] rows of x [B][L][H] into out (rest zero), r2rmodel.py:2326-2330. */

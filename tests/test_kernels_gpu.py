@@ -56,10 +56,12 @@ def test_gemm_layouts(dev):
     ops.matmul_nn(big[:, :92], B.to(dev), out=out, beta=1.0)
     ref2 = (big[:, :92].cpu().double() @ B.double() + C0.double()).float()
     assert (out.cpu() - ref2).abs().max() < 1e-5
-    # the float4 operand contract: unaligned row strides are rejected, not silently mis-read
-    from dasa_amd._lib import DasaError
-    with pytest.raises(DasaError):
-        ops.matmul_nn(_rand(5, 90, g=g).to(dev), _rand(90, 8, g=g).to(dev))
+    # unaligned row strides take the scalar-load variant
+    A2, B2 = _rand(37, 45, g=g), _rand(45, 3, g=g)
+    ref3 = (A2.double() @ B2.double()).float()
+    assert (ops.matmul_nn(A2.to(dev), B2.to(dev)).cpu() - ref3).abs().max() < 1e-5
+    assert (ops.matmul_tn(A2.t().contiguous().to(dev), B2.to(dev)).cpu() - ref3).abs().max() < 1e-5
+    assert (ops.colsum(B2.to(dev)).cpu() - B2.sum(0)).abs().max() < 1e-5
 
 
 def test_layernorm_and_embed(dev):
@@ -199,15 +201,15 @@ def test_bilstm(dev, B, L):
     ((out_ref * gout).sum() + (hn * ghn).sum() + (cn * gcn).sum()).backward()
     Wih = torch.cat([lstm.weight_ih_l0, lstm.weight_ih_l0_reverse], 0).detach()
     bias = torch.cat([lstm.bias_ih_l0 + lstm.bias_hh_l0, lstm.bias_ih_l0_reverse + lstm.bias_hh_l0_reverse]).detach()
-    whh = torch.stack([lstm.weight_hh_l0, lstm.weight_hh_l0_reverse]).detach().contiguous()
+    whh_f, whh_b = lstm.weight_hh_l0.detach().to(dev), lstm.weight_hh_l0_reverse.detach().to(dev)
     xd = x.to(dev)
     xproj = ops.linear(xd.view(B * L, E), Wih.to(dev), bias.to(dev)).view(B, L, 2, 4 * H)
     li = lengths.to(torch.int32).to(dev)
-    out, h_n, c_n, saved = ops.bilstm_fwd(xproj, whh.to(dev), li, H, save=(B <= 32))
+    out, h_n, c_n, saved = ops.bilstm_fwd(xproj, whh_f, whh_b, li, H, save=(B <= 32))
     assert (out.cpu() - out_ref).abs().max() < 2e-5
     assert (h_n.cpu() - hn).abs().max() < 2e-5 and (c_n.cpu() - cn).abs().max() < 2e-5
     if B <= 32:
-        dg = ops.bilstm_bwd(whh.to(dev), li, saved, gout.to(dev), ghn.to(dev), gcn.to(dev), H)
+        dg = ops.bilstm_bwd(whh_f, whh_b, li, saved, gout.to(dev), ghn.to(dev), gcn.to(dev), H)
         # weight grads from dgates: dW_hh[dir] = sum_t dg^T h_prev
         dgc = dg.cpu()
         dWih = torch.einsum("blg,ble->ge", dgc[:, :, 0], x)
@@ -216,6 +218,11 @@ def test_bilstm(dev, B, L):
         assert (dWih_r - lstm.weight_ih_l0_reverse.grad).abs().max() < 1e-3 * max(1, lstm.weight_ih_l0_reverse.grad.abs().max())
         db = dgc[:, :, 0].sum((0, 1))
         assert (db - lstm.bias_ih_l0.grad).abs().max() < 1e-3 * max(1, lstm.bias_ih_l0.grad.abs().max())
+        hp = ops.bilstm_hprev(out, H).cpu()
+        dWhh = torch.einsum("blg,blh->gh", dgc[:, :, 0], hp[0])
+        assert (dWhh - lstm.weight_hh_l0.grad).abs().max() < 1e-3 * max(1, lstm.weight_hh_l0.grad.abs().max())
+        dWhh_r = torch.einsum("blg,blh->gh", dgc[:, :, 1], hp[1])
+        assert (dWhh_r - lstm.weight_hh_l0_reverse.grad).abs().max() < 1e-3 * max(1, lstm.weight_hh_l0_reverse.grad.abs().max())
 
 
 def test_adain_musigma_reverse_dropout(dev):

@@ -1,0 +1,257 @@
+"""GPU parity of the product modules (dasa_amd.r2r on libdasa_hip.so) against the reference's golden
+vectors (tests/golden, produced by the reference itself) and the CPU oracle. Tolerance: the north
+star's 1e-4 fp32 on logits / critic values / states; gradients to 1e-3 relative."""
+import numpy as np
+import pytest
+import torch
+
+from dasa_amd.synth import SynthR2RBatch, SynthWorld, init_params
+from tests import golden_inputs as GI
+from tests.helpers import check_grads, close, golden
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+
+
+@pytest.fixture(scope="module")
+def R(dev):
+    from dasa_amd.r2r import param
+    param.readme_train(["--d_vl_layers", "1", "--batchSize", "2", "--maxAction", "5"])
+    from dasa_amd.r2r import agent_dg, model, r2rmodel, vilmodel
+    return param, agent_dg, model, r2rmodel, vilmodel
+
+
+def _req(t, dev):
+    return t.to(dev).requires_grad_(True)
+
+
+def test_ada_channel(R, dev):
+    param, agent_dg, *_ = R
+    G = golden("ops")
+    ada = init_params(agent_dg.DGAdaChannel(2048), GI.SEED_ADA).to(dev)
+    f, d, g = GI.ada_inputs()
+    y = ada(f.to(dev), d.to(dev))
+    close(y.detach().cpu(), G["ada/out"], 1e-5, "ada")
+    (y * g.to(dev)).sum().backward()
+    assert check_grads(G, "ada/", [(k, p.grad) for k, p in ada.named_parameters()], rtol=1e-3) == 2
+    # the fused 2176-wide feature path used by the rollout (AdaFeatFn) agrees with forward()
+    fa = torch.cat([f, torch.rand(2, 10, 128)], -1).to(dev)
+    da = torch.cat([d, torch.rand(2, 10, 128)], -1).to(dev)
+    with torch.no_grad():
+        out = ada.feature(fa, da)
+    close(out[..., :2048].cpu(), G["ada/out"], 1e-5, "ada feature rgb")
+    close(out[..., 2048:].cpu(), fa[..., 2048:].cpu(), 0.0, "ada feature angle")
+
+
+@pytest.mark.parametrize("K", [5, 3])
+def test_shift_attention(R, dev, K):
+    model = R[2]
+    G = golden("ops")
+    m = init_params(model.ShiftSoftDotAttention(1024, 2176, K), 20 + K).to(dev)
+    h, ctx, gw = GI.shift_inputs(K)
+    h, ctx = _req(h, dev), _req(ctx, dev)
+    wctx, attn = m(h, ctx, output_tilde=False)
+    close(wctx.detach().cpu(), G[f"shift{K}/wctx"], TOL, "wctx")
+    close(attn.detach().cpu(), G[f"shift{K}/attn"], 1e-5, "attn")
+    (wctx * gw.to(dev)).sum().backward()
+    close(h.grad.cpu(), G[f"shift{K}/dh"], 1e-3 * np.abs(G[f"shift{K}/dh"]).max(), "dh")
+    assert check_grads(G, f"shift{K}/", [("ctx", ctx.grad)] + [(k, p.grad) for k, p in m.named_parameters()],
+                       rtol=1e-3) >= 3
+
+
+def test_softdot(R, dev):
+    model = R[2]
+    G = golden("ops")
+    h, ctx, mask, cand, g1, g2 = GI.softdot_inputs()
+    att = init_params(model.SoftDotAttention(1024, 2048), 30).to(dev)
+    h1 = _req(h, dev)
+    ht, alpha = att(h1, ctx.to(dev), mask.to(dev))
+    close(ht.detach().cpu(), G["softdot/h_tilde"], 1e-5, "h_tilde")
+    close(alpha.cpu(), G["softdot/alpha"], 1e-6, "alpha")
+    (ht * g1.to(dev)).sum().backward()
+    close(h1.grad.cpu(), G["softdot/dh"], 1e-4, "dh")
+    assert check_grads(G, "softdot/", [(k, p.grad) for k, p in att.named_parameters()], rtol=1e-3) == 2
+    catt = init_params(model.SoftDotAttention(1024, 2176), 31).to(dev)
+    h2, cd = _req(h, dev), _req(cand, dev)
+    _, logit = catt(h2, cd, output_prob=False, output_tilde=False)
+    close(logit.detach().cpu(), G["cand/logit"], TOL, "cand logit")
+    (logit * g2.to(dev)).sum().backward()
+    close(h2.grad.cpu(), G["cand/dh"], 1e-4, "cand dh")
+    check_grads(G, "cand/", [("cand", cd.grad), ("linear_in.weight", catt.linear_in.weight.grad)], rtol=1e-3)
+
+
+def test_decoder_and_critic(R, dev):
+    param, agent_dg, model = R[0], R[1], R[2]
+    A = param.args
+    G = golden("ops")
+    dec = init_params(model.BAttnDecoderLSTM(A.aemb, A.d_hidden_size, A.dropout, feature_size=2176), GI.SEED_DEC)
+    dec = dec.to(dev).eval()
+    ins = [t.to(dev) for t in GI.decoder_inputs()]
+    h1, c1, logit, ht, _ = dec(*ins)
+    for k, v in dict(h1=h1, c1=c1, logit=logit, h_tilde=ht).items():
+        close(v.detach().cpu(), G["dec/" + k], TOL, k)
+    rng = np.random.default_rng(121)
+    w = [torch.from_numpy(rng.standard_normal(t.shape).astype(np.float32)).to(dev) for t in (h1, c1, logit, ht)]
+    ((h1 * w[0]).sum() + (c1 * w[1]).sum() + (logit * w[2]).sum() + (ht * w[3]).sum()).backward()
+    assert check_grads(G, "dec/", [(k, p.grad) for k, p in dec.named_parameters() if p.grad is not None],
+                       rtol=1e-3) >= 10
+    cr = init_params(model.Critic(), GI.SEED_CRITIC).to(dev).eval()
+    v = cr(GI.critic_inputs().to(dev))
+    close(v.detach().cpu(), G["critic/value"], TOL, "critic")
+    (v * torch.arange(1.0, 5.0, device=dev)).sum().backward()
+    assert check_grads(G, "critic/", [(k, p.grad) for k, p in cr.named_parameters()], rtol=1e-3) == 4
+
+
+def test_lxrt_layer(R, dev):
+    vilmodel = R[4]
+    G = golden("ops")
+    lx = init_params(vilmodel.LXRTXLayer(vilmodel.BertConfig()), 40).to(dev).eval()
+    lang, lmask, visn, vmask = GI.lxrt_inputs()
+    with torch.no_grad():
+        lo, vo = lx(lang.to(dev), lmask[:, None, None, :].to(dev), visn.to(dev), vmask[:, None, None, :].to(dev))
+    close(lo.cpu(), G["lxrt/lang"], TOL, "lang")
+    close(vo.cpu(), G["lxrt/visn"], TOL, "visn")
+
+
+def test_dic_encoder(R, dev):
+    param, r2rmodel = R[0], R[3]
+    A = param.args
+    G = golden("ops")
+    enc = r2rmodel.DicEncoder(2176, A.d_enc_hidden_size, A.d_hidden_size, A.d_dropout_ratio, A.d_bidirectional,
+                              A.d_transformer_update, A.d_bert_n_layers, A.d_reverse_input, A.d_top_lstm, 1,
+                              A.d_la_layers, A.d_bert_type, update_add_layer=A.d_update_add_layer)
+    enc = init_params(enc, GI.SEED_ENC).to(dev).eval()
+    seq, mask, lengths, f = GI.encoder_inputs()
+    ctx, dinit, ct, _, vis = enc(seq.to(dev), mask.to(dev), torch.tensor(lengths), f_t_all=f.to(dev))
+    close(ctx.detach().cpu(), G["enc/ctx"], TOL, "ctx")
+    close(dinit.detach().cpu(), G["enc/decoder_init"], TOL, "decoder_init")
+    close(ct.detach().cpu(), G["enc/c_t"], TOL, "c_t")
+    close(vis.detach().cpu(), G["enc/vision"], TOL, "vision")
+    rng = np.random.default_rng(151)
+    w = [torch.from_numpy(rng.standard_normal(t.shape).astype(np.float32)).to(dev) for t in (ctx, dinit, ct)]
+    ((ctx * w[0]).sum() + (dinit * w[1]).sum() + (ct * w[2]).sum()).backward()
+    assert check_grads(G, "enc/", [(k, p.grad) for k, p in enc.named_parameters() if p.grad is not None],
+                       rtol=1e-3) == 12
+
+
+def _agent(R, env, T, seed_weights=True):
+    agent_dg = R[1]
+    import contextlib
+    import io
+    with contextlib.redirect_stdout(io.StringIO()):
+        ag = agent_dg.Seq2SeqAgent(env, "", None, T, "Dic")
+    if seed_weights:
+        init_params(ag.encoder, GI.SEED_ENC)
+        init_params(ag.decoder, GI.SEED_DEC)
+        init_params(ag.critic, GI.SEED_CRITIC)
+        init_params(ag.adaIn, GI.SEED_ADA)
+    return ag
+
+
+class _HostOnlyEnv:
+    """Hides device_input_feat so the agent takes the reference numpy + H2D path."""
+
+    def __init__(self, env):
+        self._e = env
+
+    def __getattr__(self, k):
+        if k == "device_input_feat":
+            raise AttributeError(k)
+        return getattr(self._e, k)
+
+
+@pytest.mark.parametrize("host_path", [False, True])
+def test_rollout_eval_argmax(R, dev, host_path):
+    G = golden("cfg1_rollout")
+    cfg = GI.CFG1
+    env = SynthR2RBatch(SynthWorld(16, 0, 3), cfg["batch"], seed=7, mode="goal", instr_len=cfg["instr_len"],
+                        variable_len=True)
+    if host_path:
+        env = _HostOnlyEnv(env)
+    ag = _agent(R, env, cfg["max_action"])
+    rec = {"logit": [], "h1": [], "h_tilde": []}
+    fwd = ag.decoder.forward
+
+    def wrap(*a, **k):
+        r = fwd(*a, **k)
+        rec["logit"].append(r[2].detach().cpu())
+        rec["h1"].append(r[0].detach().cpu())
+        rec["h_tilde"].append(r[3].detach().cpu())
+        return r
+    ag.decoder.forward = wrap
+    ag.loss = 0
+    ag.feedback = "argmax"
+    for m in (ag.encoder, ag.decoder, ag.critic):
+        m.eval()
+    with torch.no_grad():
+        traj = ag.vl_rollout(train_ml=None, train_rl=False, reset=True)
+    assert len(rec["logit"]) == int(G["eval/steps"])
+    for t in range(len(rec["logit"])):
+        close(rec["logit"][t], G[f"eval/logit/{t}"], TOL, f"logit{t}")
+        close(rec["h1"][t], G[f"eval/h1/{t}"], TOL, f"h1{t}")
+        close(rec["h_tilde"][t], G[f"eval/h_tilde/{t}"], TOL, f"h_tilde{t}")
+    assert abs(ag.logs["ml_loss"][-1] - float(G["eval/ml_loss"])) < 1e-3
+    assert ["|".join(p[0] for p in tr["path"]) for tr in traj] == list(G["eval/paths"])
+
+
+def test_train_iteration_grads(R, dev):
+    """accumulate_gradient('sample') + backward with every dropout p = 0 and argmax 'sampling'."""
+    param = R[0]
+    G = golden("cfg1_rollout")
+    cfg = GI.CFG1
+    env = SynthR2RBatch(SynthWorld(16, 0, 3), cfg["batch"], seed=8, mode="goal", instr_len=cfg["instr_len"],
+                        variable_len=True)
+    ag = _agent(R, env, cfg["max_action"])
+    for m in ag.models:
+        for sub in m.modules():
+            if isinstance(sub, torch.nn.Dropout):
+                sub.p = 0.0
+    param.args.ml_weight = param.args.ml_weight_org
+    ag.sample_fn = lambda p: p.argmax(-1)
+    ag.zero_grad()
+    ag.accumulate_gradient("sample")
+    assert abs(ag.loss.item() - float(G["train/loss"])) < TOL * max(1.0, abs(float(G["train/loss"])))
+    assert abs(ag.logs["ml_loss"][0] - float(G["train/ml_loss_teacher"])) < 1e-3
+    assert abs(ag.logs["ml_loss"][1] - float(G["train/ml_loss_sample"])) < 1e-3
+    assert abs(ag.logs["normalized_rl_loss"][-1] - float(G["train/rl_loss"])) < TOL
+    assert ag.logs["viewsteps/teacher"][-1] == int(G["train/steps_teacher"])
+    assert ag.logs["viewsteps/sample"][-1] == int(G["train/steps_sample"])
+    ag.loss.backward()
+    n = 0
+    for name, mod in (("encoder", ag.encoder), ("decoder", ag.decoder), ("critic", ag.critic), ("adaIn", ag.adaIn)):
+        n += check_grads(G, f"train/{name}.", [(k, p.grad) for k, p in mod.named_parameters()], rtol=2e-3)
+    assert n == 30
+
+
+def test_cfg2_step_vs_oracle(R, dev):
+    """One eval policy step at the cfg2 shape (B=20, L=80, vl=3, C<=16) against the CPU oracle."""
+    from oracle import policy as O
+    from tests.helpers import oracle_weights
+    param = R[0]
+    param.readme_train(["--d_vl_layers", "3"])
+    try:
+        world = SynthWorld(32, 0, 5)
+        env = SynthR2RBatch(world, 20, seed=11, mode="wander", instr_len=80)
+        env2 = SynthR2RBatch(world, 20, seed=11, mode="wander", instr_len=80)
+        ag = _agent(R, env, 1)
+        W = oracle_weights(3)
+        rec = {}
+        fwd = ag.decoder.forward
+
+        def wrap(*a, **k):
+            r = fwd(*a, **k)
+            rec["logit"] = r[2].detach().cpu()
+            rec["h_tilde"] = r[3].detach().cpu()
+            return r
+        ag.decoder.forward = wrap
+        ag.loss = 0
+        ag.feedback = "teacher"
+        for m in (ag.encoder, ag.decoder, ag.critic):
+            m.eval()
+        with torch.no_grad():
+            ag.vl_rollout(train_ml=None, train_rl=False, reset=True)
+            r = O.vl_rollout(W, env2, "teacher", la_layers=9, vl_layers=3, episode_len=1)
+        close(rec["logit"], r["logits"][0], TOL, "cfg2 logit")
+        close(rec["h_tilde"], r["states"][0][2], TOL, "cfg2 h_tilde")
+    finally:
+        param.readme_train(["--d_vl_layers", "1", "--batchSize", "2", "--maxAction", "5"])
