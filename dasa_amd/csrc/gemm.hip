@@ -62,6 +62,11 @@ __device__ __forceinline__ float4 load4(const float* rowp, int e, int limit) {
 
 constexpr int BKT = 32;
 
+// Component-wise select (a whole-float4 ternary is lowered through scratch memory by hipcc).
+__device__ __forceinline__ float4 sel4(bool c, float4 v) {
+  return make_float4(c ? v.x : 0.f, c ? v.y : 0.f, c ? v.z : 0.f, c ? v.w : 0.f);
+}
+
 // KC = operand stored with K contiguous ([rows][K]); else stored [K][rows].
 template <int ROWS, bool KC, bool VEC>
 struct TileLoader {
@@ -72,17 +77,33 @@ struct TileLoader {
 
   __device__ __forceinline__ void load(const float* base, long ld, int r0, int rlimit, int k0, int klimit) {
     const int tid = threadIdx.x;
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int i = 0; i < NF4; ++i) {
       const int q = tid + 256 * i;
-      if (KC) {
+      if (VEC) {
+        // Unconditional, clamped loads + a select: a branch around each load would make hipcc wait
+        // vmcnt(0) per load and serialise the tile fetch. With K % 4 == 0 (VEC) a quad is either fully
+        // in range or fully out.
+        if (KC) {
+          const int row = q / (BKT / 4), kq = q % (BKT / 4);
+          const int gr = r0 + row, gk = k0 + 4 * kq;
+          const float4 v = *reinterpret_cast<const float4*>(base + (long)min(gr, rlimit - 1) * ld + min(gk, klimit - 4));
+          r[i] = sel4(gr < rlimit && gk < klimit, v);
+        } else {
+          const int kr = q / (ROWS / 4), rq = q % (ROWS / 4);
+          const int gk = k0 + kr, gr = r0 + 4 * rq;
+          const float4 v = *reinterpret_cast<const float4*>(base + (long)min(gk, klimit - 1) * ld + min(gr, rlimit - 4));
+          r[i] = sel4(gk < klimit && gr < rlimit, v);
+        }
+      } else if (KC) {
         const int row = q / (BKT / 4), kq = q % (BKT / 4);
         const int gr = r0 + row;
-        r[i] = (gr < rlimit) ? load4<VEC>(base + (long)gr * ld, k0 + 4 * kq, klimit) : make_float4(0.f, 0.f, 0.f, 0.f);
+        r[i] = (gr < rlimit) ? load4<VEC>(base + (long)gr * ld, k0 + 4 * kq, klimit) : z;
       } else {
         const int kr = q / (ROWS / 4), rq = q % (ROWS / 4);
         const int gk = k0 + kr;
-        r[i] = (gk < klimit) ? load4<VEC>(base + (long)gk * ld, r0 + 4 * rq, rlimit) : make_float4(0.f, 0.f, 0.f, 0.f);
+        r[i] = (gk < klimit) ? load4<VEC>(base + (long)gk * ld, r0 + 4 * rq, rlimit) : z;
       }
     }
   }
@@ -172,21 +193,84 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p) {
   }
 
   // C/D map of the 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+  // Epilogue: every optional operand is fetched with unconditional clamped loads inside ONE uniform
+  // branch per operand (a per-element branch around a load makes hipcc wait vmcnt(0) per element).
+  const bool full_tile = (m0 + BM <= p.M) && (n0 + BN <= p.N);
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + wn + j * 32 + rl;
+    const int colc = min(col, p.N - 1);
+    float bj = 0.f, cs = 1.f;
+    if (p.splitk == 1) {
+      if (p.bias) bj = p.bias[colc];
+      if (p.colscale) cs = p.colscale[colc];
+    }
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+    for (int i = 0; i < TM; ++i) {
+      const int rbase = m0 + wm + i * 32 + 4 * hl;
+      if (p.splitk > 1) {
+        float* ws = p.ws + ((long)split * p.batch + b) * p.M * p.N;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = rbase + (r & 3) + 8 * (r >> 2);
+          if (full_tile || (row < p.M && col < p.N)) ws[(long)row * p.N + col] = acc[i][j][r];
+        }
+        continue;
+      }
+      float v[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = p.alpha * acc[i][j][r] + bj;
+      switch (p.act) {   // one uniform branch per tile, not per element
+        case DASA_ACT_RELU:
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] = fmaxf(v[r], 0.f);
+          break;
+        case DASA_ACT_GELU:
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] = gelu_erf(v[r]);
+          break;
+        case DASA_ACT_TANH:
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] = tanhf(v[r]);
+          break;
+        case DASA_ACT_SIGMOID:
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] = sigmoidf_(v[r]);
+          break;
+        default:
+          break;
+      }
+      if (p.aux) {
+        const float* ab = p.aux + (long)b * p.sAux;
+        float av[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = min(rbase + (r & 3) + 8 * (r >> 2), p.M - 1);
+          av[r] = ab[(long)row * p.ld_aux + colc];
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] *= av[r];
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] *= cs;
+      float* cb = p.C + (long)b * p.sC;
+      if (p.beta != 0.f) {
+        float cv[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = min(rbase + (r & 3) + 8 * (r >> 2), p.M - 1);
+          cv[r] = cb[(long)row * p.ldc + colc];
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] += p.beta * cv[r];
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-        const int col = n0 + wn + j * 32 + rl;
-        if (row < p.M && col < p.N) {
-          if (p.splitk > 1)
-            p.ws[(((long)split * p.batch + b) * p.M + row) * p.N + col] = acc[i][j][r];
-          else
-            epilogue_store(p, b, row, col, acc[i][j][r]);
-        }
+        const int row = rbase + (r & 3) + 8 * (r >> 2);
+        if (full_tile || (row < p.M && col < p.N)) cb[(long)row * p.ldc + col] = v[r];
       }
+    }
+  }
 }
 
 __global__ void splitk_reduce_kernel(GemmP p) {
@@ -267,8 +351,11 @@ extern "C" int dasa_gemm_f32(const dasa_gemm_desc* d, void* ws, int64_t ws_bytes
   if (M == 0 || N == 0) return 0;
   // float4 operand loads need 16-B aligned rows; anything else takes the scalar-load variant
   const uintptr_t am = (uintptr_t)d->A | (uintptr_t)d->B;
-  const bool vec = !((am & 15) || (d->lda & 3) || (d->ldb & 3) ||
-                     (batch > 1 && ((d->strideA & 3) || (d->strideB & 3))));
+  // VEC also needs the contiguous extent of each operand to be a multiple of 4 (K for K-contiguous
+  // operands, M / N for the transposed ones) so that quads never straddle the edge.
+  const bool ext4 = (K & 3) == 0 && (d->opA == 0 || (M & 3) == 0) && (d->opB == 1 || (N & 3) == 0);
+  const bool vec = ext4 && !((am & 15) || (d->lda & 3) || (d->ldb & 3) ||
+                             (batch > 1 && ((d->strideA & 3) || (d->strideB & 3))));
   if (d->opA == 0 ? d->lda < K : d->lda < M) return (int)hipErrorInvalidValue;
   if (d->opB == 1 ? d->ldb < K : d->ldb < N) return (int)hipErrorInvalidValue;
   if (d->ldc < N) return (int)hipErrorInvalidValue;

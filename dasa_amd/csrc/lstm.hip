@@ -100,41 +100,60 @@ __device__ __forceinline__ void cell_apply(const SeqArgs& a, int dir, int t, int
   }
 }
 
-// Fused step for B <= 32: grid (H/8, 2), 256 threads.
-__global__ __launch_bounds__(256) void bilstm_step_fused_kernel(SeqArgs a, int s) {
-  __shared__ float red[4][32][33];
-  const int dir = blockIdx.y, u0 = blockIdx.x * 8;
+// Fused step for B <= 32: grid (H/4, 2), 1024 threads. A workgroup owns 4 hidden units = 16 gate
+// columns (i,f,g,o interleaved); its 16 waves split the K = H recurrent reduction (v_mfma_f32_16x16x4_f32,
+// batch rows padded to 2 x 16) and reduce through LDS before the cell update.
+constexpr int kFwdUnits = 4, kFwdWaves = 16;
+__global__ __launch_bounds__(1024) void bilstm_step_fused_kernel(SeqArgs a, int s) {
+  __shared__ float red[kFwdWaves][32][17];
+  const int dir = blockIdx.y, u0 = blockIdx.x * kFwdUnits;
   const int H = a.H, B = a.B;
   const int t = dir == 0 ? s : a.L - 1 - s;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int hl = lane >> 5, r = lane & 31;
-  const float* hrow = a.hin + ((long)dir * B + r) * H;
-  const bool arow = r < B;
-  const int q = r & 3, unit = u0 + (r >> 2);
+  const int i16 = lane & 15, kg = lane >> 4;
+  // rows >= B are clamped to B-1 and zeroed by a select (no branch around the loads)
+  const float* h0 = a.hin + ((long)dir * B + min(i16, B - 1)) * H;
+  const float* h1 = a.hin + ((long)dir * B + min(16 + i16, B - 1)) * H;
+  const bool r0 = i16 < B, r1 = 16 + i16 < B;
+  const int q = i16 & 3, unit = u0 + (i16 >> 2);
   const float* wrow = (dir ? a.whh1 : a.whh0) + ((long)q * H + unit) * H;
-  const int kq = H / 4, k0 = w * kq;
-  floatx16 acc;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  const int kq = H / kFwdWaves, k0 = w * kq;
+  floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll 4
-  for (int kb = k0; kb < k0 + kq; kb += 8) {
-    const float4 av = arow ? *reinterpret_cast<const float4*>(hrow + kb + 4 * hl) : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4 bv = *reinterpret_cast<const float4*>(wrow + kb + 4 * hl);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, bv.x, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, bv.y, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, bv.z, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, bv.w, acc, 0, 0, 0);
+  for (int kb = k0; kb < k0 + kq; kb += 16) {
+    const int ko = kb + 4 * kg;
+    const float4 bv = *reinterpret_cast<const float4*>(wrow + ko);
+    float4 a0 = *reinterpret_cast<const float4*>(h0 + ko);
+    float4 a1 = *reinterpret_cast<const float4*>(h1 + ko);
+    if (!r0) a0 = z;   // uniform per lane-row; component selects, no branch around the loads
+    if (!r1) a1 = z;
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, bv.x, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, bv.x, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, bv.y, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, bv.y, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, bv.z, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, bv.z, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, bv.w, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, bv.w, acc1, 0, 0, 0);
   }
+  // 16x16 C/D map: col = lane & 15, row = 4 * (lane >> 4) + reg
 #pragma unroll
-  for (int i = 0; i < 16; ++i) red[w][(i & 3) + 8 * (i >> 2) + 4 * hl][r] = acc[i];
+  for (int r = 0; r < 4; ++r) {
+    red[w][4 * kg + r][i16] = acc0[r];
+    red[w][16 + 4 * kg + r][i16] = acc1[r];
+  }
   __syncthreads();
-  const int b = threadIdx.x >> 3, ul = threadIdx.x & 7;
-  if (b < B) {
-    float g[4];
+  if (threadIdx.x < 32 * kFwdUnits) {
+    const int b = threadIdx.x / kFwdUnits, ul = threadIdx.x % kFwdUnits;
+    if (b < B) {
+      float g[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int qq = 0; qq < 4; ++qq) g[qq] = red[0][b][4 * ul + qq] + red[1][b][4 * ul + qq] + red[2][b][4 * ul + qq] +
-                                           red[3][b][4 * ul + qq];
-    cell_apply(a, dir, t, b, u0 + ul, g[0], g[1], g[2], g[3]);
+      for (int ww = 0; ww < kFwdWaves; ++ww)
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) g[qq] += red[ww][b][4 * ul + qq];
+      cell_apply(a, dir, t, b, u0 + ul, g[0], g[1], g[2], g[3]);
+    }
   }
 }
 
@@ -158,8 +177,8 @@ __global__ void copy_kernel(const float* src, float* dst, long n) {
 
 // ---------------------------------------------------------------- bi-LSTM BPTT
 struct BpttArgs {
-  const float* whh0;      // [4H][H]
-  const float* whh1;
+  const float* wt0;       // W_hh^T [H][4H] forward direction (transposed once per call)
+  const float* wt1;
   const int* len;
   const float* save_act;  // [L][2][B][4H]
   const float* save_c;    // [L][2][B][H]
@@ -170,60 +189,94 @@ struct BpttArgs {
   int B, L, H;
 };
 
-// grid (H/32, 2), 512 threads (8 waves split the 4H reduction). s = BPTT step.
-__global__ __launch_bounds__(512) void bilstm_bptt_step_kernel(BpttArgs a, int s) {
-  __shared__ float red[8][32][33];
-  const int dir = blockIdx.y, j0 = blockIdx.x * 32;
+// out[c][r] = in[r][c] for an [R][C] matrix, 32x32 LDS tiles.
+__global__ void transpose_kernel(const float* __restrict__ in, float* __restrict__ out, int R, int C) {
+  __shared__ float tile[32][33];
+  const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 256 threads: 32 x 8
+  for (int k = ty; k < 32; k += 8) {
+    const int r = r0 + k, c = c0 + tx;
+    tile[k][tx] = (r < R && c < C) ? in[(long)r * C + c] : 0.f;
+  }
+  __syncthreads();
+  for (int k = ty; k < 32; k += 8) {
+    const int c = c0 + k, r = r0 + tx;
+    if (c < C && r < R) out[(long)c * R + r] = tile[tx][k];
+  }
+}
+
+// BPTT step for B <= 32: grid (H/16, 2), 1024 threads. The workgroup owns 16 hidden units j: its 16
+// waves split the K = 4H reduction rec[b][j] = sum_n dgates_prev[b][n] W_hh[n][j] (v_mfma 16x16x4 on
+// W_hh^T so both operands stream K-contiguous float4s), then the cell backward for those units.
+constexpr int kBwdUnits = 16, kBwdWaves = 16;
+__global__ __launch_bounds__(1024) void bilstm_bptt_step_kernel(BpttArgs a, int s) {
+  __shared__ float red[kBwdWaves][32][17];
+  const int dir = blockIdx.y, j0 = blockIdx.x * kBwdUnits;
   const int H = a.H, B = a.B, L = a.L, G4 = 4 * H;
   const int t = dir == 0 ? (L - 1 - s) : s;
   const int tp = dir == 0 ? t + 1 : t - 1;  // step processed just before in BPTT order
   const bool tpv = tp >= 0 && tp < L;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int hl = lane >> 5, r = lane & 31;
-  floatx16 acc;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  const int i16 = lane & 15, kg = lane >> 4;
+  floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   if (tpv) {
-    const bool arow = r < B;
-    const float* grow = a.dgates + (((long)r * L + tp) * 2 + dir) * G4;
-    const float* W = (dir ? a.whh1 : a.whh0) + j0 + r;
-    const int kq = G4 / 8, k0 = w * kq;
-#pragma unroll 8
-    for (int n = k0; n < k0 + kq; n += 2) {
-      const float av = arow ? grow[n + hl] : 0.f;
-      const float bv = W[(long)(n + hl) * H];
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+    const bool r0 = i16 < B, r1 = 16 + i16 < B;
+    const float* g0 = a.dgates + (((long)min(i16, B - 1) * L + tp) * 2 + dir) * G4;
+    const float* g1 = a.dgates + (((long)min(16 + i16, B - 1) * L + tp) * 2 + dir) * G4;
+    const float* wt = (dir ? a.wt1 : a.wt0) + (long)(j0 + i16) * G4;
+    const int kq = G4 / kBwdWaves, k0 = w * kq;
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 4
+    for (int kb = k0; kb < k0 + kq; kb += 16) {
+      const int ko = kb + 4 * kg;
+      const float4 bv = *reinterpret_cast<const float4*>(wt + ko);
+      float4 a0 = *reinterpret_cast<const float4*>(g0 + ko);
+      float4 a1 = *reinterpret_cast<const float4*>(g1 + ko);
+      if (!r0) a0 = z;
+      if (!r1) a1 = z;
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, bv.x, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, bv.x, acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, bv.y, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, bv.y, acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, bv.z, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, bv.z, acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, bv.w, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, bv.w, acc1, 0, 0, 0);
     }
   }
 #pragma unroll
-  for (int i = 0; i < 16; ++i) red[w][(i & 3) + 8 * (i >> 2) + 4 * hl][r] = acc[i];
+  for (int r = 0; r < 4; ++r) {
+    red[w][4 * kg + r][i16] = acc0[r];
+    red[w][16 + 4 * kg + r][i16] = acc1[r];
+  }
   __syncthreads();
-  for (int pidx = threadIdx.x; pidx < 32 * 32; pidx += 512) {
-    const int b = pidx >> 5, jl = pidx & 31, j = j0 + jl;
-    if (b >= B) continue;
-    float rec = 0.f;
+  if (threadIdx.x < 32 * kBwdUnits) {
+    const int b = threadIdx.x / kBwdUnits, jl = threadIdx.x % kBwdUnits, j = j0 + jl;
+    if (b < B) {
+      float rec = 0.f;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) rec += red[i][b][jl];
-    const long sidx = ((long)dir * B + b) * H + j;
-    float* dg = a.dgates + (((long)b * L + t) * 2 + dir) * G4;
-    if (t < a.len[b]) {
-      const float G = rec + a.dout[((long)b * L + t) * 2 * H + dir * H + j] + a.dh[sidx];
-      const float* sa = a.save_act + (((long)t * 2 + dir) * B + b) * G4;
-      const float i_ = sa[j], f_ = sa[H + j], g_ = sa[2 * H + j], o_ = sa[3 * H + j];
-      const float ct = a.save_c[(((long)t * 2 + dir) * B + b) * H + j];
-      const int tq = dir == 0 ? t - 1 : t + 1;  // previous step in forward order
-      const float cp = (tq >= 0 && tq < L) ? a.save_c[(((long)tq * 2 + dir) * B + b) * H + j] : 0.f;
-      const float tc = tanh_(ct);
-      const float dcv = a.dc[sidx] + G * o_ * (1.f - tc * tc);
-      dg[j] = dcv * g_ * i_ * (1.f - i_);
-      dg[H + j] = dcv * cp * f_ * (1.f - f_);
-      dg[2 * H + j] = dcv * i_ * (1.f - g_ * g_);
-      dg[3 * H + j] = G * tc * o_ * (1.f - o_);
-      a.dc[sidx] = dcv * f_;
-      a.dh[sidx] = 0.f;
-    } else {
-      dg[j] = 0.f; dg[H + j] = 0.f; dg[2 * H + j] = 0.f; dg[3 * H + j] = 0.f;
-      a.dh[sidx] = rec + a.dh[sidx];
+      for (int i = 0; i < kBwdWaves; ++i) rec += red[i][b][jl];
+      const long sidx = ((long)dir * B + b) * H + j;
+      float* dg = a.dgates + (((long)b * L + t) * 2 + dir) * G4;
+      if (t < a.len[b]) {
+        const float G = rec + a.dout[((long)b * L + t) * 2 * H + dir * H + j] + a.dh[sidx];
+        const float* sa = a.save_act + (((long)t * 2 + dir) * B + b) * G4;
+        const float i_ = sa[j], f_ = sa[H + j], g_ = sa[2 * H + j], o_ = sa[3 * H + j];
+        const float ct = a.save_c[(((long)t * 2 + dir) * B + b) * H + j];
+        const int tq = dir == 0 ? t - 1 : t + 1;  // previous step in forward order
+        const float cp = (tq >= 0 && tq < L) ? a.save_c[(((long)tq * 2 + dir) * B + b) * H + j] : 0.f;
+        const float tc = tanh_(ct);
+        const float dcv = a.dc[sidx] + G * o_ * (1.f - tc * tc);
+        dg[j] = dcv * g_ * i_ * (1.f - i_);
+        dg[H + j] = dcv * cp * f_ * (1.f - f_);
+        dg[2 * H + j] = dcv * i_ * (1.f - g_ * g_);
+        dg[3 * H + j] = G * tc * o_ * (1.f - o_);
+        a.dc[sidx] = dcv * f_;
+        a.dh[sidx] = 0.f;
+      } else {
+        dg[j] = 0.f; dg[H + j] = 0.f; dg[2 * H + j] = 0.f; dg[3 * H + j] = 0.f;
+        a.dh[sidx] = rec + a.dh[sidx];
+      }
     }
   }
 }
@@ -284,7 +337,7 @@ extern "C" int dasa_bilstm_fwd(const float* xproj, const float* whh_fwd, const f
                                const int32_t* lengths, float* out, float* h_n, float* c_n, float* save_act,
                                float* save_c, int32_t B, int32_t L, int32_t H, float* ws, void* stream) {
   if (B <= 0 || L <= 0) return 0;
-  if ((H % 32) || !ws || (((uintptr_t)whh_fwd | (uintptr_t)whh_bwd) & 15) ||
+  if ((H % 256) || !ws || (((uintptr_t)whh_fwd | (uintptr_t)whh_bwd) & 15) ||
       (save_act != nullptr) != (save_c != nullptr))
     return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
@@ -300,7 +353,7 @@ extern "C" int dasa_bilstm_fwd(const float* xproj, const float* whh_fwd, const f
     a.hin = (s & 1) ? h1 : h0;
     a.hout = (s & 1) ? h0 : h1;
     if (B <= 32) {
-      hipLaunchKernelGGL(bilstm_step_fused_kernel, dim3(H / 8, 2), dim3(256), 0, st, a, s);
+      hipLaunchKernelGGL(bilstm_step_fused_kernel, dim3(H / kFwdUnits, 2), dim3(1024), 0, st, a, s);
       DASA_CHECK_LAUNCH();
     } else {
       for (int dir = 0; dir < 2; ++dir) {
@@ -330,25 +383,37 @@ extern "C" int dasa_bilstm_fwd(const float* xproj, const float* whh_fwd, const f
   return 0;
 }
 
+extern "C" int64_t dasa_bilstm_bwd_workspace(int32_t B, int32_t H) {
+  return (int64_t)((4L * B * H + 8L * H * H) * sizeof(float));
+}
+
 extern "C" int dasa_bilstm_bwd(const float* whh_fwd, const float* whh_bwd, const int32_t* lengths,
-                               const float* save_act, const float* save_c,
-                               const float* dout, const float* dh_n, const float* dc_n, float* dgates, int32_t B,
-                               int32_t L, int32_t H, float* ws, void* stream) {
+                               const float* save_act, const float* save_c, const float* dout, const float* dh_n,
+                               const float* dc_n, float* dgates, int32_t B, int32_t L, int32_t H, float* ws,
+                               void* stream) {
   if (B <= 0 || L <= 0) return 0;
-  if ((H % 32) || !ws || B > 32 || !save_act || !save_c || !dout) return (int)hipErrorInvalidValue;
+  if ((H % 64) || !ws || B > 32 || !save_act || !save_c || !dout || ((uintptr_t)ws & 15))
+    return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   const long S = 2L * B * H;
   float* dh = ws;
   float* dc = ws + S;
+  float* wt0 = ws + 2 * S;
+  wt0 += (16 - ((uintptr_t)wt0 & 15) / 4) % 4;   // 16-B align (ws budget has slack: 8H^2 >> 3)
+  float* wt1 = wt0 + 4L * H * H;
   if (dh_n) hipLaunchKernelGGL(copy_kernel, dim3(cdivi(S, 256)), dim3(256), 0, st, dh_n, dh, S);
   else hipLaunchKernelGGL(fill_kernel, dim3(cdivi(S, 256)), dim3(256), 0, st, dh, S, 0.f);
   DASA_CHECK_LAUNCH();
   if (dc_n) hipLaunchKernelGGL(copy_kernel, dim3(cdivi(S, 256)), dim3(256), 0, st, dc_n, dc, S);
   else hipLaunchKernelGGL(fill_kernel, dim3(cdivi(S, 256)), dim3(256), 0, st, dc, S, 0.f);
   DASA_CHECK_LAUNCH();
-  BpttArgs a{whh_fwd, whh_bwd, lengths, save_act, save_c, dout, dgates, dh, dc, B, L, H};
+  hipLaunchKernelGGL(transpose_kernel, dim3(H / 32, 4 * H / 32), dim3(256), 0, st, whh_fwd, wt0, 4 * H, H);
+  DASA_CHECK_LAUNCH();
+  hipLaunchKernelGGL(transpose_kernel, dim3(H / 32, 4 * H / 32), dim3(256), 0, st, whh_bwd, wt1, 4 * H, H);
+  DASA_CHECK_LAUNCH();
+  BpttArgs a{wt0, wt1, lengths, save_act, save_c, dout, dgates, dh, dc, B, L, H};
   for (int s = 0; s < L; ++s) {
-    hipLaunchKernelGGL(bilstm_bptt_step_kernel, dim3(H / 32, 2), dim3(512), 0, st, a, s);
+    hipLaunchKernelGGL(bilstm_bptt_step_kernel, dim3(H / kBwdUnits, 2), dim3(1024), 0, st, a, s);
     DASA_CHECK_LAUNCH();
   }
   return 0;

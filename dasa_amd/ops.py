@@ -403,7 +403,7 @@ def bilstm_bwd(whh_f, whh_b, lengths_i32, saved, dout, dh_n, dc_n, H):
     L, _, B, _ = sa.shape
     dev = sa.device
     dgates = torch.empty(B, L, 2, 4 * H, dtype=torch.float32, device=dev)
-    ws = torch.empty(4 * B * H, dtype=torch.float32, device=dev)
+    ws = torch.empty(_lib.lib().dasa_bilstm_bwd_workspace(B, H) // 4 + 4, dtype=torch.float32, device=dev)
     _call("dasa_bilstm_bwd", "bilstm_bptt", _lib.lib().dasa_bilstm_bwd, _p(whh_f.contiguous()), _p(whh_b.contiguous()),
           _p(lengths_i32), _p(sa), _p(sc), _p(dout.contiguous()),
           _p(dh_n.contiguous() if dh_n is not None else None),

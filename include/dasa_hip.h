@@ -130,7 +130,9 @@ int dasa_bilstm_fwd(const float* xproj, const float* whh_fwd, const float* whh_b
                     const int32_t* lengths, float* out, float* h_n, float* c_n, float* save_act,
                     float* save_c, int32_t B, int32_t L, int32_t H, float* ws, void* stream);
 /* BPTT: dout [B][L][2H], dh_n/dc_n [2][B][H] (may be NULL) -> dgates [B][L][2][4H] (time-major
- * grads of the pre-activation gates; zero at padded steps). B <= 32. ws: 4*B*H floats.          */
+ * grads of the pre-activation gates; zero at padded steps). B <= 32, H % 64 == 0.
+ * ws: dasa_bilstm_bwd_workspace(B, H) bytes (carries + W_hh^T of both directions).              */
+int64_t dasa_bilstm_bwd_workspace(int32_t B, int32_t H);
 int dasa_bilstm_bwd(const float* whh_fwd, const float* whh_bwd, const int32_t* lengths,
                     const float* save_act, const float* save_c,
                     const float* dout, const float* dh_n, const float* dc_n, float* dgates,
