@@ -10,6 +10,7 @@
 // (bias, activation, gate-multiply for DGAdaChannel, column scale for env-drop, beta accumulate).
 // Split-K over gridDim.z with a deterministic fixed-order reduce for skinny (M<=64) decoder GEMMs.
 #include "common.h"
+#include <cstdlib>
 #include "../../include/dasa_hip.h"
 
 namespace {
@@ -68,11 +69,12 @@ __device__ __forceinline__ float4 sel4(bool c, float4 v) {
 }
 
 // KC = operand stored with K contiguous ([rows][K]); else stored [K][rows].
-template <int ROWS, bool KC, bool VEC>
+template <int ROWS, bool KC, bool VEC, int NT>
 struct TileLoader {
   static constexpr int PAD = KC ? 1 : 4;
-  static constexpr int NF4 = ROWS * BKT / 4 / 256;
-  static_assert(NF4 >= 1, "tile too small");
+  static constexpr int TOTAL = ROWS * BKT / 4;   // float4 per tile
+  static constexpr int NF4 = (TOTAL + NT - 1) / NT;
+  static constexpr bool EXACT = (TOTAL % NT) == 0;
   float4 r[NF4];
 
   __device__ __forceinline__ void load(const float* base, long ld, int r0, int rlimit, int k0, int klimit) {
@@ -80,7 +82,7 @@ struct TileLoader {
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int i = 0; i < NF4; ++i) {
-      const int q = tid + 256 * i;
+      const int q = EXACT ? tid + NT * i : min(tid + NT * i, TOTAL - 1);   // surplus threads re-load a valid quad
       if (VEC) {
         // Unconditional, clamped loads + a select: a branch around each load would make hipcc wait
         // vmcnt(0) per load and serialise the tile fetch. With K % 4 == 0 (VEC) a quad is either fully
@@ -111,7 +113,8 @@ struct TileLoader {
     const int tid = threadIdx.x;
 #pragma unroll
     for (int i = 0; i < NF4; ++i) {
-      const int q = tid + 256 * i;
+      const int q = tid + NT * i;
+      if (!EXACT && q >= TOTAL) continue;
       if (KC) {
         const int row = q / (BKT / 4), kq = q % (BKT / 4);
         S[4 * kq + 0][row] = r[i].x;
@@ -126,18 +129,25 @@ struct TileLoader {
   }
 };
 
-template <int BM, int BN, int WM, int WN, bool AKC, bool BKC, bool VEC>
-__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p) {
+// KW > 1 splits every 32-deep K-tile between KW wave groups that own the same output sub-tiles
+// (in-block split-K): more waves per block for mid-size GEMMs, reduced through LDS at the end.
+template <int BM, int BN, int WM, int WN, int KW, bool AKC, bool BKC, bool VEC>
+__global__ __launch_bounds__(64 * (BM / WM) * (BN / WN) * KW) void gemm_f32_kernel(GemmP p) {
   constexpr int TM = WM / 32, TN = WN / 32;
   constexpr int WAVES_N = BN / WN;
-  static_assert((BM / WM) * (BN / WN) == 4, "4 waves per block");
-  using LA = TileLoader<BM, AKC, VEC>;
-  using LB = TileLoader<BN, BKC, VEC>;
+  constexpr int NWG = (BM / WM) * (BN / WN);
+  constexpr int NT = 64 * NWG * KW;
+  static_assert(BKT % (2 * KW) == 0, "K-split must divide the K tile");
+  using LA = TileLoader<BM, AKC, VEC, NT>;
+  using LB = TileLoader<BN, BKC, VEC, NT>;
   __shared__ float As[2][BKT][BM + LA::PAD];
   __shared__ float Bs[2][BKT][BN + LB::PAD];
+  static_assert((KW - 1) * BM * BN <= 2 * BKT * (BM + LA::PAD) + 2 * BKT * (BN + LB::PAD),
+                "LDS too small for the K-split reduction");
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = (wave / WAVES_N) * WM, wn = (wave % WAVES_N) * WN;
+  const int kgrp = wave / NWG, wt = wave % NWG;
+  const int wm = (wt / WAVES_N) * WM, wn = (wt % WAVES_N) * WN;
   const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
   const int b = blockIdx.z / p.splitk, split = blockIdx.z % p.splitk;
   const int kbeg = split * p.kchunk;
@@ -173,7 +183,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p) {
       lb.load(B, p.ldb, n0, p.N, k0, kend);
     }
 #pragma unroll
-    for (int kk = 0; kk < BKT; kk += 2) {
+    for (int kk = kgrp * (BKT / KW); kk < (kgrp + 1) * (BKT / KW); kk += 2) {
       float av[TM], bv[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) av[i] = As[buf][kk + hl][wm + i * 32 + rl];
@@ -192,6 +202,30 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p) {
     __syncthreads();
   }
 
+  if (KW > 1) {   // fold the K-split wave groups into group 0 through LDS
+    float* red = &As[0][0][0];
+    __syncthreads();
+    if (kgrp > 0) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            red[((((kgrp - 1) * NWG + wt) * TM + i) * TN + j) * 1024 + r * 64 + lane] = acc[i][j][r];
+    }
+    __syncthreads();
+    if (kgrp > 0) return;
+#pragma unroll
+    for (int g = 1; g < KW; ++g)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            acc[i][j][r] += red[((((g - 1) * NWG + wt) * TM + i) * TN + j) * 1024 + r * 64 + lane];
+  }
   // C/D map of the 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
   // Epilogue: every optional operand is fetched with unconditional clamped loads inside ONE uniform
   // branch per operand (a per-element branch around a load makes hipcc wait vmcnt(0) per element).
@@ -287,16 +321,54 @@ __global__ void splitk_reduce_kernel(GemmP p) {
   }
 }
 
-template <int BM, int BN, int WM, int WN, bool VEC>
+template <int BM, int BN, int WM, int WN, int KW, bool VEC>
 int launch_tile(const GemmP& p, int opA, int opB, hipStream_t st) {
   dim3 grid((p.N + BN - 1) / BN, (p.M + BM - 1) / BM, p.batch * p.splitk);
+  dim3 block(64 * (BM / WM) * (BN / WN) * KW);
   const bool akc = (opA == 0), bkc = (opB == 1);
-  if (akc && bkc) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, true, true, VEC>), grid, dim3(256), 0, st, p);
-  else if (akc && !bkc) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, true, false, VEC>), grid, dim3(256), 0, st, p);
-  else if (!akc && bkc) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, false, true, VEC>), grid, dim3(256), 0, st, p);
-  else hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, false, false, VEC>), grid, dim3(256), 0, st, p);
+  if (akc && bkc) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, KW, true, true, VEC>), grid, block, 0, st, p);
+  else if (akc && !bkc) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, KW, true, false, VEC>), grid, block, 0, st, p);
+  else if (!akc && bkc) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, KW, false, true, VEC>), grid, block, 0, st, p);
+  else hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, KW, false, false, VEC>), grid, block, 0, st, p);
   DASA_CHECK_LAUNCH();
   return 0;
+}
+
+// Tile configurations: {BM, BN, WM, WN, KW}
+struct TileCfg { int bm, bn, wm, wn, kw; };
+constexpr TileCfg kCfgs[] = {
+    {128, 128, 64, 64, 1},  // 0: large GEMMs
+    {64, 128, 32, 64, 1},   // 1
+    {64, 64, 32, 32, 1},    // 2
+    {32, 128, 32, 32, 1},   // 3: skinny M
+    {64, 64, 32, 32, 2},    // 4: mid-size, 8 waves
+    {32, 64, 32, 32, 2},    // 5: mid-size, many small blocks
+    {128, 64, 64, 32, 1},   // 6
+    {64, 128, 32, 64, 2},   // 7
+    {128, 128, 64, 64, 2},  // 8
+    {32, 64, 32, 32, 4},    // 9
+    {64, 32, 32, 32, 2},    // 10
+};
+constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
+
+int launch_cfg(int cfg, bool vec, const GemmP& p, int opA, int opB, hipStream_t st) {
+  if (!vec) {
+    return kCfgs[cfg].bm == 32 ? launch_tile<32, 128, 32, 32, 1, false>(p, opA, opB, st)
+                               : launch_tile<64, 64, 32, 32, 1, false>(p, opA, opB, st);
+  }
+  switch (cfg) {
+    case 0: return launch_tile<128, 128, 64, 64, 1, true>(p, opA, opB, st);
+    case 1: return launch_tile<64, 128, 32, 64, 1, true>(p, opA, opB, st);
+    case 2: return launch_tile<64, 64, 32, 32, 1, true>(p, opA, opB, st);
+    case 3: return launch_tile<32, 128, 32, 32, 1, true>(p, opA, opB, st);
+    case 4: return launch_tile<64, 64, 32, 32, 2, true>(p, opA, opB, st);
+    case 5: return launch_tile<32, 64, 32, 32, 2, true>(p, opA, opB, st);
+    case 6: return launch_tile<128, 64, 64, 32, 1, true>(p, opA, opB, st);
+    case 7: return launch_tile<64, 128, 32, 64, 2, true>(p, opA, opB, st);
+    case 8: return launch_tile<128, 128, 64, 64, 2, true>(p, opA, opB, st);
+    case 9: return launch_tile<32, 64, 32, 32, 4, true>(p, opA, opB, st);
+    default: return launch_tile<64, 32, 32, 32, 2, true>(p, opA, opB, st);
+  }
 }
 
 inline long cdiv(long a, long b) { return (a + b - 1) / b; }
@@ -305,17 +377,28 @@ inline long cdiv(long a, long b) { return (a + b - 1) / b; }
 
 struct Plan { int cfg, splitk, kchunk; int64_t ws; };
 
+static int g_force_cfg = -2;   // DASA_GEMM_CFG=<index> pins a tile config (tuning sweeps)
+
 static Plan make_plan(const dasa_gemm_desc* d) {
   const int M = d->M, N = d->N, K = d->K, batch = d->batch < 1 ? 1 : d->batch;
-  // Tile choice (DESIGN.md "GEMM"): fill 256 CUs first, then maximise per-wave reuse.
+  if (g_force_cfg == -2) {
+    const char* e = getenv("DASA_GEMM_CFG");
+    g_force_cfg = e ? atoi(e) : -1;
+  }
   auto tiles = [&](int bm, int bn) { return cdiv(M, bm) * cdiv(N, bn) * batch; };
   Plan pl;
+  // Tile choice (DESIGN.md "GEMM"): fill the 256 CUs with >= 1 full wave of blocks, prefer fewer,
+  // larger tiles when there are plenty, and split K inside the block (KW = 2) for mid-size shapes.
+  // Rules fitted to the MI355X sweep in profiles/r01_gemm_sweep_v2.txt (policy shapes).
+  const long t64 = tiles(64, 64);
   if (M <= 32) pl.cfg = 3;
-  else if (tiles(128, 128) >= 240) pl.cfg = 0;
-  else if (tiles(64, 128) >= 200) pl.cfg = 1;
-  else pl.cfg = 2;
-  const int bm = (pl.cfg == 0) ? 128 : (pl.cfg == 3 ? 32 : 64);
-  const int bn = (pl.cfg == 2) ? 64 : 128;
+  else if (t64 >= 2048) pl.cfg = 0;
+  else if (t64 >= 500) pl.cfg = 2;
+  else if (t64 >= 250) pl.cfg = 10;
+  else if (K >= 2048) pl.cfg = 0;     // few tiles, long K: 128x128 + split-K
+  else pl.cfg = 7;
+  if (g_force_cfg >= 0 && g_force_cfg < kNumCfgs) pl.cfg = g_force_cfg;
+  const int bm = kCfgs[pl.cfg].bm, bn = kCfgs[pl.cfg].bn;
   const long blocks = tiles(bm, bn);
   int splitk = 1;
   if (blocks < 160 && K >= 512) {
@@ -332,6 +415,11 @@ static Plan make_plan(const dasa_gemm_desc* d) {
   pl.kchunk = kchunk;
   pl.ws = splitk > 1 ? (int64_t)splitk * batch * M * N * (int64_t)sizeof(float) : 0;
   return pl;
+}
+
+extern "C" int dasa_gemm_force_config(int cfg) {
+  g_force_cfg = cfg;
+  return kNumCfgs;
 }
 
 extern "C" int64_t dasa_gemm_f32_workspace(const dasa_gemm_desc* d) {
@@ -371,17 +459,7 @@ extern "C" int dasa_gemm_f32(const dasa_gemm_desc* d, void* ws, int64_t ws_bytes
   p.ws = (float*)ws;
   hipStream_t st = (hipStream_t)stream;
   int rc;
-  if (!vec) {
-    rc = pl.cfg == 3 ? launch_tile<32, 128, 32, 32, false>(p, d->opA, d->opB, st)
-                     : launch_tile<64, 64, 32, 32, false>(p, d->opA, d->opB, st);
-  } else {
-    switch (pl.cfg) {
-      case 0: rc = launch_tile<128, 128, 64, 64, true>(p, d->opA, d->opB, st); break;
-      case 1: rc = launch_tile<64, 128, 32, 64, true>(p, d->opA, d->opB, st); break;
-      case 3: rc = launch_tile<32, 128, 32, 32, true>(p, d->opA, d->opB, st); break;
-      default: rc = launch_tile<64, 64, 32, 32, true>(p, d->opA, d->opB, st); break;
-    }
-  }
+  rc = launch_cfg(pl.cfg, vec, p, d->opA, d->opB, st);
   if (rc) return rc;
   if (pl.splitk > 1) {
     const long total = (long)batch * M * N;

@@ -27,7 +27,37 @@ def bench(fn, it=20):
     return e0.elapsed_time(e1) / it
 
 
+def sweep():
+    from dasa_amd import _lib
+    L = _lib.lib()
+    n = L.dasa_gemm_force_config(-1)
+    dev = torch.device("cuda")
+    print(f"{'shape':<18}" + "".join(f"{c:>7}" for c in range(n)) + "   auto  torch")
+    for M, N, K, name in SHAPES:
+        if "(tn)" in name:
+            A = torch.randn(K, M, device=dev)
+            B = torch.randn(K, N, device=dev)
+            f1 = lambda: ops.matmul_tn(A, B)
+            f2 = lambda: A.t() @ B
+        else:
+            A = torch.randn(M, K, device=dev)
+            W = torch.randn(N, K, device=dev)
+            f1 = lambda: ops.linear(A, W)
+            f2 = lambda: A @ W.t()
+        fl = 2.0 * M * N * K
+        row = []
+        for c in range(n):
+            L.dasa_gemm_force_config(c)
+            row.append(fl / bench(f1) / 1e9)
+        L.dasa_gemm_force_config(-1)
+        row.append(fl / bench(f1) / 1e9)
+        row.append(fl / bench(f2) / 1e9)
+        print(f"{name:<18}" + "".join(f"{x:>7.1f}" for x in row), flush=True)
+
+
 def main():
+    if "--sweep" in sys.argv:
+        return sweep()
     dev = torch.device("cuda")
     torch.backends.cuda.matmul.allow_tf32 = False
     print(f"{'shape':<18}{'M':>6}{'N':>6}{'K':>6}{'dasa us':>10}{'TF':>8}{'torch us':>10}{'TF':>8}")
