@@ -44,7 +44,10 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-fwd", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=16)
-    p.add_argument("--profile-kernels", action="store_true", default=True)
+    p.add_argument("--no-profile", action="store_true")
+    p.add_argument("--backend", default="nccl", help="nccl (= RCCL on ROCm) | gloo (rehearsal only)")
+    p.add_argument("--same-device", action="store_true",
+                   help="map every rank to cuda:0 (rehearsing the DP path on a one-GPU box with gloo)")
     return p.parse_args()
 
 
@@ -53,9 +56,13 @@ def setup_dist(a):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
+        dev = 0 if a.same_device else local
+        torch.cuda.set_device(dev)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(a.backend)
     else:
         torch.cuda.set_device(0)
     return rank, world
@@ -184,7 +191,7 @@ def main():
         fu, fdt = timed(lambda: fwd_rollout(agent), 2, rank, world)
         out["fwd_value"] = round(fu / fdt, 2)
         out["fwd_note"] = "eval/argmax rollout decisions/s (language stack computed once per batch: exact in eval)"
-    if a.profile_kernels:
+    if not a.no_profile:
         summ = kernel_profile(agent, lambda: train_step(agent))
         if rank == 0:
             out.update(summ)

@@ -140,10 +140,13 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN) * KW) void gemm_f32_kern
   static_assert(BKT % (2 * KW) == 0, "K-split must divide the K tile");
   using LA = TileLoader<BM, AKC, VEC, NT>;
   using LB = TileLoader<BN, BKC, VEC, NT>;
-  __shared__ float As[2][BKT][BM + LA::PAD];
-  __shared__ float Bs[2][BKT][BN + LB::PAD];
-  static_assert((KW - 1) * BM * BN <= 2 * BKT * (BM + LA::PAD) + 2 * BKT * (BN + LB::PAD),
-                "LDS too small for the K-split reduction");
+  // one LDS array: the A/B double buffers, reused by the K-split reduction after the main loop
+  constexpr int A_FL = 2 * BKT * (BM + LA::PAD), B_FL = 2 * BKT * (BN + LB::PAD);
+  constexpr int RED_FL = (KW - 1) * BM * BN;
+  constexpr int SMEM_FL = (A_FL + B_FL) > RED_FL ? (A_FL + B_FL) : RED_FL;
+  __shared__ __attribute__((aligned(16))) float smem[SMEM_FL];
+  auto As = reinterpret_cast<float (*)[BKT][BM + LA::PAD]>(smem);
+  auto Bs = reinterpret_cast<float (*)[BKT][BN + LB::PAD]>(smem + A_FL);
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int kgrp = wave / NWG, wt = wave % NWG;
@@ -203,7 +206,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN) * KW) void gemm_f32_kern
   }
 
   if (KW > 1) {   // fold the K-split wave groups into group 0 through LDS
-    float* red = &As[0][0][0];
+    float* red = smem;
     __syncthreads();
     if (kgrp > 0) {
 #pragma unroll

@@ -1,0 +1,66 @@
+"""Drop-in launcher: run the reference's r2r_src/train.py unchanged on the MI355X policy.
+
+    python -m dasa_amd.launch /path/to/DASA/r2r_src/train.py --agent_type dg --adaIn_type channel ...
+
+train.py does `from param import args`, `from agent_dg import Seq2SeqAgent`, and its helpers import
+`model`, `vilmodel`, `r2rmodel`. This launcher binds those module names to dasa_amd.r2r (whose
+classes, signatures, state_dict keys and args flags match the reference), parses the command line
+into the shared `args` like param.py does at import, and executes train.py as __main__. Everything
+else (env, utils, speaker, eval, tokenizers, MatterSim) is the reference's own code. Names the
+policy modules do not define (e.g. SpeakerEncoder/SpeakerDecoder, the alternative decoders) resolve
+to the reference's definitions, loaded under a private module name.
+"""
+import importlib.util
+import os
+import runpy
+import sys
+import types
+
+
+def _load_reference(name, path):
+    spec = importlib.util.spec_from_file_location("_dasa_ref_" + name, path)
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[spec.name] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def _proxy(ours, ref_dir, name):
+    """Module `name`: our definitions, falling back to the reference module for anything else."""
+    px = types.ModuleType(name)
+    px.__dict__.update({k: v for k, v in vars(ours).items() if not k.startswith("__")})
+    ref_path = os.path.join(ref_dir, name + ".py")
+    state = {}
+
+    def __getattr__(attr):
+        if "ref" not in state:
+            if not os.path.exists(ref_path):
+                raise AttributeError(attr)
+            state["ref"] = _load_reference(name, ref_path)
+        return getattr(state["ref"], attr)
+    px.__getattr__ = __getattr__
+    px.__file__ = ours.__file__
+    return px
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    if not argv:
+        print(__doc__)
+        return 2
+    script = os.path.abspath(argv[0])
+    ref_dir = os.path.dirname(script)
+    sys.argv = [script] + argv[1:]
+    sys.path.insert(0, ref_dir)
+    from dasa_amd.r2r import param
+    param.parse(sys.argv[1:], make_dirs=True)
+    sys.modules["param"] = param
+    from dasa_amd.r2r import agent_dg, model, r2rmodel, vilmodel
+    for name, ours in (("model", model), ("vilmodel", vilmodel), ("r2rmodel", r2rmodel), ("agent_dg", agent_dg)):
+        sys.modules[name] = _proxy(ours, ref_dir, name)
+    runpy.run_path(script, run_name="__main__")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

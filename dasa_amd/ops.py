@@ -269,6 +269,8 @@ def mha(Q, K, V, addmask, heads, scale, drop_p=0.0, seed=0, save_probs=False):
     B, Lq, Hd = Q.shape
     Lk = K.shape[1]
     dh = Hd // heads
+    for t in (Q, K, V):   # rows may be strided views of a fused QKV buffer, heads contiguous inside a row
+        assert t.stride(2) == 1 and t.stride(0) == t.shape[1] * t.stride(1)
     out = torch.empty(B, Lq, Hd, dtype=torch.float32, device=Q.device)
     probs = torch.empty(B, heads, Lq, Lk, dtype=torch.float32, device=Q.device) if save_probs else None
     _call("dasa_mha_fwd", "mha", _lib.lib().dasa_mha_fwd, _p(Q), Q.stride(1), _p(K), K.stride(1), _p(V), V.stride(1),

@@ -55,6 +55,25 @@ def _lin(x, m, act=None):
     return DF.linear(x, m.weight, m.bias, act)
 
 
+def _needs_grad(*ts):
+    return torch.is_grad_enabled() and any(t.requires_grad for t in ts)
+
+
+def _fused_weights(owner, mods):
+    """Concatenated [W_1; W_2; ...] / [b_1; ...] of several nn.Linear (one wide MFMA GEMM instead of
+    several narrow ones), cached until any of the parameters changes (data_ptr or in-place version)."""
+    params = [t for m in mods for t in (m.weight, m.bias)]
+    key = tuple((t.data_ptr(), t._version) for t in params)
+    cache = getattr(owner, "_fused_cache", None)
+    if cache is None or cache[0] != key:
+        with torch.no_grad():
+            W = torch.cat([m.weight for m in mods], 0).contiguous()
+            b = torch.cat([m.bias for m in mods], 0).contiguous()
+        cache = (key, W, b)
+        owner._fused_cache = cache
+    return cache[1], cache[2]
+
+
 class BertEmbeddings(nn.Module):
     """vilmodel.py:147-176: word + position + token_type(0) -> LayerNorm -> dropout, one kernel."""
 
@@ -94,7 +113,13 @@ class BertSelfAttention(nn.Module):
     def forward(self, hidden_states, attention_mask, head_mask=None):
         if head_mask is not None:
             raise NotImplementedError("head_mask")
-        q, k, v = _lin(hidden_states, self.query), _lin(hidden_states, self.key), _lin(hidden_states, self.value)
+        if _needs_grad(hidden_states, self.query.weight, self.key.weight, self.value.weight):
+            q, k, v = _lin(hidden_states, self.query), _lin(hidden_states, self.key), _lin(hidden_states, self.value)
+        else:   # one [M, 3H] GEMM; Q/K/V are row-strided views the attention kernel reads in place
+            W, b = _fused_weights(self, (self.query, self.key, self.value))
+            qkv = ops.linear(hidden_states, W, b)
+            Hs = self.all_head_size
+            q, k, v = qkv[..., :Hs], qkv[..., Hs:2 * Hs], qkv[..., 2 * Hs:]
         ctx = DF.mha(q, k, v, _addmask(attention_mask, q.shape[0]), self.num_attention_heads,
                      1.0 / math.sqrt(self.attention_head_size), self.dropout.p, self.training)
         return (ctx,)
@@ -195,7 +220,14 @@ class BertOutAttention(nn.Module):
         self.dropout = nn.Dropout(config.attention_probs_dropout_prob)
 
     def forward(self, hidden_states, context, attention_mask=None):
-        q, k, v = _lin(hidden_states, self.query), _lin(context, self.key), _lin(context, self.value)
+        q = _lin(hidden_states, self.query)
+        if _needs_grad(context, self.key.weight, self.value.weight):
+            k, v = _lin(context, self.key), _lin(context, self.value)
+        else:
+            W, b = _fused_weights(self, (self.key, self.value))
+            kv = ops.linear(context, W, b)
+            Hs = self.all_head_size
+            k, v = kv[..., :Hs], kv[..., Hs:]
         return DF.mha(q, k, v, _addmask(attention_mask, q.shape[0]), self.num_attention_heads,
                       1.0 / math.sqrt(self.attention_head_size), self.dropout.p, self.training)
 

@@ -102,3 +102,24 @@ def test_oracle_sort_and_masks():
     seq, mask, lens, perm = O.sort_batch(obs)
     assert lens == [5, 3] and perm == [1, 0] and mask.shape == (2, 5) and mask[1, 3:].all()
     assert O.length2mask([3, 1]).tolist() == [[False, False, False], [False, True, True]]
+
+
+def test_dropin_launcher_binds_reference_module_names(tmp_path, monkeypatch):
+    """dasa_amd.launch runs an unchanged train.py with param/agent_dg/model bound to dasa_amd.r2r and
+    reference-only names (e.g. SpeakerEncoder) falling back to the reference file."""
+    import subprocess
+    import sys
+    (tmp_path / "model.py").write_text("SpeakerEncoder = 'reference-speaker-encoder'\n")
+    (tmp_path / "train.py").write_text(
+        "from param import args\n"
+        "import model, agent_dg\n"
+        "assert args.d_vl_layers == 3 and args.use_shift, args.d_vl_layers\n"
+        "assert agent_dg.Seq2SeqAgent.__module__.startswith('dasa_amd.r2r')\n"
+        "assert model.BAttnDecoderLSTM.__module__ == 'dasa_amd.r2r.model'\n"
+        "assert model.SpeakerEncoder == 'reference-speaker-encoder'\n"
+        "print('DROPIN-OK')\n")
+    from dasa_amd.r2r import param
+    r = subprocess.run([sys.executable, "-m", "dasa_amd.launch", str(tmp_path / "train.py")] + param.README_TRAIN_FLAGS,
+                       cwd=str(tmp_path), capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, PYTHONPATH=ROOT))
+    assert r.returncode == 0 and "DROPIN-OK" in r.stdout, r.stderr[-2000:]

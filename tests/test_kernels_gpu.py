@@ -64,6 +64,35 @@ def test_gemm_layouts(dev):
     assert (ops.colsum(B2.to(dev)).cpu() - B2.sum(0)).abs().max() < 1e-5
 
 
+def test_gemm_every_config(dev):
+    """Force each tile configuration (incl. in-block K-split and split-K) over ragged shapes, both
+    operand layouts and the fused epilogue, so a config the shape rules pick only at bench sizes is
+    still checked."""
+    from dasa_amd import _lib, ops
+    lib = _lib.lib()
+    ncfg = lib.dasa_gemm_force_config(-1)
+    g = torch.Generator().manual_seed(11)
+    shapes = [(37, 45, 100), (130, 200, 36), (64, 128, 1024), (257, 96, 2100)]
+    try:
+        for cfg in range(ncfg):
+            lib.dasa_gemm_force_config(cfg)
+            for M, N, K in shapes:
+                x, W, b = _rand(M, K, g=g), _rand(N, K, g=g, scale=0.05), _rand(N, g=g)
+                aux = _rand(M, N, g=g)
+                z = torch.nn.functional.linear(x.double(), W.double(), b.double())
+                ref = (torch.tanh(z) * aux.double()).float()
+                y = ops.linear(x.to(dev), W.to(dev), b.to(dev), act="tanh", aux=aux.to(dev)).cpu()
+                assert (y - ref).abs().max().item() < 1e-5, (cfg, M, N, K)
+                B = _rand(K, N, g=g)
+                ref_nn = (x.double() @ B.double()).float()
+                tol = 1e-4 * max(1.0, ref_nn.abs().max().item())
+                assert (ops.matmul_nn(x.to(dev), B.to(dev)).cpu() - ref_nn).abs().max() < tol, (cfg, M, N, K)
+                xt = x.t().contiguous()
+                assert (ops.matmul_tn(xt.to(dev), B.to(dev)).cpu() - ref_nn).abs().max() < tol, (cfg, M, N, K)
+    finally:
+        lib.dasa_gemm_force_config(-1)
+
+
 def test_layernorm_and_embed(dev):
     from dasa_amd import ops
     g = torch.Generator().manual_seed(7)

@@ -1,7 +1,36 @@
+#!/bin/bash
+# One GPU session: parity tests, smoke, DP rehearsal (2 ranks on one GPU over gloo), bench, rocprof stats.
+# Any step that faults, aborts or times out ends the session (nothing else touches the GPU after it).
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -m pytest tests/test_kernels_gpu.py -q -m gpu > gpurun_out/k4.log 2>&1; echo k_rc=$?
-timeout -k 10 200 python tools/gemm_bench.py > gpurun_out/gemm2.log 2>&1; echo g_rc=$?
-timeout -k 10 600 python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/bench3.log 2>&1; echo bench_rc=$?
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof1 -o r01 -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-fwd > gpurun_out/prof1.log 2>&1; echo prof_rc=$?
+TAG=${TAG:-r01}
+
+step() {   # step <name> <timeout> <log> cmd...
+  local name=$1 t=$2 log=$3; shift 3
+  timeout -k 10 "$t" "$@" > "$log" 2>&1
+  local rc=$?
+  echo "${name}_rc=$rc"
+  case $rc in
+    124|134|137|139) echo "stopping after $name (rc=$rc)"; tail -20 "$log"; exit $rc ;;
+  esac
+  return 0
+}
+
+step tests 400 gpurun_out/tests_$TAG.log python -m pytest tests -q -m gpu
+grep -E "passed|failed" gpurun_out/tests_$TAG.log | tail -3
+step smoke 200 gpurun_out/smoke_$TAG.log python -c "import __graft_entry__ as g; g.smoke()"
+if [ "${DP:-1}" = "1" ]; then
+  step dp 400 gpurun_out/dp2_$TAG.log python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+    --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 1 --warmup 0 --backend gloo \
+    --same-device --no-fwd --no-profile --max-action 4
+fi
+step bench 600 gpurun_out/bench_$TAG.log python bench.py --steps ${STEPS:-3} --warmup 1
+tail -1 gpurun_out/bench_$TAG.log
+if [ "${PROF:-1}" = "1" ]; then
+  cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+  step prof 600 gpurun_out/profrun_$TAG.log rocprofv3 --kernel-trace --stats --output-format csv \
+    -d gpurun_out/prof_$TAG -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-fwd
+  # keep only the summaries (the full kernel trace is far larger than gpurun's copy-back limit)
+  find gpurun_out/prof_$TAG \( -name "*kernel_trace*" -o -name "*.db" \) -delete 2>/dev/null
+  find gpurun_out/prof_$TAG -type f
+fi
