@@ -45,6 +45,7 @@ def parse():
     p.add_argument("--no-fwd", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--no-profile", action="store_true")
+    p.add_argument("--shapes", type=int, default=0, help="add the top-N GEMM shapes by device time")
     p.add_argument("--backend", default="nccl", help="nccl (= RCCL on ROCm) | gloo (rehearsal only)")
     p.add_argument("--same-device", action="store_true",
                    help="map every rank to cuda:0 (rehearsing the DP path on a one-GPU box with gloo)")
@@ -128,11 +129,11 @@ def timed(fn, n, rank, world):
     return units, dt
 
 
-def kernel_profile(agent, fn):
+def kernel_profile(agent, fn, shapes=0):
     """One extra (untimed) step with HIP events around every libdasa_hip launch on its stream:
     per-kernel-family device time + algorithmic FLOPs/bytes for the roofline."""
     from dasa_amd import prof
-    with prof.collect() as rec:
+    with prof.collect(shapes) as rec:
         fn()
     return rec.summary()
 
@@ -192,7 +193,7 @@ def main():
         out["fwd_value"] = round(fu / fdt, 2)
         out["fwd_note"] = "eval/argmax rollout decisions/s (language stack computed once per batch: exact in eval)"
     if not a.no_profile:
-        summ = kernel_profile(agent, lambda: train_step(agent))
+        summ = kernel_profile(agent, lambda: train_step(agent), a.shapes)
         if rank == 0:
             out.update(summ)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

@@ -69,13 +69,18 @@ __device__ __forceinline__ float4 sel4(bool c, float4 v) {
 }
 
 // KC = operand stored with K contiguous ([rows][K]); else stored [K][rows].
+// LDS images: KC -> [ROWS][BKT] with the eight 16-B quads of each row XOR-swizzled by (row>>1)&7, so
+// the K-permuted ds_read_b128 fragment reads below hit 16 distinct bank slots per lane group;
+// !KC -> [BKT][ROWS + 4] (k-major, read one float per lane).
 template <int ROWS, bool KC, bool VEC, int NT>
 struct TileLoader {
-  static constexpr int PAD = KC ? 1 : 4;
+  static constexpr int PAD = KC ? 0 : 4;
+  static constexpr int LDS_FL = KC ? ROWS * BKT : BKT * (ROWS + PAD);
   static constexpr int TOTAL = ROWS * BKT / 4;   // float4 per tile
   static constexpr int NF4 = (TOTAL + NT - 1) / NT;
   static constexpr bool EXACT = (TOTAL % NT) == 0;
   float4 r[NF4];
+  bool ok[NF4];
 
   __device__ __forceinline__ void load(const float* base, long ld, int r0, int rlimit, int k0, int klimit) {
     const int tid = threadIdx.x;
@@ -84,50 +89,66 @@ struct TileLoader {
     for (int i = 0; i < NF4; ++i) {
       const int q = EXACT ? tid + NT * i : min(tid + NT * i, TOTAL - 1);   // surplus threads re-load a valid quad
       if (VEC) {
-        // Unconditional, clamped loads + a select: a branch around each load would make hipcc wait
-        // vmcnt(0) per load and serialise the tile fetch. With K % 4 == 0 (VEC) a quad is either fully
-        // in range or fully out.
+        // Unconditional, clamped loads; the range select is applied when the tile is written to LDS
+        // (after the MFMAs), so the loads stay in flight across the compute of the current tile.
+        // With K % 4 == 0 (VEC) a quad is either fully in range or fully out.
         if (KC) {
           const int row = q / (BKT / 4), kq = q % (BKT / 4);
           const int gr = r0 + row, gk = k0 + 4 * kq;
-          const float4 v = *reinterpret_cast<const float4*>(base + (long)min(gr, rlimit - 1) * ld + min(gk, klimit - 4));
-          r[i] = sel4(gr < rlimit && gk < klimit, v);
+          r[i] = *reinterpret_cast<const float4*>(base + (long)min(gr, rlimit - 1) * ld + min(gk, klimit - 4));
+          ok[i] = gr < rlimit && gk < klimit;
         } else {
           const int kr = q / (ROWS / 4), rq = q % (ROWS / 4);
           const int gk = k0 + kr, gr = r0 + 4 * rq;
-          const float4 v = *reinterpret_cast<const float4*>(base + (long)min(gk, klimit - 1) * ld + min(gr, rlimit - 4));
-          r[i] = sel4(gk < klimit && gr < rlimit, v);
+          r[i] = *reinterpret_cast<const float4*>(base + (long)min(gk, klimit - 1) * ld + min(gr, rlimit - 4));
+          ok[i] = gk < klimit && gr < rlimit;
         }
       } else if (KC) {
         const int row = q / (BKT / 4), kq = q % (BKT / 4);
         const int gr = r0 + row;
         r[i] = (gr < rlimit) ? load4<VEC>(base + (long)gr * ld, k0 + 4 * kq, klimit) : z;
+        ok[i] = true;
       } else {
         const int kr = q / (ROWS / 4), rq = q % (ROWS / 4);
         const int gk = k0 + kr;
         r[i] = (gk < klimit) ? load4<VEC>(base + (long)gk * ld, r0 + 4 * rq, rlimit) : z;
+        ok[i] = true;
       }
     }
   }
-  __device__ __forceinline__ void store(float (*S)[ROWS + PAD]) {
+  __device__ __forceinline__ void store(float* S) {
     const int tid = threadIdx.x;
 #pragma unroll
     for (int i = 0; i < NF4; ++i) {
       const int q = tid + NT * i;
       if (!EXACT && q >= TOTAL) continue;
+      const float4 v = sel4(ok[i], r[i]);
       if (KC) {
         const int row = q / (BKT / 4), kq = q % (BKT / 4);
-        S[4 * kq + 0][row] = r[i].x;
-        S[4 * kq + 1][row] = r[i].y;
-        S[4 * kq + 2][row] = r[i].z;
-        S[4 * kq + 3][row] = r[i].w;
+        *reinterpret_cast<float4*>(S + row * BKT + 4 * (kq ^ ((row >> 1) & 7))) = v;
       } else {
         const int kr = q / (ROWS / 4), rq = q % (ROWS / 4);
-        *reinterpret_cast<float4*>(&S[kr][4 * rq]) = r[i];
+        *reinterpret_cast<float4*>(S + kr * (ROWS + PAD) + 4 * rq) = v;
       }
     }
   }
+  // Fragment of K-group s (k = 8s .. 8s+7) for MFMA row `row` of the 32x32x2 layout: lane half h
+  // supplies k = 8s + 4h + e to MFMA e (e = 0..3). Both operands use the same permutation, so the
+  // four MFMAs together accumulate exactly k = 8s .. 8s+7.
+  __device__ __forceinline__ static float4 frag(const float* S, int row, int s, int h) {
+    if (KC) {
+      return *reinterpret_cast<const float4*>(S + row * BKT + 4 * ((2 * s + h) ^ ((row >> 1) & 7)));
+    } else {
+      const int k = 8 * s + 4 * h;
+      return make_float4(S[(k + 0) * (ROWS + PAD) + row], S[(k + 1) * (ROWS + PAD) + row],
+                         S[(k + 2) * (ROWS + PAD) + row], S[(k + 3) * (ROWS + PAD) + row]);
+    }
+  }
 };
+
+__device__ __forceinline__ float f4get(const float4& v, int e) {
+  return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w;
+}
 
 // KW > 1 splits every 32-deep K-tile between KW wave groups that own the same output sub-tiles
 // (in-block split-K): more waves per block for mid-size GEMMs, reduced through LDS at the end.
@@ -137,21 +158,32 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN) * KW) void gemm_f32_kern
   constexpr int WAVES_N = BN / WN;
   constexpr int NWG = (BM / WM) * (BN / WN);
   constexpr int NT = 64 * NWG * KW;
-  static_assert(BKT % (2 * KW) == 0, "K-split must divide the K tile");
+  constexpr int NGRP = BKT / 8;                 // K-groups of 8 per tile
+  static_assert(NGRP % KW == 0, "K-split must divide the K tile");
+  constexpr int GPW = NGRP / KW;                // K-groups per wave group
   using LA = TileLoader<BM, AKC, VEC, NT>;
   using LB = TileLoader<BN, BKC, VEC, NT>;
   // one LDS array: the A/B double buffers, reused by the K-split reduction after the main loop
-  constexpr int A_FL = 2 * BKT * (BM + LA::PAD), B_FL = 2 * BKT * (BN + LB::PAD);
+  constexpr int A_FL = 2 * LA::LDS_FL, B_FL = 2 * LB::LDS_FL;
   constexpr int RED_FL = (KW - 1) * BM * BN;
   constexpr int SMEM_FL = (A_FL + B_FL) > RED_FL ? (A_FL + B_FL) : RED_FL;
   __shared__ __attribute__((aligned(16))) float smem[SMEM_FL];
-  auto As = reinterpret_cast<float (*)[BKT][BM + LA::PAD]>(smem);
-  auto Bs = reinterpret_cast<float (*)[BKT][BN + LB::PAD]>(smem + A_FL);
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int kgrp = wave / NWG, wt = wave % NWG;
   const int wm = (wt / WAVES_N) * WM, wn = (wt % WAVES_N) * WN;
-  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+  // XCD-aware tile order: workgroups are dealt round-robin to the 8 XCDs, so give each XCD a
+  // contiguous run of row-major tiles (shared A row panels and B column panels in its own L2).
+  // Bijective for any tile count (q = n/8 tiles per XCD, the first n%8 XCDs take one more).
+  int n0, m0;
+  {
+    const int gx = gridDim.x, nwg = gx * gridDim.y;
+    const int orig = blockIdx.y * gx + blockIdx.x;
+    const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+    const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+    n0 = (wgid % gx) * BN;
+    m0 = (wgid / gx) * BM;
+  }
   const int b = blockIdx.z / p.splitk, split = blockIdx.z % p.splitk;
   const int kbeg = split * p.kchunk;
   const int kend = min(p.K, kbeg + p.kchunk);
@@ -166,44 +198,68 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN) * KW) void gemm_f32_kern
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  LA la;
-  LB lb;
+  // Two register sets in a ring: the global loads of tile t+2 are issued at the top of step t and
+  // written to LDS at the end of step t+1, so each load has two MFMA phases to land.
+  LA la0, la1;
+  LB lb0, lb1;
   const int ntiles = kend > kbeg ? (kend - kbeg + BKT - 1) / BKT : 0;
   if (ntiles > 0) {
-    la.load(A, p.lda, m0, p.M, kbeg, kend);
-    lb.load(B, p.ldb, n0, p.N, kbeg, kend);
-    la.store(As[0]);
-    lb.store(Bs[0]);
+    la0.load(A, p.lda, m0, p.M, kbeg, kend);
+    lb0.load(B, p.ldb, n0, p.N, kbeg, kend);
+    const int k1 = kbeg + min(1, ntiles - 1) * BKT;
+    la1.load(A, p.lda, m0, p.M, k1, kend);
+    lb1.load(B, p.ldb, n0, p.N, k1, kend);
+    la0.store(smem);
+    lb0.store(smem + A_FL);
     __syncthreads();
   }
   const int hl = lane >> 5, rl = lane & 31;
-  for (int t = 0; t < ntiles; ++t) {
+  // step t: X = the free register set (receives tile t+2), Y = the set holding tile t+1
+  auto step = [&](int t, LA& xa, LB& xb, LA& ya, LB& yb) {
     const int buf = t & 1;
-    const bool more = (t + 1) < ntiles;
-    if (more) {
-      const int k0 = kbeg + (t + 1) * BKT;
-      la.load(A, p.lda, m0, p.M, k0, kend);
-      lb.load(B, p.ldb, n0, p.N, k0, kend);
+    {  // unconditional (clamped to the last tile): a conditional issue makes hipcc's vmcnt counts
+       // assume the no-load path and wait for the just-issued loads before the LDS write below
+      const int k0 = kbeg + min(t + 2, ntiles - 1) * BKT;
+      xa.load(A, p.lda, m0, p.M, k0, kend);
+      xb.load(B, p.ldb, n0, p.N, k0, kend);
     }
+    const float* As = smem + buf * LA::LDS_FL;
+    const float* Bs = smem + A_FL + buf * LB::LDS_FL;
+    // all fragments of this wave group's K-groups first, then the MFMAs (reads overlap the MACs)
+    float4 af[GPW][TM], bf[GPW][TN];
 #pragma unroll
-    for (int kk = kgrp * (BKT / KW); kk < (kgrp + 1) * (BKT / KW); kk += 2) {
-      float av[TM], bv[TN];
+    for (int g = 0; g < GPW; ++g) {
+      const int s = kgrp * GPW + g;
 #pragma unroll
-      for (int i = 0; i < TM; ++i) av[i] = As[buf][kk + hl][wm + i * 32 + rl];
+      for (int i = 0; i < TM; ++i) af[g][i] = LA::frag(As, wm + i * 32 + rl, s, hl);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bv[j] = Bs[buf][kk + hl][wn + j * 32 + rl];
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < TN; ++j) bf[g][j] = LB::frag(Bs, wn + j * 32 + rl, s, hl);
     }
-    if (more) {
-      la.store(As[buf ^ 1]);
-      lb.store(Bs[buf ^ 1]);
-    }
+    // keep every fragment read ahead of the MFMAs: hipcc otherwise re-uses one register set and
+    // serialises read -> lgkmcnt(0) -> 4 MFMAs per K-group, exposing the LDS latency each time
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int g = 0; g < GPW; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(af[g][i], e), f4get(bf[g][j], e),
+                                                             acc[i][j], 0, 0, 0);
+    ya.store(smem + (buf ^ 1) * LA::LDS_FL);   // past the last tile this writes an unused buffer
+    yb.store(smem + A_FL + (buf ^ 1) * LB::LDS_FL);
     __syncthreads();
+  };
+  // steps in pairs with the odd step unconditional, so both paths into the loop header carry the
+  // same pending loads (a skippable odd step makes hipcc drain vmcnt(0) at the header)
+  int t = 0;
+  for (; t + 1 < ntiles; t += 2) {
+    step(t, la0, lb0, la1, lb1);
+    step(t + 1, la1, lb1, la0, lb0);
   }
+  if (t < ntiles) step(t, la0, lb0, la1, lb1);
 
   if (KW > 1) {   // fold the K-split wave groups into group 0 through LDS
     float* red = smem;
@@ -390,27 +446,35 @@ static Plan make_plan(const dasa_gemm_desc* d) {
   }
   auto tiles = [&](int bm, int bn) { return cdiv(M, bm) * cdiv(N, bn) * batch; };
   Plan pl;
-  // Tile choice (DESIGN.md "GEMM"): fill the 256 CUs with >= 1 full wave of blocks, prefer fewer,
-  // larger tiles when there are plenty, and split K inside the block (KW = 2) for mid-size shapes.
-  // Rules fitted to the MI355X sweep in profiles/r01_gemm_sweep_v2.txt (policy shapes).
+  // Tile choice (DESIGN.md "GEMM"), fitted to the MI355X (config x split-K) grid over the policy's
+  // GEMM shapes in profiles/r01/gemm_grid_v3.txt: 8-wave 64x64 tiles (in-block K split) for large and
+  // long-K problems, 32x64 tiles for mid-size ones, split-K when there are too few tiles to fill the
+  // 256 CUs; the skinny decoder GEMMs (M <= 32) are weight-streaming and split K widely.
   const long t64 = tiles(64, 64);
-  if (M <= 32) pl.cfg = 3;
+  if (M <= 32) pl.cfg = 5;
   else if (t64 >= 2048) pl.cfg = 0;
-  else if (t64 >= 500) pl.cfg = 2;
-  else if (t64 >= 250) pl.cfg = 10;
-  else if (K >= 2048) pl.cfg = 0;     // few tiles, long K: 128x128 + split-K
-  else pl.cfg = 7;
-  if (g_force_cfg >= 0 && g_force_cfg < kNumCfgs) pl.cfg = g_force_cfg;
+  else if (t64 >= 800) pl.cfg = 4;
+  else if (t64 >= 400) pl.cfg = (t64 >= 500 && K < 1536) ? 5 : 4;
+  else if (t64 >= 250 && (K < 1536 || t64 >= 320)) pl.cfg = 5;
+  else pl.cfg = 4;
+  const int fcfg = g_force_cfg >= 0 ? g_force_cfg % 64 : -1, fsplit = g_force_cfg >= 0 ? g_force_cfg / 64 : 0;
+  if (fcfg >= 0 && fcfg < kNumCfgs) pl.cfg = fcfg;
   const int bm = kCfgs[pl.cfg].bm, bn = kCfgs[pl.cfg].bn;
   const long blocks = tiles(bm, bn);
   int splitk = 1;
-  if (blocks < 160 && K >= 512) {
-    splitk = (int)cdiv(256, blocks);
-    const int maxs = K / 256;  // keep >= 8 K-tiles per split
-    if (splitk > maxs) splitk = maxs;
-    if (splitk > 16) splitk = 16;
-    if (splitk < 1) splitk = 1;
+  if (M <= 32) {
+    if (blocks < 160 && K >= 512) {
+      splitk = (int)cdiv(256, blocks);
+      const int maxs = K / 256;  // keep >= 8 K-tiles per split
+      if (splitk > maxs) splitk = maxs;
+      if (splitk > 16) splitk = 16;
+      if (splitk < 1) splitk = 1;
+    }
+  } else if (blocks < 400 && K >= 1536) {
+    splitk = (int)((K + 384) / 768);
+    if (splitk > 4) splitk = 4;
   }
+  if (fsplit > 0) splitk = fsplit;
   int kchunk = (int)(cdiv(cdiv(K, splitk), BKT) * BKT);
   if (kchunk < BKT) kchunk = BKT;
   splitk = K > 0 ? (int)cdiv(K, kchunk) : 1;

@@ -17,7 +17,7 @@ def check(rc, what, family=None, flops=0.0, nbytes=0.0, _ev=None):
     _lib.check(rc, what)
 
 
-def _call(what, family, fn, *a, flops=0.0, nbytes=0.0):
+def _call(what, family, fn, *a, flops=0.0, nbytes=0.0, detail=None):
     """Launch through the C-ABI; under prof.collect() bracket it with HIP events on the stream."""
     if prof.active():
         e0 = torch.cuda.Event(enable_timing=True)
@@ -25,7 +25,7 @@ def _call(what, family, fn, *a, flops=0.0, nbytes=0.0):
         e0.record()
         rc = fn(*a)
         e1.record()
-        prof.record(family, e0, e1, flops, nbytes)
+        prof.record(family, e0, e1, flops, nbytes, detail)
     else:
         rc = fn(*a)
     _lib.check(rc, what)
@@ -92,7 +92,8 @@ def gemm(A, B, C, *, M, N, K, opA=0, opB=1, lda, ldb, ldc, bias=None, act=None, 
         ws = torch.empty(need // 4 + 1, dtype=torch.float32, device=C.device)
     b = max(1, int(batch))
     _call("dasa_gemm_f32", "gemm", L.dasa_gemm_f32, ctypes.byref(d), _p(ws), int(need), _stream(),
-          flops=2.0 * M * N * K * b, nbytes=4.0 * b * (M * K + K * N + M * N))
+          flops=2.0 * M * N * K * b, nbytes=4.0 * b * (M * K + K * N + M * N),
+          detail=(int(M), int(N), int(K), b, int(opA), int(opB)))
 
 
 def linear(x, W, b=None, act=None, out=None, aux=None, colscale=None, beta=0.0, alpha=1.0):

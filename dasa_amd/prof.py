@@ -28,14 +28,21 @@ FAMILIES = {
 
 
 class _Recorder:
-    def __init__(self):
+    def __init__(self, want_shapes=0):
         self.items = []
+        self.want_shapes = want_shapes
 
     def summary(self, peak_tf=157.3, peak_gbs=8000.0):
         torch.cuda.synchronize()
         fam = defaultdict(lambda: {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0})
-        for name, e0, e1, flops, nbytes in self.items:
+        shapes = defaultdict(lambda: [0, 0.0, 0.0])
+        for name, e0, e1, flops, nbytes, detail in self.items:
             f = fam[name]
+            if detail is not None:
+                sh = shapes[(name,) + tuple(detail)]
+                sh[0] += 1
+                sh[1] += e0.elapsed_time(e1)
+                sh[2] += flops
             f["launches"] += 1
             f["ms"] += e0.elapsed_time(e1)
             f["flops"] += flops
@@ -62,21 +69,28 @@ class _Recorder:
                                "alg_" + ("flops" if d["bound"] == "mfma" else "bytes"):
                                    (fam[dom_name]["flops"] if d["bound"] == "mfma" else fam[dom_name]["bytes"])
                                    / fam[dom_name]["launches"]}}
-        return {"roofline": roof, "kernels": kernels, "profiled_device_ms": round(total, 2)}
+        out = {"roofline": roof, "kernels": kernels, "profiled_device_ms": round(total, 2)}
+        if self.want_shapes:
+            top = sorted(shapes.items(), key=lambda kv: -kv[1][1])[:self.want_shapes]
+            out["shapes"] = [{"kernel": k[0], "shape": list(k[1:]), "launches": v[0], "ms": round(v[1], 3),
+                              "TFLOPs": round(v[2] / (v[1] / 1e3) / 1e12, 1) if v[1] > 0 else 0.0}
+                             for k, v in top]
+        return out
 
 
 def active():
     return _REC is not None
 
 
-def record(name, e0, e1, flops, nbytes):
-    _REC.items.append((name, e0, e1, float(flops), float(nbytes)))
+def record(name, e0, e1, flops, nbytes, detail=None):
+    _REC.items.append((name, e0, e1, float(flops), float(nbytes), detail))
 
 
 @contextlib.contextmanager
-def collect():
+def collect(shapes=0):
+    """shapes > 0 adds the `shapes` table: the top-N (kernel, shape) pairs by device time."""
     global _REC
-    rec = _Recorder()
+    rec = _Recorder(shapes)
     _REC = rec
     try:
         yield rec

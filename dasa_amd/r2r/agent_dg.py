@@ -371,7 +371,7 @@ class Seq2SeqAgent(BaseAgent):
         consistent_drop = args.consistent_drop or (speaker is not None)
         if args.decoder_consistent_drop:
             self.decoder.init_noise((seq.shape[0], args.d_enc_hidden_size))
-        self.encoder.cache_language(not self.encoder.training)
+        self.encoder.cache_language(not self.encoder.training, steps=self.episode_len)
         angle = args.angle_feat_size
         h_t = c_t = h1 = ctx = None
         for t in range(self.episode_len):

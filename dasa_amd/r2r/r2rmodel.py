@@ -6,6 +6,8 @@ kernel per timestep) -> decoder init projections. `cache_language(True)` lets ca
 steps on the same instruction batch (eval rollouts) compute the 9 language layers once — exact, since
 that stack is input-independent of the panorama and detached (vilmodel.py:1377-1378).
 """
+import os
+
 import torch
 import torch.nn as nn
 
@@ -71,22 +73,46 @@ class DicEncoder(nn.Module):
             self.ctx_v_to_v = nn.Linear(self.transformer_hidden_size, 2048 + args.angle_feat_size)
         self._lang_cache_on = False
         self._lang_cache = None
+        # train-mode language prefetch: steps of the current rollout not yet computed, and computed ones
+        self.lang_chunk = int(os.environ.get("DASA_LANG_CHUNK", "8"))
+        self._lang_budget = 0
+        self._lang_queue = []
 
     # ------------------------------------------------------------------ language-stack cache
-    def cache_language(self, on=True):
+    def cache_language(self, on=True, steps=0):
+        """Called by the agent at the start of every rollout (so nothing survives into the next batch).
+        on: eval-mode cache (the stack is deterministic and detached: computed once per rollout).
+        steps: train-mode prefetch budget. With dropout active the stack differs every step, but it
+        never sees the panorama, so the next `lang_chunk` steps' stacks (each with its own dropout
+        draw, as the reference's per-step calls) are computed in one batched pass of lang_chunk x B
+        sequences and handed out one per encoder call."""
         self._lang_cache_on = on
         self._lang_cache = None
+        self._lang_budget = int(steps)
+        self._lang_queue = []
 
     def _language(self, ids, att_mask):
         bert = self.bert
         trainable = bert.update_lang_bert and torch.is_grad_enabled()
-        if self._lang_cache_on and not trainable and not bert.training:
+        if trainable:
+            return None
+        if self._lang_cache_on and not bert.training:
             key = (ids.data_ptr(), tuple(ids.shape), ids._version, att_mask.data_ptr())
             if self._lang_cache is None or self._lang_cache[0] != key:
                 ext = ((1.0 - att_mask.float()) * -10000.0).unsqueeze(1).unsqueeze(2)
                 with torch.no_grad():
                     self._lang_cache = (key, bert.language(ids, ext))
             return self._lang_cache[1]
+        if bert.training and self.lang_chunk > 1 and (self._lang_queue or self._lang_budget > 0):
+            if not self._lang_queue:
+                S = min(self.lang_chunk, self._lang_budget)
+                self._lang_budget -= S
+                B, L = ids.shape
+                ext = ((1.0 - att_mask.float()) * -10000.0).unsqueeze(1).unsqueeze(2)
+                with torch.no_grad():
+                    x = bert.language(ids.repeat(S, 1), ext.repeat(S, 1, 1, 1))
+                self._lang_queue = list(x.view(S, B, L, x.shape[-1]).unbind(0))
+            return self._lang_queue.pop(0)
         return None
 
     # ------------------------------------------------------------------ forward

@@ -52,7 +52,8 @@ typedef struct dasa_gemm_desc {
 /* Workspace for split-K partials (skinny-M decoder GEMMs): bytes needed for this descriptor.
  * Passing ws == NULL (or too small) runs the GEMM without split-K instead. */
 int64_t dasa_gemm_f32_workspace(const dasa_gemm_desc* d);
-/* Tuning hook: pin tile configuration `cfg` for subsequent calls (-1 = automatic choice).
+/* Tuning hook: pin tile configuration `cfg % 64` (and, when cfg >= 64, split-K = cfg / 64) for
+ * subsequent calls (-1 = automatic choice).
  * Returns the number of configurations. Host-only; not thread-safe with concurrent GEMM planning. */
 int dasa_gemm_force_config(int cfg);
 int dasa_gemm_f32(const dasa_gemm_desc* d, void* ws, int64_t ws_bytes, void* stream);

@@ -69,14 +69,15 @@ def test_softdot(R, dev):
     close(ht.detach().cpu(), G["softdot/h_tilde"], 1e-5, "h_tilde")
     close(alpha.cpu(), G["softdot/alpha"], 1e-6, "alpha")
     (ht * g1.to(dev)).sum().backward()
-    close(h1.grad.cpu(), G["softdot/dh"], 1e-4, "dh")
+    # input gradients are sums over K = 2048..3200 products with |dh| up to ~40: bound relative to scale
+    close(h1.grad.cpu(), G["softdot/dh"], max(1e-4, 1e-5 * np.abs(G["softdot/dh"]).max()), "dh")
     assert check_grads(G, "softdot/", [(k, p.grad) for k, p in att.named_parameters()], rtol=1e-3) == 2
     catt = init_params(model.SoftDotAttention(1024, 2176), 31).to(dev)
     h2, cd = _req(h, dev), _req(cand, dev)
     _, logit = catt(h2, cd, output_prob=False, output_tilde=False)
     close(logit.detach().cpu(), G["cand/logit"], TOL, "cand logit")
     (logit * g2.to(dev)).sum().backward()
-    close(h2.grad.cpu(), G["cand/dh"], 1e-4, "cand dh")
+    close(h2.grad.cpu(), G["cand/dh"], max(1e-4, 1e-5 * np.abs(G["cand/dh"]).max()), "cand dh")
     check_grads(G, "cand/", [("cand", cd.grad), ("linear_in.weight", catt.linear_in.weight.grad)], rtol=1e-3)
 
 

@@ -55,9 +55,52 @@ def sweep():
         print(f"{name:<18}" + "".join(f"{x:>7.1f}" for x in row), flush=True)
 
 
+def make_fn(M, N, K, opA, opB, dev):
+    """dasa and torch closures for C[M,N] = opA(A) opB(B) in the descriptor's layouts."""
+    A = torch.randn(K, M, device=dev) if opA else torch.randn(M, K, device=dev)
+    B = torch.randn(N, K, device=dev) if opB else torch.randn(K, N, device=dev)
+    C = torch.empty(M, N, device=dev)
+    f1 = lambda: ops.gemm(A, B, C, M=M, N=N, K=K, opA=opA, opB=opB, lda=A.shape[1], ldb=B.shape[1], ldc=N)
+    At = A.t() if opA else A
+    Bt = B.t() if opB else B
+    f2 = lambda: torch.mm(At, Bt, out=C)
+    return f1, f2
+
+
+def grid(shapes):
+    """Every (tile config, split-K) pair on each shape: best five, the automatic plan and torch."""
+    from dasa_amd import _lib
+    L = _lib.lib()
+    n = L.dasa_gemm_force_config(-1)
+    dev = torch.device("cuda")
+    for M, N, K, opA, opB in shapes:
+        f1, f2 = make_fn(M, N, K, opA, opB, dev)
+        fl = 2.0 * M * N * K
+        res = []
+        for c in range(n):
+            for sk in (1, 2, 3, 4, 6, 8, 12):
+                if K // sk < 128:
+                    continue
+                L.dasa_gemm_force_config(c + 64 * sk)
+                res.append((fl / bench(f1, 10) / 1e9, c, sk))
+        L.dasa_gemm_force_config(-1)
+        auto = fl / bench(f1) / 1e9
+        tor = fl / bench(f2) / 1e9
+        res.sort(reverse=True)
+        best = " ".join(f"c{c}s{sk}:{tf:.0f}" for tf, c, sk in res[:5])
+        print(f"M{M} N{N} K{K} op{opA}{opB}  auto {auto:.1f}  torch {tor:.1f}  best {best}", flush=True)
+
+
 def main():
     if "--sweep" in sys.argv:
         return sweep()
+    if "--grid" in sys.argv:
+        import json
+        path = sys.argv[sys.argv.index("--grid") + 1]
+        rows = json.load(open(path))
+        if isinstance(rows, dict):
+            rows = rows["shapes"]
+        return grid([tuple(r["shape"][:3]) + tuple(r["shape"][4:6]) for r in rows])
     dev = torch.device("cuda")
     torch.backends.cuda.matmul.allow_tf32 = False
     print(f"{'shape':<18}{'M':>6}{'N':>6}{'K':>6}{'dasa us':>10}{'TF':>8}{'torch us':>10}{'TF':>8}")
