@@ -257,6 +257,10 @@ class Seq2SeqAgent(BaseAgent):
         return input_a_t, f_t, d_t, cf, cd, leng
 
     def _teacher_action(self, obs, ended):
+        return self._to_dev(self._teacher_action_np(obs, ended))
+
+    def _teacher_action_np(self, obs, ended):
+        """agent_dg.py:325-344 on the host (the device copy is made without a sync)."""
         a = np.zeros(len(obs), dtype=np.int64)
         for i, ob in enumerate(obs):
             if ended[i]:
@@ -269,7 +273,7 @@ class Seq2SeqAgent(BaseAgent):
                 else:
                     assert ob["teacher"] == ob["viewpoint"]
                     a[i] = len(ob["candidate"])
-        return torch.from_numpy(a).to(self.device)
+        return a
 
     def _back_teacher_action(self, obs, ended):
         a = np.zeros(len(obs), dtype=np.int64)
@@ -376,6 +380,11 @@ class Seq2SeqAgent(BaseAgent):
         h_t = c_t = h1 = ctx = None
         for t in range(self.episode_len):
             input_a_t, f_t, d_t, candidate_feat, candidate_dfeat, candidate_leng = self.get_input_feat(perm_obs)
+            # host-side inputs of the step's loss/action stage, copied up front without a sync (the
+            # reference builds them after the decoder with blocking copies; same values)
+            target_np = self._teacher_action_np(perm_obs, ended)
+            target = self._to_dev(target_np)
+            candidate_mask = utils.length2mask(candidate_leng, device=self.device)
             stage = args.env_drop_stage
             use_noise = consistent_drop and noise is not None
             all_img_feats = f_t                  # the raw panorama (agent_dg.py:730)
@@ -422,7 +431,6 @@ class Seq2SeqAgent(BaseAgent):
                 h_t, c_t, logit, h1, aux_outputs = self.decoder(input_a_t, df_t, candidate_feat, h_t, h1, c_t, ctx,
                                                                 ctx_mask, already_dropfeat=consistent_drop)
             hidden_states.append(h_t)
-            candidate_mask = utils.length2mask(candidate_leng, device=self.device)
             if args.submit:
                 cm = candidate_mask.cpu()
                 for ob_id, ob in enumerate(perm_obs):
@@ -432,7 +440,6 @@ class Seq2SeqAgent(BaseAgent):
                             cm[ob_id][c_id] = 1
                 candidate_mask = cm.to(self.device)
             logit = logit.masked_fill(candidate_mask, -float("inf"))
-            target = self._teacher_action(perm_obs, ended)
             forth_loss = self.criterion(logit, target)
             total_forth_loss += forth_loss
             if args.pred_back:
@@ -446,7 +453,7 @@ class Seq2SeqAgent(BaseAgent):
                 policy_log_probs.append(F.log_softmax(logit, 1).gather(1, a_t.unsqueeze(1)))
             elif self.feedback == "sample":
                 probs = F.softmax(logit, 1)
-                c = torch.distributions.Categorical(probs)
+                c = torch.distributions.Categorical(probs, validate_args=False)   # (validation = a host sync)
                 ent = c.entropy()
                 deferred["entropy"].append(ent.sum().detach())
                 entropys.append(ent)
@@ -454,7 +461,10 @@ class Seq2SeqAgent(BaseAgent):
                 policy_log_probs.append(c.log_prob(a_t))
             else:
                 sys.exit("Invalid feedback option")
-            cpu_a_t = a_t.cpu().numpy().copy()      # the step's one device->host sync
+            if self.feedback == "teacher":
+                cpu_a_t = target_np.copy()           # a_t is target: its host copy, no device round trip
+            else:
+                cpu_a_t = a_t.cpu().numpy().copy()  # the step's one device->host sync
             for i, next_id in enumerate(cpu_a_t):
                 if next_id == (candidate_leng[i] - 1) or next_id == args.ignoreid:
                     cpu_a_t[i] = -1
@@ -490,6 +500,11 @@ class Seq2SeqAgent(BaseAgent):
 
         if train_rl:
             input_a_t, f_t, d_t, candidate_feat, candidate_dfeat, candidate_leng = self.get_input_feat(perm_obs)
+            # host-side inputs of the step's loss/action stage, copied up front without a sync (the
+            # reference builds them after the decoder with blocking copies; same values)
+            target_np = self._teacher_action_np(perm_obs, ended)
+            target = self._to_dev(target_np)
+            candidate_mask = utils.length2mask(candidate_leng, device=self.device)
             if speaker is not None:
                 candidate_feat = self._noise_mult(candidate_feat, noise)
                 f_t = self._noise_mult(f_t, noise)

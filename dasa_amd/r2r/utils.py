@@ -21,4 +21,5 @@ def length2mask(length, size=None, device=None):
     size = int(max(length)) if size is None else size
     lens = torch.as_tensor(list(length), dtype=torch.int64)
     mask = torch.arange(size, dtype=torch.int64).unsqueeze(0) > (lens - 1).unsqueeze(1)
-    return mask.to(device if device is not None else torch.device("cuda"))
+    # pinned + non_blocking: the copy is queued on the stream instead of syncing the host with it
+    return mask.pin_memory().to(device if device is not None else torch.device("cuda"), non_blocking=True)

@@ -188,7 +188,15 @@ class _Loc:
 
 
 class _State:
-    pass
+    """MatterSim SimState snapshot; navigableLocations is built on first access (the agent polls
+    getState().viewIndex while turning, which never needs it)."""
+    __slots__ = ("scanId", "location", "viewIndex", "heading", "elevation", "step", "_nav", "_world", "_navlist")
+
+    @property
+    def navigableLocations(self):
+        if self._navlist is None:
+            self._navlist = [_Loc(self._world.ids[u]) for u in self._nav]
+        return self._navlist
 
 
 class SynthSim:
@@ -254,7 +262,9 @@ class SynthSim:
         s.heading = self.heading
         s.elevation = self.elevation
         s.step = self.step
-        s.navigableLocations = [_Loc(self.world.ids[u]) for u in self.navigable()]
+        s._nav = self.navigable()
+        s._world = self.world
+        s._navlist = None
         return s
 
 
