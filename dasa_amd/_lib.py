@@ -59,6 +59,7 @@ SIGNATURES = {
     "dasa_bilstm_fwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp]),
     "dasa_bilstm_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp]),
     "dasa_bilstm_hprev": (i32, [vp, vp, i32, i32, i32, vp]),
+    "dasa_bilstm_set_mode": (i32, [i32]),
     "dasa_bilstm_bwd_workspace": (i64, [i32, i32]),
     "dasa_adain_musigma_fwd": (i32, [vp, i64, vp, i64, vp, i64, vp, i32, i32, f32, vp]),
     "dasa_reverse_valid": (i32, [vp, vp, vp, i32, i32, i32, vp]),

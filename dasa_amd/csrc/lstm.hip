@@ -10,6 +10,8 @@
 // Packed-sequence semantics: a row is active at time t iff t < len[b]; inactive steps freeze the
 // forward state, keep the backward state at zero, and emit zero outputs (pad_packed_sequence).
 #include "common.h"
+#include <cstdlib>
+#include "lstm_internal.h"
 #include "../../include/dasa_hip.h"
 
 namespace {
@@ -328,6 +330,22 @@ extern "C" int dasa_lstm_cell_bwd(const float* act_save, const float* c_prev, co
   return 0;
 }
 
+// 0 = automatic (persistent recurrence when eligible, else step kernels), 1 = step kernels only,
+// 2 = persistent only (error when not eligible). DASA_LSTM_MODE sets the initial value.
+static int g_lstm_mode = -1;
+static int lstm_mode() {
+  if (g_lstm_mode < 0) {
+    const char* e = getenv("DASA_LSTM_MODE");
+    g_lstm_mode = e ? atoi(e) : 0;
+  }
+  return g_lstm_mode;
+}
+extern "C" int dasa_bilstm_set_mode(int mode) {
+  if (mode < 0 || mode > 2) return (int)hipErrorInvalidValue;
+  g_lstm_mode = mode;
+  return 0;
+}
+
 extern "C" int64_t dasa_bilstm_workspace(int32_t B, int32_t H) {
   const long base = 6L * B * H;
   return (int64_t)((B <= 32 ? base : base + 8L * B * H) * sizeof(float));
@@ -348,6 +366,15 @@ extern "C" int dasa_bilstm_fwd(const float* xproj, const float* whh_fwd, const f
   float* rec = ws + 3 * S;
   hipLaunchKernelGGL(fill_kernel, dim3(cdivi(3 * S, 256)), dim3(256), 0, st, ws, 3 * S, 0.f);
   DASA_CHECK_LAUNCH();
+  const int mode = lstm_mode();
+  if (mode != 1 && bilstm_persist_ok(B, H)) {
+    // ws: [0, 2S) = the [parity][dir][B][H] state hand-off, ws + 2S = zeroed barrier words
+    const int rc = bilstm_persist_fwd(xproj, whh_fwd, whh_bwd, lengths, out, h_n, c_n, save_act, save_c, B, L, H,
+                                      ws, reinterpret_cast<unsigned*>(ws + 2 * S), st);
+    if (rc == 0 || mode == 2) return rc;
+  } else if (mode == 2) {
+    return (int)hipErrorInvalidValue;
+  }
   SeqArgs a{xproj, whh_fwd, whh_bwd, lengths, out, h0, h1, c, save_act, save_c, nullptr, B, L, H};
   for (int s = 0; s < L; ++s) {
     a.hin = (s & 1) ? h1 : h0;
@@ -396,6 +423,16 @@ extern "C" int dasa_bilstm_bwd(const float* whh_fwd, const float* whh_bwd, const
     return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   const long S = 2L * B * H;
+  const int mode = lstm_mode();
+  if (mode != 1 && bilstm_persist_ok(B, H)) {
+    hipLaunchKernelGGL(fill_kernel, dim3(1), dim3(64), 0, st, ws, 16L, 0.f);   // barrier words
+    DASA_CHECK_LAUNCH();
+    const int rc = bilstm_persist_bwd(whh_fwd, whh_bwd, lengths, save_act, save_c, dout, dh_n, dc_n, dgates, B, L,
+                                      H, reinterpret_cast<unsigned*>(ws), st);
+    if (rc == 0 || mode == 2) return rc;
+  } else if (mode == 2) {
+    return (int)hipErrorInvalidValue;
+  }
   float* dh = ws;
   float* dc = ws + S;
   float* wt0 = ws + 2 * S;

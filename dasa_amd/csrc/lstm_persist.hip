@@ -1,0 +1,320 @@
+// Persistent (one launch per sequence) bi-LSTM recurrence for the DicEncoder top LSTM
+// (r2rmodel.py:2239-2243, 2339-2354), forward and BPTT.
+//
+// Why: the per-timestep kernels in lstm.hip re-read W_hh (2 x 16 MB fp32) from MALL every step, so a
+// step costs ~15 us (fwd) / ~21 us (BPTT) at B = 20. Here each of the 256 workgroups (one per CU, 128
+// per direction) keeps its 8-unit slice of W_hh (128 KB) in VGPRs for the whole sequence; a step is
+// one MFMA pass over the recurrent state + the cell update, and the directions' workgroups exchange
+// the new state through a per-direction counter barrier inside the launch.
+//
+// Hand-off protocol (cdna_hip_programming.md Guideline 16; MI355X_MICROARCH.md "Valid forms", row 1):
+// every handed-off word is stored sc1 (write-through), every storing wave drains vmcnt, the workgroup
+// barriers, ONE lane adds to the direction's arrival counter (agent-scope atomic), then polls it with
+// sc1 loads (bounded by a wall-clock limit that sets a timeout word instead of hanging); the other
+// waves join at a workgroup barrier and read the state with sc1 loads only.
+// Residency: one 1024-thread workgroup per CU, 2*H/8 <= 256 workgroups, launched cooperatively so
+// the runtime rejects a grid that could not be co-resident (the caller then uses the step kernels).
+#include "common.h"
+#include "lstm_internal.h"
+
+namespace {
+
+constexpr int PU = 8;                       // hidden units per workgroup
+constexpr int PW = 16;                      // waves per workgroup
+constexpr long long kSpinTicks = 20000000;  // 200 ms of the 100 MHz wall clock per barrier wait
+
+__device__ __forceinline__ float4 selz(bool c, float4 v) {
+  return make_float4(c ? v.x : 0.f, c ? v.y : 0.f, c ? v.z : 0.f, c ? v.w : 0.f);
+}
+__device__ __forceinline__ float f4e(const float4& v, int e) {
+  return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w;
+}
+__device__ __forceinline__ float4 ld_sc1(__amdgpu_buffer_rsrc_t rs, int byte_off) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 16 /* sc1 */));
+}
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // global_store_dword ... sc1
+}
+
+// Arrive + wait on the direction's monotonic counter. Returns false (after setting *tmo) if the
+// other workgroups did not arrive within kSpinTicks; every thread of the workgroup gets the answer.
+__device__ bool dir_barrier(unsigned* cnt, unsigned target, unsigned* tmo, float* flag_lds) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave drains its sc1 stores
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const long long t0 = wall_clock64();
+    float ok = 1.f;
+    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (wall_clock64() - t0 > kSpinTicks) {
+        __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0.f;
+        break;
+      }
+    }
+    *flag_lds = ok;
+  }
+  __syncthreads();
+  return *flag_lds != 0.f;
+}
+
+// ------------------------------------------------------------------------------------- forward
+struct PFwd {
+  const float* xproj;     // [B][L][2][4H]
+  const float* whh0;      // [4H][H]
+  const float* whh1;
+  const int* len;         // [B]
+  float* out;             // [B][L][2H]
+  float* save_act;        // [L][2][B][4H] or NULL
+  float* save_c;          // [L][2][B][H] or NULL
+  float* h_n;             // [2][B][H] or NULL
+  float* c_n;
+  float* hbuf;            // [2 parity][2 dir][B][H] hand-off
+  unsigned* sync;         // [0], [1] arrivals per direction; [2] timeout word (zeroed by the caller)
+  int B, L, H;
+};
+
+// NG = H / 128: K-groups of 8 per wave (the wave's K slice is H / 16).
+template <int NG>
+__global__ __launch_bounds__(1024) void bilstm_persist_fwd_kernel(PFwd a) {
+  __shared__ __attribute__((aligned(16))) float smem[PW * 1024 + 4];
+  const int H = a.H, B = a.B, L = a.L, G = H / PU;
+  const int dir = blockIdx.x / G, u0 = (blockIdx.x % G) * PU;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int n = lane & 31, hh = lane >> 5;
+  const int k0 = w * (8 * NG);
+  // This workgroup's 32 W_hh rows (gate q = n / 8 of unit u0 + n % 8), this wave's K slice, in the
+  // 32x32x2 B-operand layout with the K-permuted float4 per lane (k = 8g + 4hh + e feeds MFMA e).
+  const float* wp = (dir ? a.whh1 : a.whh0) + ((long)(n / PU) * H + u0 + (n % PU)) * H + k0 + 4 * hh;
+  float4 wf[NG];
+#pragma unroll
+  for (int g = 0; g < NG; ++g) wf[g] = *reinterpret_cast<const float4*>(wp + 8 * g);
+
+  const bool owner = threadIdx.x < B * PU;
+  const int ob = threadIdx.x / PU, ou = threadIdx.x % PU, uj = u0 + ou;
+  const int lenb = owner ? a.len[ob] : 0;
+  float c = 0.f, hp = 0.f;
+  const int b = lane & 31, bc = min(b, B - 1);
+  const bool bval = b < B;
+  for (int s = 0; s < L; ++s) {
+    const int t = dir == 0 ? s : L - 1 - s;
+    floatx16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    if (s > 0) {   // h_0 = 0: the first step has no recurrent term
+      const float* hin = a.hbuf + (long)((s & 1) * 2 + dir) * B * H;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)hin, (short)0, B * H * 4, 0x00020000);
+      float4 hf[NG];
+#pragma unroll
+      for (int g = 0; g < NG; ++g) hf[g] = selz(bval, ld_sc1(rs, (bc * H + k0 + 8 * g + 4 * hh) * 4));
+#pragma unroll
+      for (int g = 0; g < NG; ++g)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(f4e(hf[g], e), f4e(wf[g], e), acc, 0, 0, 0);
+    }
+    // C[b][n] partial over this wave's K slice: lane -> col n, reg r -> row (r&3) + 8(r>>2) + 4hh
+#pragma unroll
+    for (int r = 0; r < 16; ++r) smem[w * 1024 + r * 64 + lane] = acc[r];
+    __syncthreads();
+    {   // sum the 16 wave partials: thread i owns element i of the 32x32 tile
+      float sum = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < PW; ++ww) sum += smem[ww * 1024 + threadIdx.x];
+      smem[threadIdx.x] = sum;   // only this thread reads or writes index threadIdx.x of slot 0
+    }
+    __syncthreads();
+    if (owner) {
+      const int rr = (ob & 3) + 4 * (ob >> 3), lh = ((ob >> 2) & 1) * 32;
+      const float* xp = a.xproj + (((long)ob * L + t) * 2 + dir) * 4 * H;
+      float gq[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) gq[q] = xp[q * H + uj] + smem[rr * 64 + lh + q * PU + ou];
+      float* outp = a.out + ((long)ob * L + t) * 2 * H + dir * H + uj;
+      float* sa = a.save_act ? a.save_act + (((long)t * 2 + dir) * B + ob) * 4 * H : nullptr;
+      if (t < lenb) {
+        const float i = sigmoidf_(gq[0]), f = sigmoidf_(gq[1]), gg = tanhf(gq[2]), o = sigmoidf_(gq[3]);
+        c = f * c + i * gg;
+        hp = o * tanhf(c);
+        *outp = hp;
+        if (sa) { sa[uj] = i; sa[H + uj] = f; sa[2 * H + uj] = gg; sa[3 * H + uj] = o; }
+      } else {   // packed sequence: state frozen (fwd) / still zero (bwd), output zero
+        *outp = 0.f;
+        if (sa) { sa[uj] = 0.f; sa[H + uj] = 0.f; sa[2 * H + uj] = 0.f; sa[3 * H + uj] = 0.f; }
+      }
+      if (a.save_c) a.save_c[(((long)t * 2 + dir) * B + ob) * H + uj] = c;
+      if (s + 1 < L) st_sc1(a.hbuf + (long)(((s + 1) & 1) * 2 + dir) * B * H + (long)ob * H + uj, hp);
+    }
+    if (s + 1 < L && !dir_barrier(&a.sync[dir], (unsigned)(s + 1) * G, &a.sync[2], &smem[PW * 1024])) break;
+  }
+  if (owner) {
+    const long si = ((long)dir * B + ob) * H + uj;
+    if (a.h_n) a.h_n[si] = hp;
+    if (a.c_n) a.c_n[si] = c;
+  }
+}
+
+// ------------------------------------------------------------------------------------- BPTT
+struct PBwd {
+  const float* whh0;      // [4H][H]
+  const float* whh1;
+  const int* len;
+  const float* save_act;  // [L][2][B][4H]
+  const float* save_c;    // [L][2][B][H]
+  const float* dout;      // [B][L][2H]
+  const float* dh_n;      // [2][B][H] or NULL
+  const float* dc_n;
+  float* dgates;          // [B][L][2][4H]: output and the step-to-step hand-off (stored sc1)
+  unsigned* sync;
+  int B, L, H;
+};
+
+// rec[b][j] = sum_n dgates_prev[b][n] W_hh[n][j] with v_mfma_f32_16x16x4_f32: rows b (two 16-row
+// tiles), cols j (the workgroup's 8 units, padded to 16), K = 4H split over the 16 waves (4H/16 each,
+// NGB = 4H/256 K-groups of 16). W_hh[:, j-slice] lives in VGPRs in the K-permuted B-operand layout.
+template <int NGB>
+__global__ __launch_bounds__(1024) void bilstm_persist_bwd_kernel(PBwd a) {
+  __shared__ __attribute__((aligned(16))) float smem[PW * 512 + 4];
+  const int H = a.H, B = a.B, L = a.L, G = H / PU, G4 = 4 * H;
+  const int dir = blockIdx.x / G, j0 = (blockIdx.x % G) * PU;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c16 = lane & 15, kq = lane >> 4;
+  const int k0 = w * (16 * NGB);
+  float4 wf[NGB];
+  {
+    const float* W = dir ? a.whh1 : a.whh0;
+    const bool cv = c16 < PU;
+    const int jj = j0 + (cv ? c16 : 0);
+#pragma unroll
+    for (int g = 0; g < NGB; ++g) {
+      const int nb = k0 + 16 * g + 4 * kq;
+      const float4 v = make_float4(W[(long)(nb + 0) * H + jj], W[(long)(nb + 1) * H + jj],
+                                   W[(long)(nb + 2) * H + jj], W[(long)(nb + 3) * H + jj]);
+      wf[g] = selz(cv, v);
+    }
+  }
+  const bool owner = threadIdx.x < B * PU;
+  const int ob = threadIdx.x / PU, oj = threadIdx.x % PU, j = j0 + oj;
+  const int lenb = owner ? a.len[ob] : 0;
+  float dh = 0.f, dc = 0.f;
+  if (owner) {
+    const long si = ((long)dir * B + ob) * H + j;
+    if (a.dh_n) dh = a.dh_n[si];
+    if (a.dc_n) dc = a.dc_n[si];
+  }
+  const int r16 = lane & 15;
+  const int b0 = min(r16, B - 1), b1 = min(16 + r16, B - 1);
+  const bool v0 = r16 < B, v1 = 16 + r16 < B;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.dgates, (short)0, B * L * 2 * G4 * 4, 0x00020000);
+  for (int s = 0; s < L; ++s) {
+    const int t = dir == 0 ? (L - 1 - s) : s;
+    floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    if (s > 0) {
+      const int tp = dir == 0 ? t + 1 : t - 1;   // the step processed just before (BPTT order)
+      const int base0 = (((b0 * L + tp) * 2 + dir) * G4 + k0 + 4 * kq) * 4;
+      const int base1 = (((b1 * L + tp) * 2 + dir) * G4 + k0 + 4 * kq) * 4;
+#pragma unroll
+      for (int g0 = 0; g0 < NGB; g0 += 4) {
+        float4 x0[4], x1[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          x0[g] = selz(v0, ld_sc1(rs, base0 + 64 * (g0 + g)));
+          x1[g] = selz(v1, ld_sc1(rs, base1 + 64 * (g0 + g)));
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(f4e(x0[g], e), f4e(wf[g0 + g], e), acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(f4e(x1[g], e), f4e(wf[g0 + g], e), acc1, 0, 0, 0);
+          }
+      }
+    }
+    // 16x16 C map: col = lane & 15 (unit), row = 4 * (lane >> 4) + reg (batch within the tile)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      smem[w * 512 + r * 64 + lane] = acc0[r];
+      smem[w * 512 + 256 + r * 64 + lane] = acc1[r];
+    }
+    __syncthreads();
+    if (threadIdx.x < 512) {
+      float sum = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < PW; ++ww) sum += smem[ww * 512 + threadIdx.x];
+      smem[PW * 512 - 512 + threadIdx.x] = sum;   // the last wave's slot: read by nobody else now
+    }
+    __syncthreads();
+    if (owner) {
+      const int tile = ob >> 4, br = ob & 15;
+      const float rec = smem[PW * 512 - 512 + tile * 256 + (br & 3) * 64 + (br >> 2) * 16 + oj];
+      float* dg = a.dgates + (((long)ob * L + t) * 2 + dir) * G4;
+      if (t < lenb) {
+        const float G = rec + a.dout[((long)ob * L + t) * 2 * H + dir * H + j] + dh;
+        const float* sa = a.save_act + (((long)t * 2 + dir) * B + ob) * G4;
+        const float i_ = sa[j], f_ = sa[H + j], g_ = sa[2 * H + j], o_ = sa[3 * H + j];
+        const float ct = a.save_c[(((long)t * 2 + dir) * B + ob) * H + j];
+        const int tq = dir == 0 ? t - 1 : t + 1;   // previous step in forward order
+        const float cp = (tq >= 0 && tq < L) ? a.save_c[(((long)tq * 2 + dir) * B + ob) * H + j] : 0.f;
+        const float tc = tanhf(ct);
+        const float dcv = dc + G * o_ * (1.f - tc * tc);
+        st_sc1(dg + j, dcv * g_ * i_ * (1.f - i_));
+        st_sc1(dg + H + j, dcv * cp * f_ * (1.f - f_));
+        st_sc1(dg + 2 * H + j, dcv * i_ * (1.f - g_ * g_));
+        st_sc1(dg + 3 * H + j, G * tc * o_ * (1.f - o_));
+        dc = dcv * f_;
+        dh = 0.f;
+      } else {
+        st_sc1(dg + j, 0.f);
+        st_sc1(dg + H + j, 0.f);
+        st_sc1(dg + 2 * H + j, 0.f);
+        st_sc1(dg + 3 * H + j, 0.f);
+        dh = rec + dh;
+      }
+    }
+    if (s + 1 < L && !dir_barrier(&a.sync[dir], (unsigned)(s + 1) * G, &a.sync[2], &smem[PW * 512])) break;
+  }
+}
+
+}  // namespace
+
+bool bilstm_persist_ok(int B, int H) {
+  return B >= 1 && B <= 32 && H % 256 == 0 && H >= 256 && H <= 1024;
+}
+
+int bilstm_persist_fwd(const float* xproj, const float* whh_fwd, const float* whh_bwd, const int32_t* lengths,
+                       float* out, float* h_n, float* c_n, float* save_act, float* save_c, int B, int L, int H,
+                       float* hbuf, unsigned* sync, hipStream_t st) {
+  PFwd a{xproj, whh_fwd, whh_bwd, lengths, out, save_act, save_c, h_n, c_n, hbuf, sync, B, L, H};
+  void* args[] = {&a};
+  const dim3 grid(2 * H / PU), block(1024);
+  hipError_t e;
+  switch (H / 128) {
+    case 2: e = hipLaunchCooperativeKernel((const void*)bilstm_persist_fwd_kernel<2>, grid, block, args, 0, st); break;
+    case 4: e = hipLaunchCooperativeKernel((const void*)bilstm_persist_fwd_kernel<4>, grid, block, args, 0, st); break;
+    case 6: e = hipLaunchCooperativeKernel((const void*)bilstm_persist_fwd_kernel<6>, grid, block, args, 0, st); break;
+    case 8: e = hipLaunchCooperativeKernel((const void*)bilstm_persist_fwd_kernel<8>, grid, block, args, 0, st); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  if (e != hipSuccess) (void)hipGetLastError();
+  return (int)e;
+}
+
+int bilstm_persist_bwd(const float* whh_fwd, const float* whh_bwd, const int32_t* lengths, const float* save_act,
+                       const float* save_c, const float* dout, const float* dh_n, const float* dc_n, float* dgates,
+                       int B, int L, int H, unsigned* sync, hipStream_t st) {
+  PBwd a{whh_fwd, whh_bwd, lengths, save_act, save_c, dout, dh_n, dc_n, dgates, sync, B, L, H};
+  void* args[] = {&a};
+  const dim3 grid(2 * H / PU), block(1024);
+  hipError_t e;
+  switch (H / 64) {   // NGB = 4H / 256
+    case 4: e = hipLaunchCooperativeKernel((const void*)bilstm_persist_bwd_kernel<4>, grid, block, args, 0, st); break;
+    case 8: e = hipLaunchCooperativeKernel((const void*)bilstm_persist_bwd_kernel<8>, grid, block, args, 0, st); break;
+    case 12: e = hipLaunchCooperativeKernel((const void*)bilstm_persist_bwd_kernel<12>, grid, block, args, 0, st); break;
+    case 16: e = hipLaunchCooperativeKernel((const void*)bilstm_persist_bwd_kernel<16>, grid, block, args, 0, st); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  if (e != hipSuccess) (void)hipGetLastError();
+  return (int)e;
+}

@@ -209,8 +209,22 @@ def test_lstm_cell(dev):
     assert (dg.cpu() - gates.grad).abs().max() < 1e-5 and (dc0.cpu() - c0.grad).abs().max() < 1e-5
 
 
+@pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("B,L", [(20, 80), (3, 11), (40, 9)])
-def test_bilstm(dev, B, L):
+def test_bilstm(dev, B, L, mode):
+    """mode 1: one launch per timestep; mode 2: the persistent cooperative recurrence (B <= 32)."""
+    from dasa_amd import _lib, ops
+    if mode == 2 and B > 32:
+        pytest.skip("persistent recurrence needs B <= 32")
+    lib = _lib.lib()
+    assert lib.dasa_bilstm_set_mode(mode) == 0
+    try:
+        _check_bilstm(dev, B, L)
+    finally:
+        lib.dasa_bilstm_set_mode(0)
+
+
+def _check_bilstm(dev, B, L):
     from dasa_amd import ops
     torch.manual_seed(B + L)
     H, E = 1024, 768
