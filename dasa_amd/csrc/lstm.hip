@@ -283,6 +283,39 @@ __global__ __launch_bounds__(1024) void bilstm_bptt_step_kernel(BpttArgs a, int 
   }
 }
 
+// BPTT cell step for any B (the recurrent product rec[dir][b][j] was computed by dasa_gemm_f32).
+// Carries dh/dc [2][B][H] live in the workspace; same math as the fused step kernel above.
+__global__ void bilstm_bptt_cell_kernel(BpttArgs a, const float* __restrict__ rec, int s) {
+  const long total = 2L * a.B * a.H;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  const int H = a.H, B = a.B, L = a.L, G4 = 4 * H;
+  const int dir = (int)(idx / ((long)B * H));
+  const int rem = (int)(idx % ((long)B * H)), b = rem / H, j = rem % H;
+  const int t = dir == 0 ? (L - 1 - s) : s;
+  const float r = s > 0 ? rec[idx] : 0.f;
+  float* dg = a.dgates + (((long)b * L + t) * 2 + dir) * G4;
+  if (t < a.len[b]) {
+    const float G = r + a.dout[((long)b * L + t) * 2 * H + dir * H + j] + a.dh[idx];
+    const float* sa = a.save_act + (((long)t * 2 + dir) * B + b) * G4;
+    const float i_ = sa[j], f_ = sa[H + j], g_ = sa[2 * H + j], o_ = sa[3 * H + j];
+    const float ct = a.save_c[(((long)t * 2 + dir) * B + b) * H + j];
+    const int tq = dir == 0 ? t - 1 : t + 1;
+    const float cp = (tq >= 0 && tq < L) ? a.save_c[(((long)tq * 2 + dir) * B + b) * H + j] : 0.f;
+    const float tc = tanh_(ct);
+    const float dcv = a.dc[idx] + G * o_ * (1.f - tc * tc);
+    dg[j] = dcv * g_ * i_ * (1.f - i_);
+    dg[H + j] = dcv * cp * f_ * (1.f - f_);
+    dg[2 * H + j] = dcv * i_ * (1.f - g_ * g_);
+    dg[3 * H + j] = G * tc * o_ * (1.f - o_);
+    a.dc[idx] = dcv * f_;
+    a.dh[idx] = 0.f;
+  } else {
+    dg[j] = 0.f; dg[H + j] = 0.f; dg[2 * H + j] = 0.f; dg[3 * H + j] = 0.f;
+    a.dh[idx] = r + a.dh[idx];
+  }
+}
+
 // hprev[dir][b][t][:] = the recurrent input of step t: fwd out[b][t-1][0:H], bwd out[b][t+1][H:2H], 0 at the ends.
 __global__ void bilstm_hprev_kernel(const float* __restrict__ out, float* __restrict__ hprev, int B, int L, int H) {
   const long total = 2L * B * L * H;
@@ -411,6 +444,7 @@ extern "C" int dasa_bilstm_fwd(const float* xproj, const float* whh_fwd, const f
 }
 
 extern "C" int64_t dasa_bilstm_bwd_workspace(int32_t B, int32_t H) {
+  if (B > 32) return (int64_t)(6L * B * H * sizeof(float));   // carries + rec (GEMM path)
   return (int64_t)((4L * B * H + 8L * H * H) * sizeof(float));
 }
 
@@ -419,10 +453,43 @@ extern "C" int dasa_bilstm_bwd(const float* whh_fwd, const float* whh_bwd, const
                                const float* dc_n, float* dgates, int32_t B, int32_t L, int32_t H, float* ws,
                                void* stream) {
   if (B <= 0 || L <= 0) return 0;
-  if ((H % 64) || !ws || B > 32 || !save_act || !save_c || !dout || ((uintptr_t)ws & 15))
+  if ((H % 64) || !ws || !save_act || !save_c || !dout || ((uintptr_t)ws & 15))
     return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   const long S = 2L * B * H;
+  if (B > 32) {
+    // Large batch (e.g. every rollout step's sequences of one optimizer step, batched): per timestep
+    // one MFMA GEMM per direction for rec = dgates_prev . W_hh, then the cell kernel.
+    float* dh = ws;
+    float* dc = ws + S;
+    float* rec = ws + 2 * S;
+    if (dh_n) hipLaunchKernelGGL(copy_kernel, dim3(cdivi(S, 256)), dim3(256), 0, st, dh_n, dh, S);
+    else hipLaunchKernelGGL(fill_kernel, dim3(cdivi(S, 256)), dim3(256), 0, st, dh, S, 0.f);
+    DASA_CHECK_LAUNCH();
+    if (dc_n) hipLaunchKernelGGL(copy_kernel, dim3(cdivi(S, 256)), dim3(256), 0, st, dc_n, dc, S);
+    else hipLaunchKernelGGL(fill_kernel, dim3(cdivi(S, 256)), dim3(256), 0, st, dc, S, 0.f);
+    DASA_CHECK_LAUNCH();
+    BpttArgs a{nullptr, nullptr, lengths, save_act, save_c, dout, dgates, dh, dc, B, L, H};
+    for (int s = 0; s < L; ++s) {
+      if (s > 0) {
+        for (int dir = 0; dir < 2; ++dir) {
+          const int t = dir == 0 ? (L - 1 - s) : s;
+          const int tp = dir == 0 ? t + 1 : t - 1;
+          dasa_gemm_desc d{};
+          d.M = B; d.N = H; d.K = 4 * H; d.batch = 1; d.opA = 0; d.opB = 0;
+          d.A = dgates + ((long)tp * 2 + dir) * 4 * H; d.lda = (long)L * 2 * 4 * H;
+          d.B = dir ? whh_bwd : whh_fwd; d.ldb = H;
+          d.C = rec + (long)dir * B * H; d.ldc = H;
+          d.alpha = 1.f; d.beta = 0.f;
+          const int rc = dasa_gemm_f32(&d, nullptr, 0, stream);
+          if (rc) return rc;
+        }
+      }
+      hipLaunchKernelGGL(bilstm_bptt_cell_kernel, dim3(cdivi(S, 256)), dim3(256), 0, st, a, (const float*)rec, s);
+      DASA_CHECK_LAUNCH();
+    }
+    return 0;
+  }
   const int mode = lstm_mode();
   if (mode != 1 && bilstm_persist_ok(B, H)) {
     hipLaunchKernelGGL(fill_kernel, dim3(1), dim3(64), 0, st, ws, 16L, 0.f);   // barrier words

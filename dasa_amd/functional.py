@@ -3,6 +3,8 @@
 These are the differentiable building blocks of the reference-API modules in dasa_amd.r2r. Only
 the tensors a backward actually needs are saved, and nothing is saved when no input requires grad.
 """
+import contextlib
+
 import numpy as np
 import torch
 
@@ -282,6 +284,87 @@ class LSTMCellFn(torch.autograd.Function):
         return da, dx2, dh, (dc_prev if n[3] else None), dW_ih, dW_hh, db, db
 
 
+class _BpttDeferral:
+    """Batches the bi-LSTM BPTT of every encoder call of one backward pass.
+
+    The rollout runs the DicEncoder once per step (agent_dg.py:725-936), so one optimizer step holds
+    ~70 independent bi-LSTM graphs whose backward passes share nothing but the weights. When the
+    sequence input needs no gradient (its BERT/LXRT producer is detached, the README train config),
+    BiLSTMFn.backward only queues its saved tensors and the incoming gradients; flush() then runs ONE
+    recurrence over all queued sequences (B = steps x batch: an MFMA GEMM per timestep instead of 70
+    latency-bound recurrences) and adds dW_ih / dW_hh / db into the parameters' .grad. Same sums as
+    the per-call backward, in a different order."""
+
+    def __init__(self):
+        self.active = False
+        self.items = []
+
+
+_BPTT = _BpttDeferral()
+
+
+@contextlib.contextmanager
+def defer_bilstm_backward():
+    prev = _BPTT.active
+    _BPTT.active = True
+    try:
+        yield
+    finally:
+        _BPTT.active = prev
+
+
+def _acc_grad(p, g):
+    if p.grad is None:
+        p.grad = g
+    else:
+        p.grad.add_(g)
+
+
+def flush_bilstm_backward():
+    """Run the queued bi-LSTM backward passes (grouped by weights and shapes) into .grad."""
+    items, _BPTT.items = _BPTT.items, []
+    groups = {}
+    for it in items:
+        key = (tuple(id(p) for p in it["params"]), tuple(it["x"].shape))
+        groups.setdefault(key, []).append(it)
+    for grp in groups.values():
+        _batched_bptt(grp)
+
+
+def _batched_bptt(grp):
+    W_ih_f, W_hh_f, b_ih_f, b_hh_f, W_ih_b, W_hh_b, b_ih_b, b_hh_b = grp[0]["params"]
+    n = grp[0]["needs"]
+    B, L, E = grp[0]["x"].shape
+    H = W_hh_f.shape[1]
+    NB = B * len(grp)
+    sa = torch.cat([it["sa"] for it in grp], dim=2)          # [L][2][NB][4H]
+    sc = torch.cat([it["sc"] for it in grp], dim=2)          # [L][2][NB][H]
+    dout = torch.cat([it["dout"] if it["dout"] is not None else torch.zeros_like(it["out"]) for it in grp], 0)
+
+    def carry(k):
+        if all(it[k] is None for it in grp):
+            return None
+        return torch.cat([it[k] if it[k] is not None else torch.zeros(2, B, H, device=sa.device) for it in grp], 1)
+    lens = torch.cat([it["lens"] for it in grp], 0)
+    dgates = ops.bilstm_bwd(W_hh_f, W_hh_b, lens, (sa, sc), dout, carry("dh_n"), carry("dc_n"), H)
+    del sa, sc, dout
+    hprev = ops.bilstm_hprev(torch.cat([it["out"] for it in grp], 0), H)    # [2][NB][L][H]
+    x2 = torch.cat([it["x"] for it in grp], 0).reshape(NB * L, E)
+    for d, (iw, ihh, ibi, ibh) in enumerate(((2, 3, 4, 5), (6, 7, 8, 9))):
+        dg = dgates[:, :, d, :]                                # [NB, L, 4H] rows of stride 8H
+        P = grp[0]["params"]
+        if n[iw]:
+            _acc_grad(P[iw - 2], ops.matmul_tn(dg, x2))
+        if n[ihh]:
+            _acc_grad(P[ihh - 2], ops.matmul_tn(dg, hprev[d].reshape(NB * L, H)))
+        if n[ibi] or n[ibh]:
+            db = ops.colsum(dg)
+            if n[ibi]:
+                _acc_grad(P[ibi - 2], db)
+            if n[ibh]:
+                _acc_grad(P[ibh - 2], db.clone() if n[ibi] else db)
+
+
 class BiLSTMFn(torch.autograd.Function):
     """Packed single-layer bidirectional nn.LSTM (r2rmodel.py:2339-2343, pack/pad_packed semantics)."""
 
@@ -296,11 +379,10 @@ class BiLSTMFn(torch.autograd.Function):
         ops.linear(x2, W_ih_f, bf, out=xproj[:, :, 0, :])
         ops.linear(x2, W_ih_b, bb, out=xproj[:, :, 1, :])
         need = any(ctx.needs_input_grad)
-        out, h_n, c_n, saved = ops.bilstm_fwd(xproj, W_hh_f, W_hh_b, lengths_i32, H, save=need and B <= 32)
+        out, h_n, c_n, saved = ops.bilstm_fwd(xproj, W_hh_f, W_hh_b, lengths_i32, H, save=need)
         if need:
-            if B > 32:
-                raise NotImplementedError("bi-LSTM backward is implemented for B <= 32 per rank")
             ctx.save_for_backward(x, lengths_i32, out, saved[0], saved[1], W_ih_f, W_hh_f, W_ih_b, W_hh_b)
+            ctx.params = (W_ih_f, W_hh_f, b_ih_f, b_hh_f, W_ih_b, W_hh_b, b_ih_b, b_hh_b)
         ctx.H = H
         return out, h_n, c_n
 
@@ -309,12 +391,18 @@ class BiLSTMFn(torch.autograd.Function):
         x, lens, out, sa, sc, W_ih_f, W_hh_f, W_ih_b, W_hh_b = ctx.saved_tensors
         H = ctx.H
         B, L, E = x.shape
+        n = ctx.needs_input_grad
+        if _BPTT.active and not n[0]:
+            _BPTT.items.append(dict(x=x, lens=lens, out=out, sa=sa, sc=sc, params=ctx.params, needs=n,
+                                    dout=dout.contiguous() if dout is not None else None,
+                                    dh_n=dh_n.contiguous() if dh_n is not None else None,
+                                    dc_n=dc_n.contiguous() if dc_n is not None else None))
+            return (None,) * 10
         if dout is None:
             dout = torch.zeros_like(out)
         dgates = ops.bilstm_bwd(W_hh_f, W_hh_b, lens, (sa, sc), dout, dh_n, dc_n, H)
         hprev = ops.bilstm_hprev(out, H)
         x2 = x.reshape(B * L, E)
-        n = ctx.needs_input_grad
         grads = [None] * 10
         dx = None
         for d, (iw, ihh, ibi, ibh, Wih) in enumerate(((2, 3, 4, 5, W_ih_f), (6, 7, 8, 9, W_ih_b))):

@@ -607,7 +607,9 @@ class Seq2SeqAgent(BaseAgent):
 
     def optim_step(self, **kwargs):
         """agent_dg.py:1389-1405 (+ data-parallel gradient all-reduce before clipping)."""
-        self.loss.backward()
+        with DF.defer_bilstm_backward():     # the encoder's per-step bi-LSTM BPTTs run batched below
+            self.loss.backward()
+        DF.flush_bilstm_backward()
         if self.grad_sync is not None:
             self.grad_sync()
         torch.nn.utils.clip_grad_norm_(self.encoder.parameters(), 40.0)

@@ -195,8 +195,11 @@ def test_rollout_eval_argmax(R, dev, host_path):
     assert ["|".join(p[0] for p in tr["path"]) for tr in traj] == list(G["eval/paths"])
 
 
-def test_train_iteration_grads(R, dev):
-    """accumulate_gradient('sample') + backward with every dropout p = 0 and argmax 'sampling'."""
+@pytest.mark.parametrize("deferred", [False, True])
+def test_train_iteration_grads(R, dev, deferred):
+    """accumulate_gradient('sample') + backward with every dropout p = 0 and argmax 'sampling'.
+    deferred: the bi-LSTM BPTTs of all encoder calls run as one batched recurrence (optim_step's path)."""
+    from dasa_amd import functional as DF
     param = R[0]
     G = golden("cfg1_rollout")
     cfg = GI.CFG1
@@ -217,7 +220,12 @@ def test_train_iteration_grads(R, dev):
     assert abs(ag.logs["normalized_rl_loss"][-1] - float(G["train/rl_loss"])) < TOL
     assert ag.logs["viewsteps/teacher"][-1] == int(G["train/steps_teacher"])
     assert ag.logs["viewsteps/sample"][-1] == int(G["train/steps_sample"])
-    ag.loss.backward()
+    if deferred:
+        with DF.defer_bilstm_backward():
+            ag.loss.backward()
+        DF.flush_bilstm_backward()
+    else:
+        ag.loss.backward()
     n = 0
     for name, mod in (("encoder", ag.encoder), ("decoder", ag.decoder), ("critic", ag.critic), ("adaIn", ag.adaIn)):
         n += check_grads(G, f"train/{name}.", [(k, p.grad) for k, p in mod.named_parameters()], rtol=2e-3)
