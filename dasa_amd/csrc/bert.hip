@@ -211,61 +211,108 @@ struct MhaArgs {
   int B, heads, Lq, Lk; float scale; float p; uint64_t seed;
 };
 
-// grid (B*heads, ceil(Lq/16)), 256 threads; each wave handles 4 query rows.
-__global__ __launch_bounds__(256) void mha_fwd_kernel(MhaArgs a) {
-  __shared__ float Ks[kMaxLk][kDh + 1];
-  __shared__ float Vs[kMaxLk][kDh];
-  __shared__ float qs[4][kDh];
-  __shared__ float ps[4][kMaxLk];
-  const int bh = blockIdx.x, b = bh / a.heads, h = bh % a.heads;
-  const int Lk = a.Lk;
-  for (int idx = threadIdx.x; idx < Lk * kDh; idx += 256) {
-    const int j = idx / kDh, d = idx % kDh;
-    Ks[j][d] = a.K[((long)b * Lk + j) * a.ldk + h * kDh + d];
-    Vs[j][d] = a.V[((long)b * Lk + j) * a.ldv + h * kDh + d];
+// Forward on matrix cores (v_mfma_f32_32x32x2_f32), one wave per (batch, head, 32-query tile), no
+// LDS and no workgroup barriers. The wave computes S^T = K Q^T (keys on the rows/registers, queries
+// on the lanes), so the softmax over keys is an in-lane reduction plus one cross-half shuffle, and
+// the probability tile, as it sits in the accumulator, is directly the A operand of O = P V (an
+// MFMA summing over the accumulator's row index takes it with no lane movement: register r of lane
+// half hh holds key (r&3) + 8(r>>2) + 4hh, and the V operand is loaded for exactly that key).
+// NKT = ceil(Lk / 32) key tiles (Lk <= 128).
+__device__ __forceinline__ int acc_row(int r, int hh) { return (r & 3) + 8 * (r >> 2) + 4 * hh; }
+
+template <int NKT>
+__global__ __launch_bounds__(256) void mha_fwd_kernel(MhaArgs a, int nqt) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long wid = (long)blockIdx.x * 4 + w;
+  if (wid >= (long)a.B * a.heads * nqt) return;   // whole waves only; no barriers below
+  const int qt = (int)(wid % nqt);
+  const long bh = wid / nqt;
+  const int h = (int)(bh % a.heads), b = (int)(bh / a.heads);
+  const int Lq = a.Lq, Lk = a.Lk, q0 = qt * 32;
+  const int j = lane & 31, hh = lane >> 5;
+  // B operand of S^T: Q^T, lane (query j, half hh) holds Q[q0 + j][8g + 4hh .. +3] (K-permuted)
+  const float* qp = a.Q + ((long)b * Lq + min(q0 + j, Lq - 1)) * a.ldq + h * kDh + 4 * hh;
+  float4 qf[8];
+#pragma unroll
+  for (int g = 0; g < 8; ++g) qf[g] = *reinterpret_cast<const float4*>(qp + 8 * g);
+  floatx16 st[NKT];
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+    const float* kp = a.K + ((long)b * Lk + min(kt * 32 + j, Lk - 1)) * a.ldk + h * kDh + 4 * hh;
+    float4 kf[8];
+#pragma unroll
+    for (int g = 0; g < 8; ++g) kf[g] = *reinterpret_cast<const float4*>(kp + 8 * g);
+    floatx16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(kf[g].x, qf[g].x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(kf[g].y, qf[g].y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(kf[g].z, qf[g].z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(kf[g].w, qf[g].w, acc, 0, 0, 0);
+    }
+    st[kt] = acc;
   }
-  __syncthreads();
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // scale + additive key mask; keys past Lk -> -inf
   const float* mrow = a.mask ? a.mask + (long)b * Lk : nullptr;
-  for (int qi = 0; qi < 4; ++qi) {
-    const int i = blockIdx.y * 16 + w * 4 + qi;
-    if (i >= a.Lq) break;
-    qs[w][lane] = a.Q[((long)b * a.Lq + i) * a.ldq + h * kDh + lane];
-    __builtin_amdgcn_wave_barrier();
-    float s0 = -INFINITY, s1 = -INFINITY;
-    if (lane < Lk) {
-      float acc = 0.f;
-#pragma unroll 16
-      for (int d = 0; d < kDh; ++d) acc = fmaf(qs[w][d], Ks[lane][d], acc);
-      s0 = acc * a.scale + (mrow ? mrow[lane] : 0.f);
+  float m = -INFINITY;
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = kt * 32 + acc_row(r, hh);
+      const float mk = mrow ? mrow[min(key, Lk - 1)] : 0.f;
+      const float v = key < Lk ? st[kt][r] * a.scale + mk : -INFINITY;
+      st[kt][r] = v;
+      m = fmaxf(m, v);
     }
-    if (lane + 64 < Lk) {
-      float acc = 0.f;
-#pragma unroll 16
-      for (int d = 0; d < kDh; ++d) acc = fmaf(qs[w][d], Ks[lane + 64][d], acc);
-      s1 = acc * a.scale + (mrow ? mrow[lane + 64] : 0.f);
+  m = fmaxf(m, __shfl_xor(m, 32));
+  float sum = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float e = __expf(st[kt][r] - m);
+      st[kt][r] = e;
+      sum += e;
     }
-    const float m = wave_max(fmaxf(s0, s1));
-    const float e0 = lane < Lk ? __expf(s0 - m) : 0.f;
-    const float e1 = lane + 64 < Lk ? __expf(s1 - m) : 0.f;
-    const float inv = 1.f / wave_sum(e0 + e1);
-    float p0 = e0 * inv, p1 = e1 * inv;
-    const long prow = (((long)b * a.heads + h) * a.Lq + i) * Lk;
-    if (a.probs) {
-      if (lane < Lk) a.probs[prow + lane] = p0;
-      if (lane + 64 < Lk) a.probs[prow + lane + 64] = p1;
+  sum += __shfl_xor(sum, 32);
+  const float inv = 1.f / sum;
+  const int q = q0 + j;
+  const long prow = (bh * Lq + q) * (long)Lk;   // probs / dropout index base of this query row
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = kt * 32 + acc_row(r, hh);
+      float p = st[kt][r] * inv;
+      if (a.probs && q < Lq && key < Lk) a.probs[prow + key] = p;
+      if (a.p > 0.f) p *= dasa_dropout_scale(a.p, a.seed, (uint64_t)(prow + key));
+      st[kt][r] = p;
     }
-    if (a.p > 0.f) {
-      p0 *= dasa_dropout_scale(a.p, a.seed, (uint64_t)prow + lane);
-      p1 *= dasa_dropout_scale(a.p, a.seed, (uint64_t)prow + lane + 64);
+  // O = P V: A operand = the probability accumulator (rows = keys), B operand = V[key][d0 + lane]
+  floatx16 o0, o1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { o0[r] = 0.f; o1[r] = 0.f; }
+  const float* vb = a.V + (long)b * Lk * a.ldv + h * kDh + j;
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float* vr = vb + (long)min(kt * 32 + acc_row(r, hh), Lk - 1) * a.ldv;
+      o0 = __builtin_amdgcn_mfma_f32_32x32x2f32(st[kt][r], vr[0], o0, 0, 0, 0);
+      o1 = __builtin_amdgcn_mfma_f32_32x32x2f32(st[kt][r], vr[32], o1, 0, 0, 0);
     }
-    ps[w][lane] = p0;
-    ps[w][lane + 64] = p1;
-    __builtin_amdgcn_wave_barrier();
-    float o = 0.f;
-    for (int j = 0; j < Lk; ++j) o = fmaf(ps[w][j], Vs[j][lane], o);
-    a.out[((long)b * a.Lq + i) * a.ldo + h * kDh + lane] = o;
-    __builtin_amdgcn_wave_barrier();
+  // O tile: col = d (lane), row = query q0 + acc_row(r, hh)
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int qq = q0 + acc_row(r, hh);
+    if (qq < Lq) {
+      float* op = a.out + ((long)b * Lq + qq) * a.ldo + h * kDh + j;
+      op[0] = o0[r];
+      op[32] = o1[r];
+    }
   }
 }
 
@@ -444,7 +491,15 @@ extern "C" int dasa_mha_fwd(const float* Q, int64_t ldq, const float* K, int64_t
   if (B <= 0 || Lq <= 0) return 0;
   if (dh != kDh || Lk <= 0 || Lk > kMaxLk) return (int)hipErrorInvalidValue;
   MhaArgs a{Q, ldq, K, ldk, V, ldv, addmask, out, ldo, probs, B, heads, Lq, Lk, scale, drop_p, seed};
-  hipLaunchKernelGGL(mha_fwd_kernel, dim3(B * heads, cdivi(Lq, 16)), dim3(256), 0, (hipStream_t)stream, a);
+  const int nqt = cdivi(Lq, 32);
+  const dim3 grid(cdivi((long)B * heads * nqt, 4)), block(256);
+  hipStream_t st = (hipStream_t)stream;
+  switch (cdivi(Lk, 32)) {
+    case 1: hipLaunchKernelGGL(mha_fwd_kernel<1>, grid, block, 0, st, a, nqt); break;
+    case 2: hipLaunchKernelGGL(mha_fwd_kernel<2>, grid, block, 0, st, a, nqt); break;
+    case 3: hipLaunchKernelGGL(mha_fwd_kernel<3>, grid, block, 0, st, a, nqt); break;
+    default: hipLaunchKernelGGL(mha_fwd_kernel<4>, grid, block, 0, st, a, nqt); break;
+  }
   DASA_CHECK_LAUNCH();
   return 0;
 }

@@ -17,7 +17,7 @@ FAMILIES = {
     "shift_attn_bwd": ("hbm", "scores_kernel+apply_bwd_kernel"),
     "softdot": ("hbm", "scores_kernel+apply_fwd_kernel"),
     "softdot_bwd": ("hbm", "scores_kernel+apply_bwd_kernel"),
-    "mha": ("hbm", "mha_fwd_kernel"),
+    "mha": ("mfma", "mha_fwd_kernel"),
     "layernorm": ("hbm", "ln_fwd_kernel"),
     "embed": ("hbm", "embed_kernel"),
     "ada_gate": ("hbm", "ada_gate_*_kernel"),
