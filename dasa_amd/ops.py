@@ -34,8 +34,13 @@ _ACT_IDS = {None: ACT_NONE, "none": ACT_NONE, "relu": ACT_RELU, "gelu": ACT_GELU
             "sigmoid": ACT_SIGMOID}
 
 
+_raw_stream = torch._C._cuda_getCurrentRawStream
+
+
 def _stream():
-    return torch.cuda.current_stream().cuda_stream
+    """Raw hipStream_t of torch's current stream on the current device (the fast C accessor: the
+    torch.cuda.current_stream() object path costs ~8 us per launch on the host)."""
+    return _raw_stream(torch.cuda.current_device())
 
 
 def _p(t):
@@ -54,6 +59,9 @@ def _f32(t, name):
 
 def _rows(t):
     """(rows, ld) of a tensor viewed as a 2-D row-major matrix over its last dim (unit inner stride)."""
+    if t.is_contiguous():
+        n = t.shape[-1] if t.dim() else 1
+        return (t.numel() // n if n else 0), n
     if t.stride(-1) != 1:
         raise _lib.DasaError("inner dimension must be contiguous")
     if t.dim() == 1:
@@ -71,6 +79,30 @@ def _rows(t):
 
 
 # ------------------------------------------------------------------------------------------ GEMM
+_WS = {}
+_WS_MIN = 32 << 20
+
+
+def _gemm_ws(device, d):
+    """Split-K partials workspace: one buffer per (device, stream), grown on demand and reused by every
+    GEMM on that stream (a GEMM's split-K pass and its reduce run back to back on the stream, so a later
+    GEMM on the same stream cannot overwrite partials still in use). Saves a workspace query and an
+    allocation per launch; falls back to the exact query when the buffer is too small."""
+    key = (device.index, _stream())
+    buf = _WS.get(key)
+    if buf is None:
+        buf = torch.empty(_WS_MIN // 4, dtype=torch.float32, device=device)
+        _WS[key] = buf
+    nbytes = buf.numel() * 4
+    if d.M * d.N * max(1, d.batch) * 16 * 4 > nbytes:   # split-K is at most 16-way
+        need = _lib.lib().dasa_gemm_f32_workspace(ctypes.byref(d))
+        if need > nbytes:
+            buf = torch.empty(need // 4 + 1, dtype=torch.float32, device=device)
+            _WS[key] = buf
+            nbytes = buf.numel() * 4
+    return buf.data_ptr(), nbytes
+
+
 def gemm(A, B, C, *, M, N, K, opA=0, opB=1, lda, ldb, ldc, bias=None, act=None, aux=None, ld_aux=0,
          colscale=None, alpha=1.0, beta=0.0, batch=1, strideA=0, strideB=0, strideC=0, strideAux=0):
     """Raw descriptor call (see include/dasa_hip.h). A/B/C are tensors (base pointers used)."""
@@ -86,12 +118,9 @@ def gemm(A, B, C, *, M, N, K, opA=0, opB=1, lda, ldb, ldc, bias=None, act=None, 
     d.colscale = _p(colscale)
     d.alpha, d.beta = float(alpha), float(beta)
     L = _lib.lib()
-    need = L.dasa_gemm_f32_workspace(ctypes.byref(d))
-    ws = None
-    if need > 0:
-        ws = torch.empty(need // 4 + 1, dtype=torch.float32, device=C.device)
+    ws, ws_bytes = _gemm_ws(C.device, d)
     b = max(1, int(batch))
-    _call("dasa_gemm_f32", "gemm", L.dasa_gemm_f32, ctypes.byref(d), _p(ws), int(need), _stream(),
+    _call("dasa_gemm_f32", "gemm", L.dasa_gemm_f32, ctypes.byref(d), ws, ws_bytes, _stream(),
           flops=2.0 * M * N * K * b, nbytes=4.0 * b * (M * K + K * N + M * N),
           detail=(int(M), int(N), int(K), b, int(opA), int(opB)))
 

@@ -31,6 +31,48 @@ class ReverseFn(torch.autograd.Function):
         return ops.reverse_valid(dy.contiguous(), lens), None
 
 
+class _LangPipe:
+    """Language stack of the coming rollout steps, computed in chunks of `chunk` steps, one unit
+    (embeddings, then each BertLayer) per pump() call. Outputs come out in step order."""
+
+    def __init__(self, bert, ids, att_mask, steps, chunk):
+        self.bert = bert
+        self.ids = ids
+        self.ext = ((1.0 - att_mask.float()) * -10000.0).unsqueeze(1).unsqueeze(2)
+        self.budget = steps
+        self.chunk = chunk
+        self.ready = []
+        self.cur = None
+
+    def pump(self, units):
+        bert = self.bert
+        with torch.no_grad():
+            while units > 0:
+                if self.cur is None:
+                    if self.budget <= 0:
+                        return
+                    S = min(self.chunk, self.budget)
+                    self.budget -= S
+                    self.cur = [S, None, 0, self.ids.repeat(S, 1), self.ext.repeat(S, 1, 1, 1)]
+                S, x, k, ids, ext = self.cur
+                x = bert.embeddings(ids) if k == 0 else bert.lalayer[k - 1](x, ext)[0]
+                k += 1
+                units -= 1
+                if k == len(bert.lalayer) + 1:
+                    B, L = self.ids.shape
+                    self.ready.extend(x.view(S, B, L, x.shape[-1]).unbind(0))
+                    self.cur = None
+                else:
+                    self.cur = [S, x, k, ids, ext]
+
+    def take(self):
+        while not self.ready:
+            if self.cur is None and self.budget <= 0:
+                return None
+            self.pump(1)
+        return self.ready.pop(0)
+
+
 class DicEncoder(nn.Module):
     lstm_num_layers = 1
 
@@ -73,23 +115,28 @@ class DicEncoder(nn.Module):
             self.ctx_v_to_v = nn.Linear(self.transformer_hidden_size, 2048 + args.angle_feat_size)
         self._lang_cache_on = False
         self._lang_cache = None
-        # train-mode language prefetch: steps of the current rollout not yet computed, and computed ones
+        # train-mode language pipeline (see cache_language)
         self.lang_chunk = int(os.environ.get("DASA_LANG_CHUNK", "8"))
-        self._lang_budget = 0
-        self._lang_queue = []
+        self._lang_steps = 0
+        self._lang_pipe = None
 
     # ------------------------------------------------------------------ language-stack cache
     def cache_language(self, on=True, steps=0):
         """Called by the agent at the start of every rollout (so nothing survives into the next batch).
         on: eval-mode cache (the stack is deterministic and detached: computed once per rollout).
-        steps: train-mode prefetch budget. With dropout active the stack differs every step, but it
-        never sees the panorama, so the next `lang_chunk` steps' stacks (each with its own dropout
-        draw, as the reference's per-step calls) are computed in one batched pass of lang_chunk x B
-        sequences and handed out one per encoder call."""
+        steps: train-mode pipeline budget. With dropout active the stack differs every step, but it
+        never sees the panorama, so the stacks of the next `lang_chunk` steps (each with its own dropout
+        draw, as the reference's per-step calls) are computed as one batched pass over lang_chunk x B
+        sequences, one layer at a time: lang_pump() advances it where the GPU would otherwise wait for
+        the host (after the step's action sync), and each encoder call takes the next step's output."""
         self._lang_cache_on = on
         self._lang_cache = None
-        self._lang_budget = int(steps)
-        self._lang_queue = []
+        self._lang_steps = int(steps)
+        self._lang_pipe = None
+
+    def lang_pump(self, units=2):
+        if self._lang_pipe is not None:
+            self._lang_pipe.pump(units)
 
     def _language(self, ids, att_mask):
         bert = self.bert
@@ -103,16 +150,11 @@ class DicEncoder(nn.Module):
                 with torch.no_grad():
                     self._lang_cache = (key, bert.language(ids, ext))
             return self._lang_cache[1]
-        if bert.training and self.lang_chunk > 1 and (self._lang_queue or self._lang_budget > 0):
-            if not self._lang_queue:
-                S = min(self.lang_chunk, self._lang_budget)
-                self._lang_budget -= S
-                B, L = ids.shape
-                ext = ((1.0 - att_mask.float()) * -10000.0).unsqueeze(1).unsqueeze(2)
-                with torch.no_grad():
-                    x = bert.language(ids.repeat(S, 1), ext.repeat(S, 1, 1, 1))
-                self._lang_queue = list(x.view(S, B, L, x.shape[-1]).unbind(0))
-            return self._lang_queue.pop(0)
+        if bert.training and self.lang_chunk > 1:
+            if self._lang_pipe is None and self._lang_steps > 0:
+                self._lang_pipe = _LangPipe(bert, ids, att_mask, self._lang_steps, self.lang_chunk)
+            if self._lang_pipe is not None:
+                return self._lang_pipe.take()
         return None
 
     # ------------------------------------------------------------------ forward
