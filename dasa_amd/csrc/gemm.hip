@@ -61,7 +61,7 @@ __device__ __forceinline__ float4 load4(const float* rowp, int e, int limit) {
   return r;
 }
 
-constexpr int BKT = 32;
+constexpr int BKT = 32;   // default K tile (the BK = 64 configurations set their own)
 
 // Component-wise select (a whole-float4 ternary is lowered through scratch memory by hipcc).
 __device__ __forceinline__ float4 sel4(bool c, float4 v) {
@@ -69,11 +69,17 @@ __device__ __forceinline__ float4 sel4(bool c, float4 v) {
 }
 
 // KC = operand stored with K contiguous ([rows][K]); else stored [K][rows].
-// LDS images: KC -> [ROWS][BKT] with the eight 16-B quads of each row XOR-swizzled by (row>>1)&7, so
-// the K-permuted ds_read_b128 fragment reads below hit 16 distinct bank slots per lane group;
-// !KC -> [BKT][ROWS + 4] (k-major, read one float per lane).
-template <int ROWS, bool KC, bool VEC, int NT>
+// LDS images: KC -> [ROWS][BK] with the 16-B quads of each row XOR-swizzled by row (BK = 32: eight
+// quads, two rows per 256-B bank row, swizzle (row>>1)&7; BK = 64: sixteen quads, one row per bank
+// row, swizzle row&15), so the K-permuted ds_read_b128 fragment reads below hit 16 distinct bank
+// slots in each of the instruction's four 16-lane groups; !KC -> [BK][ROWS + 4] (k-major, read one
+// float per lane).
+template <int BK>
+__device__ __forceinline__ int qswz(int row) { return BK == 32 ? ((row >> 1) & 7) : (row & 15); }
+
+template <int ROWS, bool KC, bool VEC, int NT, int BK>
 struct TileLoader {
+  static constexpr int BKT = BK;
   static constexpr int PAD = KC ? 0 : 4;
   static constexpr int LDS_FL = KC ? ROWS * BKT : BKT * (ROWS + PAD);
   static constexpr int TOTAL = ROWS * BKT / 4;   // float4 per tile
@@ -125,7 +131,7 @@ struct TileLoader {
       const float4 v = sel4(ok[i], r[i]);
       if (KC) {
         const int row = q / (BKT / 4), kq = q % (BKT / 4);
-        *reinterpret_cast<float4*>(S + row * BKT + 4 * (kq ^ ((row >> 1) & 7))) = v;
+        *reinterpret_cast<float4*>(S + row * BKT + 4 * (kq ^ qswz<BK>(row))) = v;
       } else {
         const int kr = q / (ROWS / 4), rq = q % (ROWS / 4);
         *reinterpret_cast<float4*>(S + kr * (ROWS + PAD) + 4 * rq) = v;
@@ -137,7 +143,7 @@ struct TileLoader {
   // four MFMAs together accumulate exactly k = 8s .. 8s+7.
   __device__ __forceinline__ static float4 frag(const float* S, int row, int s, int h) {
     if (KC) {
-      return *reinterpret_cast<const float4*>(S + row * BKT + 4 * ((2 * s + h) ^ ((row >> 1) & 7)));
+      return *reinterpret_cast<const float4*>(S + row * BKT + 4 * ((2 * s + h) ^ qswz<BK>(row)));
     } else {
       const int k = 8 * s + 4 * h;
       return make_float4(S[(k + 0) * (ROWS + PAD) + row], S[(k + 1) * (ROWS + PAD) + row],
@@ -152,7 +158,7 @@ __device__ __forceinline__ float f4get(const float4& v, int e) {
 
 // KW > 1 splits every 32-deep K-tile between KW wave groups that own the same output sub-tiles
 // (in-block split-K): more waves per block for mid-size GEMMs, reduced through LDS at the end.
-template <int BM, int BN, int WM, int WN, int KW, bool AKC, bool BKC, bool VEC>
+template <int BM, int BN, int WM, int WN, int KW, bool AKC, bool BKC, bool VEC, int BKT>
 __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN) * KW) void gemm_f32_kernel(GemmP p) {
   constexpr int TM = WM / 32, TN = WN / 32;
   constexpr int WAVES_N = BN / WN;
@@ -161,8 +167,9 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN) * KW) void gemm_f32_kern
   constexpr int NGRP = BKT / 8;                 // K-groups of 8 per tile
   static_assert(NGRP % KW == 0, "K-split must divide the K tile");
   constexpr int GPW = NGRP / KW;                // K-groups per wave group
-  using LA = TileLoader<BM, AKC, VEC, NT>;
-  using LB = TileLoader<BN, BKC, VEC, NT>;
+  constexpr int PH = GPW < 4 ? GPW : 4;         // K-groups per fragment-read phase
+  using LA = TileLoader<BM, AKC, VEC, NT, BKT>;
+  using LB = TileLoader<BN, BKC, VEC, NT, BKT>;
   // one LDS array: the A/B double buffers, reused by the K-split reduction after the main loop
   constexpr int A_FL = 2 * LA::LDS_FL, B_FL = 2 * LB::LDS_FL;
   constexpr int RED_FL = (KW - 1) * BM * BN;
@@ -225,29 +232,32 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN) * KW) void gemm_f32_kern
     }
     const float* As = smem + buf * LA::LDS_FL;
     const float* Bs = smem + A_FL + buf * LB::LDS_FL;
-    // all fragments of this wave group's K-groups first, then the MFMAs (reads overlap the MACs)
-    float4 af[GPW][TM], bf[GPW][TN];
+    // fragments of up to 4 K-groups first, then their MFMAs (the reads overlap the MACs)
 #pragma unroll
-    for (int g = 0; g < GPW; ++g) {
-      const int s = kgrp * GPW + g;
+    for (int g0 = 0; g0 < GPW; g0 += PH) {
+      float4 af[PH][TM], bf[PH][TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[g][i] = LA::frag(As, wm + i * 32 + rl, s, hl);
+      for (int g = 0; g < PH; ++g) {
+        const int s = kgrp * GPW + g0 + g;
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bf[g][j] = LB::frag(Bs, wn + j * 32 + rl, s, hl);
+        for (int i = 0; i < TM; ++i) af[g][i] = LA::frag(As, wm + i * 32 + rl, s, hl);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bf[g][j] = LB::frag(Bs, wn + j * 32 + rl, s, hl);
+      }
+      // keep the fragment reads ahead of the MFMAs: hipcc otherwise re-uses one register set and
+      // serialises read -> lgkmcnt(0) -> 4 MFMAs per K-group, exposing the LDS latency each time
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int g = 0; g < PH; ++g)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(af[g][i], e), f4get(bf[g][j], e),
+                                                               acc[i][j], 0, 0, 0);
     }
-    // keep every fragment read ahead of the MFMAs: hipcc otherwise re-uses one register set and
-    // serialises read -> lgkmcnt(0) -> 4 MFMAs per K-group, exposing the LDS latency each time
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int g = 0; g < GPW; ++g)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(af[g][i], e), f4get(bf[g][j], e),
-                                                             acc[i][j], 0, 0, 0);
     ya.store(smem + (buf ^ 1) * LA::LDS_FL);   // past the last tile this writes an unused buffer
     yb.store(smem + A_FL + (buf ^ 1) * LB::LDS_FL);
     __syncthreads();
@@ -380,15 +390,15 @@ __global__ void splitk_reduce_kernel(GemmP p) {
   }
 }
 
-template <int BM, int BN, int WM, int WN, int KW, bool VEC>
+template <int BM, int BN, int WM, int WN, int KW, bool VEC, int BK = 32>
 int launch_tile(const GemmP& p, int opA, int opB, hipStream_t st) {
   dim3 grid((p.N + BN - 1) / BN, (p.M + BM - 1) / BM, p.batch * p.splitk);
   dim3 block(64 * (BM / WM) * (BN / WN) * KW);
   const bool akc = (opA == 0), bkc = (opB == 1);
-  if (akc && bkc) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, KW, true, true, VEC>), grid, block, 0, st, p);
-  else if (akc && !bkc) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, KW, true, false, VEC>), grid, block, 0, st, p);
-  else if (!akc && bkc) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, KW, false, true, VEC>), grid, block, 0, st, p);
-  else hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, KW, false, false, VEC>), grid, block, 0, st, p);
+  if (akc && bkc) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, KW, true, true, VEC, BK>), grid, block, 0, st, p);
+  else if (akc && !bkc) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, KW, true, false, VEC, BK>), grid, block, 0, st, p);
+  else if (!akc && bkc) hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, KW, false, true, VEC, BK>), grid, block, 0, st, p);
+  else hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, KW, false, false, VEC, BK>), grid, block, 0, st, p);
   DASA_CHECK_LAUNCH();
   return 0;
 }
@@ -407,6 +417,10 @@ constexpr TileCfg kCfgs[] = {
     {128, 128, 64, 64, 2},  // 8
     {32, 64, 32, 32, 4},    // 9
     {64, 32, 32, 32, 2},    // 10
+    {64, 64, 32, 32, 2},    // 11: BK = 64
+    {32, 64, 32, 32, 2},    // 12: BK = 64
+    {128, 64, 64, 32, 1},   // 13: BK = 64
+    {64, 128, 32, 64, 2},   // 14: BK = 64
 };
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
@@ -426,7 +440,11 @@ int launch_cfg(int cfg, bool vec, const GemmP& p, int opA, int opB, hipStream_t 
     case 7: return launch_tile<64, 128, 32, 64, 2, true>(p, opA, opB, st);
     case 8: return launch_tile<128, 128, 64, 64, 2, true>(p, opA, opB, st);
     case 9: return launch_tile<32, 64, 32, 32, 4, true>(p, opA, opB, st);
-    default: return launch_tile<64, 32, 32, 32, 2, true>(p, opA, opB, st);
+    case 10: return launch_tile<64, 32, 32, 32, 2, true>(p, opA, opB, st);
+    case 11: return launch_tile<64, 64, 32, 32, 2, true, 64>(p, opA, opB, st);
+    case 12: return launch_tile<32, 64, 32, 32, 2, true, 64>(p, opA, opB, st);
+    case 13: return launch_tile<128, 64, 64, 32, 1, true, 64>(p, opA, opB, st);
+    default: return launch_tile<64, 128, 32, 64, 2, true, 64>(p, opA, opB, st);
   }
 }
 
@@ -452,7 +470,8 @@ static Plan make_plan(const dasa_gemm_desc* d) {
   // 256 CUs; the skinny decoder GEMMs (M <= 32) are weight-streaming and split K widely.
   const long t64 = tiles(64, 64);
   if (M <= 32) pl.cfg = 5;
-  else if (t64 >= 2048) pl.cfg = 0;
+  else if (d->opA == 1 && K >= 8192 && t64 >= 256) pl.cfg = 8;   // weight grads over many rows
+  else if (t64 >= 2048) pl.cfg = 6;                              // profiles/r01/gemm_grid_v4.txt
   else if (t64 >= 800) pl.cfg = 4;
   else if (t64 >= 400) pl.cfg = (t64 >= 500 && K < 1536) ? 5 : 4;
   else if (t64 >= 250 && (K < 1536 || t64 >= 320)) pl.cfg = 5;
@@ -472,11 +491,11 @@ static Plan make_plan(const dasa_gemm_desc* d) {
     }
   } else if (blocks < 400 && K >= 1536) {
     splitk = (int)((K + 384) / 768);
-    if (splitk > 4) splitk = 4;
+    if (splitk > (blocks < 200 ? 3 : 4)) splitk = blocks < 200 ? 3 : 4;
   }
   if (fsplit > 0) splitk = fsplit;
-  int kchunk = (int)(cdiv(cdiv(K, splitk), BKT) * BKT);
-  if (kchunk < BKT) kchunk = BKT;
+  int kchunk = (int)(cdiv(cdiv(K, splitk), 64) * 64);   // a whole number of K tiles for BK 32 and 64
+  if (kchunk < 64) kchunk = 64;
   splitk = K > 0 ? (int)cdiv(K, kchunk) : 1;
   pl.splitk = splitk;
   pl.kchunk = kchunk;
@@ -501,7 +520,7 @@ extern "C" int dasa_gemm_f32(const dasa_gemm_desc* d, void* ws, int64_t ws_bytes
   Plan pl = make_plan(d);
   if (pl.splitk > 1 && (ws == nullptr || ws_bytes < pl.ws)) {  // no workspace: single pass
     pl.splitk = 1;
-    pl.kchunk = K > 0 ? (int)(cdiv(K, BKT) * BKT) : BKT;
+    pl.kchunk = K > 0 ? (int)(cdiv(K, 64) * 64) : 64;
   }
   if (M == 0 || N == 0) return 0;
   // float4 operand loads need 16-B aligned rows; anything else takes the scalar-load variant

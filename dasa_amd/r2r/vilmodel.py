@@ -7,6 +7,7 @@ attention core (dasa_mha_fwd). Attention masks arrive in the reference's additiv
 [B, 1, 1, L] (0 / -10000).
 """
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -61,16 +62,24 @@ def _needs_grad(*ts):
 
 def _fused_weights(owner, mods):
     """Concatenated [W_1; W_2; ...] / [b_1; ...] of several nn.Linear (one wide MFMA GEMM instead of
-    several narrow ones), cached until any of the parameters changes (data_ptr or in-place version)."""
+    several narrow ones), cached until any of the parameters changes (data_ptr or in-place version).
+    Stream-safe: a use on another stream than the one that built the cache waits for the build."""
     params = [t for m in mods for t in (m.weight, m.bias)]
     key = tuple((t.data_ptr(), t._version) for t in params)
     cache = getattr(owner, "_fused_cache", None)
+    cur = torch.cuda.current_stream()
     if cache is None or cache[0] != key:
         with torch.no_grad():
             W = torch.cat([m.weight for m in mods], 0).contiguous()
             b = torch.cat([m.bias for m in mods], 0).contiguous()
-        cache = (key, W, b)
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        cache = (key, W, b, ev, cur)
         owner._fused_cache = cache
+    elif cur != cache[4]:
+        cur.wait_event(cache[3])
+        cache[1].record_stream(cur)
+        cache[2].record_stream(cur)
     return cache[1], cache[2]
 
 
@@ -244,6 +253,18 @@ class BertXAttention(nn.Module):
         return self.output(self.att(input_tensor, ctx_tensor, ctx_att_mask), input_tensor)
 
 
+_TWO_STREAMS = os.environ.get("DASA_LXRT_STREAMS", "1") != "0"
+_SIDE = {}
+
+
+def _side_stream(device):
+    st = _SIDE.get(device.index)
+    if st is None:
+        st = torch.cuda.Stream(device=device)
+        _SIDE[device.index] = st
+    return st
+
+
 class LXRTXLayer(nn.Module):
     """vilmodel.py:1014-1064: cross attention (ONE shared visual_attention for both directions),
     then self attention and FFN on each stream."""
@@ -272,9 +293,27 @@ class LXRTXLayer(nn.Module):
         return lang, visn
 
     def forward(self, lang_feats, lang_attention_mask, visn_feats, visn_attention_mask):
-        la, va = self.cross_att(lang_feats, lang_attention_mask, visn_feats, visn_attention_mask)
-        la, va = self.self_att(la, lang_attention_mask, va, visn_attention_mask)
-        return self.output_fc(la[0], va[0])
+        if torch.is_grad_enabled() or not _TWO_STREAMS:
+            la, va = self.cross_att(lang_feats, lang_attention_mask, visn_feats, visn_attention_mask)
+            la, va = self.self_att(la, lang_attention_mask, va, visn_attention_mask)
+            return self.output_fc(la[0], va[0])
+        # No autograd (the detached train config and eval): after the cross attention reads both
+        # inputs, the language and vision streams are independent, so the vision branch (36 rows per
+        # sample) runs on a second HIP stream beside the language branch (80 rows): the two streams'
+        # GEMM/attention grids share the CUs instead of each leaving part of the chip idle.
+        main = torch.cuda.current_stream()
+        side = _side_stream(lang_feats.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            va = self.visual_attention(visn_feats, lang_feats, ctx_att_mask=lang_attention_mask)
+            va = self.visn_self_att(va, visn_attention_mask)[0]
+            visn = self.visn_output(self.visn_inter(va), va)
+        la = self.visual_attention(lang_feats, visn_feats, ctx_att_mask=visn_attention_mask)
+        la = self.lang_self_att(la, lang_attention_mask)[0]
+        lang = self.lang_output(self.lang_inter(la), la)
+        main.wait_stream(side)
+        visn.record_stream(main)
+        return lang, visn
 
 
 class VisionEncoder(nn.Module):
