@@ -46,6 +46,8 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--no-profile", action="store_true")
     p.add_argument("--shapes", type=int, default=0, help="add the top-N GEMM shapes by device time")
+    p.add_argument("--fast-exit", action="store_true",
+                   help="os._exit after the JSON line (skips interpreter teardown; used under rocprofv3)")
     p.add_argument("--backend", default="nccl", help="nccl (= RCCL on ROCm) | gloo (rehearsal only)")
     p.add_argument("--same-device", action="store_true",
                    help="map every rank to cuda:0 (rehearsing the DP path on a one-GPU box with gloo)")
@@ -203,6 +205,10 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if a.fast_exit:
+        torch.cuda.synchronize()
+        sys.stdout.flush()
+        os._exit(0)
 
 
 if __name__ == "__main__":

@@ -29,8 +29,9 @@ tail -1 gpurun_out/bench_$TAG.log
 if [ "${PROF:-1}" = "1" ]; then
   cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
   step prof 600 gpurun_out/profrun_$TAG.log rocprofv3 --kernel-trace --stats --output-format csv \
-    -d gpurun_out/prof_$TAG -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-fwd
+    -d gpurun_out/prof_$TAG -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-fwd --fast-exit
   # keep only the summaries (the full kernel trace is far larger than gpurun's copy-back limit)
   find gpurun_out/prof_$TAG \( -name "*kernel_trace*" -o -name "*.db" \) -delete 2>/dev/null
   find gpurun_out/prof_$TAG -type f
+  python tools/prof_compare.py gpurun_out/prof_$TAG/run_kernel_stats.csv gpurun_out/profrun_$TAG.log | head -20
 fi
