@@ -12,8 +12,9 @@
 // barriers, ONE lane adds to the direction's arrival counter (agent-scope atomic), then polls it with
 // sc1 loads (bounded by a wall-clock limit that sets a timeout word instead of hanging); the other
 // waves join at a workgroup barrier and read the state with sc1 loads only.
-// Residency: one 1024-thread workgroup per CU, 2*H/8 <= 256 workgroups, launched cooperatively so
-// the runtime rejects a grid that could not be co-resident (the caller then uses the step kernels).
+// Residency: one 1024-thread workgroup per CU, 2*H/8 <= 256 workgroups; the grid is checked against
+// the occupancy query once (the caller uses the step kernels if it would not be co-resident). The
+// callers run nothing concurrently with it (the encoder's side stream is joined before the LSTM).
 #include "common.h"
 #include "lstm_internal.h"
 
@@ -279,6 +280,31 @@ __global__ __launch_bounds__(1024) void bilstm_persist_bwd_kernel(PBwd a) {
 
 }  // namespace
 
+// Residency check done once per kernel: the grid (one 1024-thread workgroup per CU) must fit the
+// device in one wave of workgroups. Launched as plain kernels: a cooperative launch adds only this
+// same check (plus ~15 us of host time per launch) and its teardown crashes rocprofv3 on exit.
+template <typename K>
+bool resident(K kernel, int grid) {
+  static int cached = -1;   // per kernel instantiation
+  if (cached < 0) {
+    int dev = 0, cus = 0, per_cu = 0;
+    cached = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 1024, 0) == hipSuccess)
+      cached = (per_cu >= 1 && (long)per_cu * cus >= grid) ? 1 : 0;
+    (void)hipGetLastError();
+  }
+  return cached == 1;
+}
+
+template <typename K, typename A>
+int launch_persistent(K kernel, int grid, const A& a, hipStream_t st) {
+  if (!resident(kernel, grid)) return (int)hipErrorCooperativeLaunchTooLarge;
+  hipLaunchKernelGGL(kernel, dim3(grid), dim3(1024), 0, st, a);
+  return (int)hipGetLastError();
+}
+
 bool bilstm_persist_ok(int B, int H) {
   return B >= 1 && B <= 32 && H % 256 == 0 && H >= 256 && H <= 1024;
 }
@@ -287,34 +313,26 @@ int bilstm_persist_fwd(const float* xproj, const float* whh_fwd, const float* wh
                        float* out, float* h_n, float* c_n, float* save_act, float* save_c, int B, int L, int H,
                        float* hbuf, unsigned* sync, hipStream_t st) {
   PFwd a{xproj, whh_fwd, whh_bwd, lengths, out, save_act, save_c, h_n, c_n, hbuf, sync, B, L, H};
-  void* args[] = {&a};
-  const dim3 grid(2 * H / PU), block(1024);
-  hipError_t e;
+  const int grid = 2 * H / PU;
   switch (H / 128) {
-    case 2: e = hipLaunchCooperativeKernel((const void*)bilstm_persist_fwd_kernel<2>, grid, block, args, 0, st); break;
-    case 4: e = hipLaunchCooperativeKernel((const void*)bilstm_persist_fwd_kernel<4>, grid, block, args, 0, st); break;
-    case 6: e = hipLaunchCooperativeKernel((const void*)bilstm_persist_fwd_kernel<6>, grid, block, args, 0, st); break;
-    case 8: e = hipLaunchCooperativeKernel((const void*)bilstm_persist_fwd_kernel<8>, grid, block, args, 0, st); break;
+    case 2: return launch_persistent(bilstm_persist_fwd_kernel<2>, grid, a, st);
+    case 4: return launch_persistent(bilstm_persist_fwd_kernel<4>, grid, a, st);
+    case 6: return launch_persistent(bilstm_persist_fwd_kernel<6>, grid, a, st);
+    case 8: return launch_persistent(bilstm_persist_fwd_kernel<8>, grid, a, st);
     default: return (int)hipErrorInvalidValue;
   }
-  if (e != hipSuccess) (void)hipGetLastError();
-  return (int)e;
 }
 
 int bilstm_persist_bwd(const float* whh_fwd, const float* whh_bwd, const int32_t* lengths, const float* save_act,
                        const float* save_c, const float* dout, const float* dh_n, const float* dc_n, float* dgates,
                        int B, int L, int H, unsigned* sync, hipStream_t st) {
   PBwd a{whh_fwd, whh_bwd, lengths, save_act, save_c, dout, dh_n, dc_n, dgates, sync, B, L, H};
-  void* args[] = {&a};
-  const dim3 grid(2 * H / PU), block(1024);
-  hipError_t e;
+  const int grid = 2 * H / PU;
   switch (H / 64) {   // NGB = 4H / 256
-    case 4: e = hipLaunchCooperativeKernel((const void*)bilstm_persist_bwd_kernel<4>, grid, block, args, 0, st); break;
-    case 8: e = hipLaunchCooperativeKernel((const void*)bilstm_persist_bwd_kernel<8>, grid, block, args, 0, st); break;
-    case 12: e = hipLaunchCooperativeKernel((const void*)bilstm_persist_bwd_kernel<12>, grid, block, args, 0, st); break;
-    case 16: e = hipLaunchCooperativeKernel((const void*)bilstm_persist_bwd_kernel<16>, grid, block, args, 0, st); break;
+    case 4: return launch_persistent(bilstm_persist_bwd_kernel<4>, grid, a, st);
+    case 8: return launch_persistent(bilstm_persist_bwd_kernel<8>, grid, a, st);
+    case 12: return launch_persistent(bilstm_persist_bwd_kernel<12>, grid, a, st);
+    case 16: return launch_persistent(bilstm_persist_bwd_kernel<16>, grid, a, st);
     default: return (int)hipErrorInvalidValue;
   }
-  if (e != hipSuccess) (void)hipGetLastError();
-  return (int)e;
 }

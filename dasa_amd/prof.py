@@ -63,12 +63,15 @@ class _Recorder:
             kernels[name] = ent
         dom_name = max(fam.items(), key=lambda kv: kv[1]["ms"])[0]
         d = kernels[dom_name]
+        nl = fam[dom_name]["launches"]
         roof = {"kernel": dom_name, "bound": d["bound"], "achieved": d["achieved"], "peak": d["peak"],
                 "unit": d["unit"], "frac": d["frac"], "traffic": None,
-                "per_launch": {"avg_us": d["avg_launch_us"],
-                               "alg_" + ("flops" if d["bound"] == "mfma" else "bytes"):
-                                   (fam[dom_name]["flops"] if d["bound"] == "mfma" else fam[dom_name]["bytes"])
-                                   / fam[dom_name]["launches"]}}
+                "per_launch": {"avg_us": d["avg_launch_us"], "alg_flops": fam[dom_name]["flops"] / nl,
+                               "alg_bytes": fam[dom_name]["bytes"] / nl}}
+        pmc = _pmc_traffic()
+        if pmc is not None and dom_name in pmc["families"]:
+            roof["traffic"] = pmc["families"][dom_name]["hbm_bytes_per_launch"]
+            roof["traffic_source"] = pmc["file"] + ": " + pmc["source"]
         out = {"roofline": roof, "kernels": kernels, "profiled_device_ms": round(total, 2)}
         if self.want_shapes:
             top = sorted(shapes.items(), key=lambda kv: -kv[1][1])[:self.want_shapes]
@@ -76,6 +79,20 @@ class _Recorder:
                               "TFLOPs": round(v[2] / (v[1] / 1e3) / 1e12, 1) if v[1] > 0 else 0.0}
                              for k, v in top]
         return out
+
+
+def _pmc_traffic():
+    """Per-launch HBM bytes per kernel family from the committed rocprofv3 PMC passes
+    (tools/pmc_traffic.py -> profiles/pmc_traffic.json), or None."""
+    import json
+    import os
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    d["file"] = "profiles/pmc_traffic.json"
+    return d
 
 
 def active():

@@ -143,7 +143,7 @@ int dasa_bilstm_bwd(const float* whh_fwd, const float* whh_bwd, const int32_t* l
                     int32_t B, int32_t L, int32_t H, float* ws, void* stream);
 /* hprev [2][B][L][H]: the recurrent input each step saw (fwd: out[b][t-1][:H], bwd: out[b][t+1][H:]),
  * zero at the sequence ends — the right operand of dW_hh = sum_t dgates_t^T hprev_t.            */
-/* Recurrence implementation for dasa_bilstm_fwd/bwd: 0 = automatic (one persistent cooperative launch
+/* Recurrence implementation for dasa_bilstm_fwd/bwd: 0 = automatic (one persistent launch
  * per sequence when B <= 32 and H is a multiple of 256 up to 1024, else one launch per timestep),
  * 1 = per-timestep launches only, 2 = persistent only (error when not eligible). Host-only setting. */
 int dasa_bilstm_set_mode(int mode);
