@@ -45,6 +45,8 @@ def parse():
     p.add_argument("--no-fwd", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--no-profile", action="store_true")
+    p.add_argument("--no-kbench", action="store_true",
+                   help="skip the isolated HBM-kernel table (dasa_amd.kbench at B=20 and B=256)")
     p.add_argument("--shapes", type=int, default=0, help="add the top-N GEMM shapes by device time")
     p.add_argument("--fast-exit", action="store_true",
                    help="os._exit after the JSON line (skips interpreter teardown; used under rocprofv3)")
@@ -198,6 +200,11 @@ def main():
         summ = kernel_profile(agent, lambda: train_step(agent), a.shapes)
         if rank == 0:
             out.update(summ)
+    if rank == 0 and world == 1 and not a.no_kbench:
+        from dasa_amd import kbench
+        out["hbm_kernels"] = kbench.hbm_kernels((a.batch, 256))
+        out["hbm_kernels_note"] = ("AdaIN gate / mu-sigma and attention kernels in isolation, graph-replayed back to back "
+                                   "(no host gaps); B=256 is BASELINE configs[4]'s batch; algorithmic bytes / time vs 8 TB/s")
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a)
     if rank == 0:

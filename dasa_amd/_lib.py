@@ -49,7 +49,8 @@ SIGNATURES = {
     "dasa_mha_fwd": (i32, [vp, i64, vp, i64, vp, i64, vp, vp, i64, vp, i32, i32, i32, i32, i32, f32, f32, u64, vp]),
     "dasa_mha_bwd": (i32, [vp, i64, vp, i64, vp, i64, vp, vp, i64, vp, vp, vp, i32, i32, i32, i32, i32, f32, f32, u64,
                            vp]),
-    "dasa_softdot_fwd": (i32, [vp, vp, i64, vp, vp, vp, vp, i32, i32, i32, vp]),
+    "dasa_softdot_fwd": (i32, [vp, vp, i64, vp, vp, vp, vp, i32, i32, i32, vp, vp]),
+    "dasa_attn_workspace": (i64, [i32, i32, i32]),
     "dasa_softdot_bwd": (i32, [vp, vp, i64, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp, vp]),
     "dasa_shift_attn_fwd": (i32, [vp, vp, i64, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp]),
     "dasa_shift_attn_bwd": (i32, [vp, vp, i64, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp, vp]),

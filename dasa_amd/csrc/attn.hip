@@ -1,12 +1,24 @@
 // SoftDotAttention / ShiftSoftDotAttention forward + backward for gfx950 (model.py:253-353).
 //
-// Both are HBM-bound: one pass over ctx [B][N][D] for the scores and one for the weighted sum
-// (the second mostly L2/MALL-served). Kernel split:
-//   scores_kernel : one wave per (b, n) row, float4 coalesced dot over D, wave-shuffle reduction.
-//   apply_kernel  : grid (B, D/256); each block recomputes the tiny N-wide softmax (+ the 3x12
-//                   circular shift for the panorama) in LDS, then its 4 waves split the N rows of a
-//                   256-column slab (float4 per lane) and reduce across waves through LDS.
-// The backward reuses scores_kernel for dp = ctx.dwctx and fuses dq and dctx in one slab pass.
+// HBM-bound: the compulsory traffic is one read of ctx [B][N][D] (+ one write of dctx in backward).
+// At the policy's shapes a call moves 3-13 MB, so the kernels are built for latency: every
+// workgroup issues all of its loads in ONE round trip and there is no grid-wide wait.
+//
+// Row-split layout: workgroup (j, b) owns rows [j*RB, j*RB + RB) of batch row b (RB = 12 for the
+// panorama: one elevation ring of 12 headings, so the K-tap circular shift stays inside the
+// workgroup; RB = 16 otherwise) and thread t owns float4 column t of those rows (D = 2176 -> 576
+// threads, 2048 -> 512), holding the RB float4 in registers for both passes over them.
+//   forward   scores of its rows (4-wide partial dots, reduce-scattered over the wave with 17
+//             shuffles, wave partials meet in LDS), a LOCAL softmax (max m_j, sum l_j, e_r =
+//             exp(s_r - m_j)), the shift of e within the ring, and the partial context
+//             sum_r e'_r ctx_r; the last workgroup of b to finish (arrival counter, release/acquire
+//             write-through stores, nothing ever waits) rescales the partials by exp(m_j - M) / Z and writes
+//             wctx, probs and the shifted weights (the online-softmax merge).
+//   backward  launch 1: dp_r = ctx_r . dwctx per row block; the last arriver forms the softmax /
+//             shift backward for all N rows (ds, the weights pw, dshift). Launch 2: dctx rows and a
+//             partial dq per row block; the last arriver sums the dq partials.
+// Workspace: dasa_attn_workspace(); its first 2 x 32768 words are arrival counters that must be zero
+// on entry and are left zero.
 #include "common.h"
 #include "../../include/dasa_hip.h"
 
@@ -14,131 +26,235 @@ namespace {
 
 constexpr int kMaxN = 256;   // max attended rows (instruction <= 80, views 36, candidates)
 constexpr int kMaxK = 15;    // max shift taps
+constexpr int kMaxW = 16;    // waves per workgroup (1024 threads)
+constexpr int kMaxBlk = kMaxN / 12 + 1;
 
-// scores[b][n] = sum_d ctx[b][n][d] * q[b][d]; one wave per row.
-__global__ __launch_bounds__(256) void scores_kernel(const float* __restrict__ q, long ldq,
-                                                     const float* __restrict__ ctx, long ldn,
-                                                     float* __restrict__ out, int B, int N, int D) {
-  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (wave >= B * N) return;
-  const int b = wave / N, n = wave % N;
-  const float4* c4 = reinterpret_cast<const float4*>(ctx + ((long)b * N + n) * ldn);
-  const float4* q4 = reinterpret_cast<const float4*>(q + (long)b * ldq);
-  float s = 0.f;
-  const int D4 = D >> 2;
-  for (int i = lane; i < D4; i += 64) {
-    const float4 c = c4[i], v = q4[i];
-    s = fmaf(c.x, v.x, s);
-    s = fmaf(c.y, v.y, s);
-    s = fmaf(c.z, v.z, s);
-    s = fmaf(c.w, v.w, s);
-  }
-  s = wave_sum(s);
-  if (lane == 0) out[(long)b * N + n] = s;
+__device__ __forceinline__ float dot4(const float4 a, const float4 b) {
+  return fmaf(a.x, b.x, fmaf(a.y, b.y, fmaf(a.z, b.z, a.w * b.w)));
 }
 
-// Softmax over n of scores[b][:N] with optional mask (-inf), written to sp[0..N).
-// Called by all 256 threads of the block; wave 0 does the work.
-__device__ void block_softmax(const float* sc, const uint8_t* mask, int N, float* sp) {
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    float m = -INFINITY;
-    for (int n = lane; n < N; n += 64) {
-      float v = sc[n];
-      if (mask && mask[n]) v = -INFINITY;
-      sp[n] = v;
-      m = fmaxf(m, v);
-    }
-    m = wave_max(m);
-    float s = 0.f;
-    for (int n = lane; n < N; n += 64) {
-      const float e = (sp[n] == -INFINITY) ? 0.f : __expf(sp[n] - m);
-      sp[n] = e;
-      s += e;
-    }
-    s = wave_sum(s);
-    const float inv = 1.f / s;
-    for (int n = lane; n < N; n += 64) sp[n] *= inv;
-  }
+__device__ __forceinline__ void fma4(float s, const float4 x, float4& acc) {
+  acc.x = fmaf(s, x.x, acc.x);
+  acc.y = fmaf(s, x.y, acc.y);
+  acc.z = fmaf(s, x.z, acc.z);
+  acc.w = fmaf(s, x.w, acc.w);
 }
 
-// 3 elevation rows x 12 headings circular correlation (model.py:337-344).
-__device__ __forceinline__ float shift_at(const float* a, const float* w, int K, int v) {
-  const int r = v / 12, j = v % 12, p = K / 2;
-  float s = 0.f;
-  for (int k = 0; k < K; ++k) {
-    int jj = j + k - p;
-    jj = ((jj % 12) + 12) % 12;
-    s = fmaf(w[k], a[r * 12 + jj], s);
+// Reduce-scatter of 16 per-lane partials over the 64-lane wave: returns on every lane the full-wave
+// sum of partial (lane >> 2) & 15. Exchange on lane bits 5..2 halves the live values each step
+// (8 + 4 + 2 + 1 shuffles), then bits 1..0 finish the sum (2 more).
+__device__ __forceinline__ float reduce_scatter16(const float (&v)[16], int lane) {
+  float u[8], w4[4], w2[2];
+  {
+    const bool up = lane & 32;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float send = up ? v[i] : v[i + 8], keep = up ? v[i + 8] : v[i];
+      u[i] = keep + __shfl_xor(send, 32, 64);
+    }
   }
+  {
+    const bool up = lane & 16;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float send = up ? u[i] : u[i + 4], keep = up ? u[i + 4] : u[i];
+      w4[i] = keep + __shfl_xor(send, 16, 64);
+    }
+  }
+  {
+    const bool up = lane & 8;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float send = up ? w4[i] : w4[i + 2], keep = up ? w4[i + 2] : w4[i];
+      w2[i] = keep + __shfl_xor(send, 8, 64);
+    }
+  }
+  const bool up = lane & 4;
+  float s = (up ? w2[1] : w2[0]) + __shfl_xor(up ? w2[0] : w2[1], 4, 64);
+  s += __shfl_xor(s, 2, 64);
+  s += __shfl_xor(s, 1, 64);
   return s;
 }
 
-struct ApplyArgs {
+// Partials handed to another workgroup of the same launch are stored write-through (sc1) and every
+// load of them is sc1, so the hand-off needs no L2-wide release / acquire fence (gfx950's L2 is
+// per XCD): writers drain vmcnt, then one lane takes a relaxed agent-scope ticket.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ws_rsrc(float* ws) {
+  return __builtin_amdgcn_make_buffer_rsrc(ws, 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void pub1(__amdgpu_buffer_rsrc_t r, int off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 16);
+}
+__device__ __forceinline__ void pub4(__amdgpu_buffer_rsrc_t r, int off, float4 v) {
+  const u32x4 u = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+  __builtin_amdgcn_raw_buffer_store_b128(u, r, off, 0, 16);
+}
+__device__ __forceinline__ float get1(__amdgpu_buffer_rsrc_t r, int off) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 16));
+}
+__device__ __forceinline__ float4 get4(__amdgpu_buffer_rsrc_t r, int off) {
+  const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
+  return make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
+}
+
+__device__ __forceinline__ void lds_wave_sync() {
+  __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes have landed
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Row dots of the workgroup's rows with vec, summed over the workgroup: returns on lane r < nr of
+// wave 0 (valid after the internal __syncthreads) the dot of row r; thread t < D/4 keeps its float4
+// of each row in x (D <= 4096, so one column per thread).
+template <int RB>
+__device__ __forceinline__ float block_row_dots(const float* rows, long ldn, int nr, const float* vec, int D4,
+                                                float4 (&x)[RB], float (*red)[16]) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, W = blockDim.x >> 6;
+  float v[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = 0.f;
+  if (t < D4) {   // D4 <= blockDim: one float4 column per thread
+    const float4 qv = reinterpret_cast<const float4*>(vec)[t];
+#pragma unroll
+    for (int i = 0; i < RB; ++i) x[i] = reinterpret_cast<const float4*>(rows + (long)min(i, nr - 1) * ldn)[t];
+#pragma unroll
+    for (int i = 0; i < RB; ++i) v[i] = dot4(x[i], qv);
+  }
+  const float s = reduce_scatter16(v, lane);
+  const int r = (lane >> 2) & 15;
+  if ((lane & 3) == 0 && r < RB) red[w][r] = s;
+  __syncthreads();
+  float tot = 0.f;
+  if (t < 64 && lane < nr)
+    for (int i = 0; i < W; ++i) tot += red[i][lane];
+  return tot;
+}
+
+// Announce this workgroup's (sc1-stored) partials for batch row b; true in exactly one workgroup,
+// the last to arrive, which then reads every partial with sc1 loads.
+__device__ __forceinline__ bool last_arriver(unsigned* cnt, int nblk, int* s_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave: its write-through stores landed
+  __syncthreads();
+  if (threadIdx.x == 0)
+    *s_flag = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(nblk - 1);
+  __syncthreads();
+  if (!*s_flag) return false;
+  if (threadIdx.x == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // re-arm
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler-only: keep the sc1 loads below the ticket
+  return true;
+}
+
+// Softmax weights over K shift taps (model.py:336) into sw[0..K), computed by wave 0.
+__device__ __forceinline__ void shift_taps(const float* logits, int K, float* sw, int lane) {
+  const float z = lane < K ? logits[lane] : -INFINITY;
+  const float zm = wave_max(z);
+  const float e = lane < K ? __expf(z - zm) : 0.f;
+  const float es = wave_sum(e);
+  if (lane < K) sw[lane] = e / es;
+}
+
+struct FwdArgs {
   const float* q; const float* ctx; long ldn;
-  const float* scores; const uint8_t* mask;
+  const uint8_t* mask;
   const float* shift_logits; int K;
-  float* probs; float* shifted; float* wsm; float* wctx;
-  int B, N, D;
+  float* scores; float* probs; float* shifted; float* wsm; float* wctx;
+  int N, D, nblk;
+  unsigned* cnt; float* ws; int o_part, o_ml, o_ee;   // workspace: counters + byte offsets of partials
 };
 
-// Forward slab kernel: softmax (+shift) then wctx[b][slab] = sum_n p'[n] ctx[b][n][slab].
-__global__ __launch_bounds__(256) void apply_fwd_kernel(ApplyArgs a) {
-  __shared__ float sp[kMaxN];
-  __shared__ float sw[kMaxK];
-  __shared__ float sa2[kMaxN];
-  __shared__ float4 red[4][64];
-  const int b = blockIdx.x;
-  const int N = a.N;
-  block_softmax(a.scores + (long)b * N, a.mask ? a.mask + (long)b * N : nullptr, N, sp);
+template <int RB>
+__global__ __launch_bounds__(1024) void attn_fwd_kernel(FwdArgs a) {
+  __shared__ float red[kMaxW][16];
+  __shared__ float se[16], sep[16], sw[kMaxK + 1], ssc[kMaxBlk];
+  __shared__ int s_flag;
+  const int j = blockIdx.x, b = blockIdx.y, t = threadIdx.x, lane = t & 63;
+  const int N = a.N, D4 = a.D >> 2, r0 = j * RB, nr = min(RB, N - r0), nblk = a.nblk;
+  const bool shift = a.shift_logits != nullptr;
+  const float* rows = a.ctx + ((long)b * N + r0) * a.ldn;
+  float4 x[RB];
+  const float s = block_row_dots<RB>(rows, a.ldn, nr, a.q + (long)b * a.D, D4, x, red);
+  const bool combine = a.wctx || a.probs || a.shifted;
+  const __amdgpu_buffer_rsrc_t wr = ws_rsrc(a.ws);
+  if (t < 64) {
+    float sm = -INFINITY;
+    if (lane < nr) {
+      if (a.scores) a.scores[(long)b * N + r0 + lane] = s;
+      sm = (a.mask && a.mask[(long)b * N + r0 + lane]) ? -INFINITY : s;
+    }
+    const float m = wave_max(sm);
+    const float e = (sm == -INFINITY) ? 0.f : __expf(sm - m);
+    const float l = wave_sum(e);
+    if (lane < 16) se[lane] = e;
+    if (shift) shift_taps(a.shift_logits + (long)b * a.K, a.K, sw, lane);
+    lds_wave_sync();
+    float ep = e;
+    if (shift && lane < nr) {   // RB = 12: this workgroup is one elevation ring (model.py:337-344)
+      const int P = a.K / 2;
+      ep = 0.f;
+      for (int k = 0; k < a.K; ++k) {
+        int jj = lane + k - P;
+        jj = ((jj % 12) + 12) % 12;
+        ep = fmaf(sw[k], se[jj], ep);
+      }
+    }
+    if (lane < 16) sep[lane] = lane < nr ? ep : 0.f;
+    if (combine && nblk > 1) {
+      if (lane < nr) {
+        pub1(wr, a.o_ee + ((b * N + r0 + lane) * 2) * 4, e);
+        pub1(wr, a.o_ee + ((b * N + r0 + lane) * 2 + 1) * 4, ep);
+      }
+      if (lane == 0) {
+        pub1(wr, a.o_ml + ((b * nblk + j) * 2) * 4, m);
+        pub1(wr, a.o_ml + ((b * nblk + j) * 2 + 1) * 4, l);
+      }
+    } else if (combine) {   // single workgroup: normalise here
+      const float inv = 1.f / l;
+      if (lane < nr) {
+        if (a.probs) a.probs[(long)b * N + lane] = e * inv;
+        if (a.shifted) a.shifted[(long)b * N + lane] = ep * inv;
+      }
+      if (shift && a.wsm && lane < a.K) a.wsm[(long)b * a.K + lane] = sw[lane];
+      if (lane == 0) ssc[0] = inv;
+    }
+  }
   __syncthreads();
-  const float* pw = sp;
-  if (a.shift_logits) {
-    if (threadIdx.x < 64) {
-      const int lane = threadIdx.x;
-      float z = lane < a.K ? a.shift_logits[(long)b * a.K + lane] : -INFINITY;
-      const float m = wave_max(z);
-      const float e = lane < a.K ? __expf(z - m) : 0.f;
-      const float s = wave_sum(e);
-      if (lane < a.K) sw[lane] = e / s;
-    }
-    __syncthreads();
-    for (int v = threadIdx.x; v < N; v += 256) sa2[v] = shift_at(sp, sw, a.K, v);
-    __syncthreads();
-    pw = sa2;
-  }
-  if (blockIdx.y == 0) {
-    for (int n = threadIdx.x; n < N; n += 256) {
-      if (a.probs) a.probs[(long)b * N + n] = sp[n];
-      if (a.shifted && a.shift_logits) a.shifted[(long)b * N + n] = sa2[n];
-    }
-    if (a.wsm && a.shift_logits && threadIdx.x < a.K) a.wsm[(long)b * a.K + threadIdx.x] = sw[threadIdx.x];
-  }
-  if (!a.wctx) return;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int d4 = blockIdx.y * 64 + lane;  // float4 index within the row
-  const int D4 = a.D >> 2;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (d4 < D4) {
-    const float* base = a.ctx + (long)b * N * a.ldn;
-    for (int n = w; n < N; n += 4) {
-      const float pn = pw[n];
-      const float4 c = reinterpret_cast<const float4*>(base + (long)n * a.ldn)[d4];
-      acc.x = fmaf(pn, c.x, acc.x);
-      acc.y = fmaf(pn, c.y, acc.y);
-      acc.z = fmaf(pn, c.z, acc.z);
-      acc.w = fmaf(pn, c.w, acc.w);
-    }
-  }
-  red[w][lane] = acc;
-  __syncthreads();
-  if (w == 0 && d4 < D4) {
-    float4 s = red[0][lane];
+  if (!combine) return;
+  if (a.wctx && t < D4) {   // partial (or, with one workgroup, final) context from the rows in VGPRs
+    const float sc = nblk == 1 ? ssc[0] : 1.f;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int i = 1; i < 4; ++i) {
-      s.x += red[i][lane].x; s.y += red[i][lane].y; s.z += red[i][lane].z; s.w += red[i][lane].w;
+    for (int i = 0; i < RB; ++i) fma4(i < nr ? sep[i] * sc : 0.f, x[i], acc);
+    if (nblk == 1) reinterpret_cast<float4*>(a.wctx + (long)b * a.D)[t] = acc;
+    else pub4(wr, a.o_part + (((b * nblk + j) * a.D) + 4 * t) * 4, acc);
+  }
+  if (nblk == 1) return;
+  if (!last_arriver(a.cnt + b, nblk, &s_flag)) return;
+  // merge: M = max_j m_j, Z = sum_j exp(m_j - M) l_j; weight of block j = exp(m_j - M) / Z
+  if (t < 64) {
+    const int ob = a.o_ml + (b * nblk * 2) * 4;
+    const float mj = lane < nblk ? get1(wr, ob + (2 * lane) * 4) : -INFINITY;
+    const float lj = lane < nblk ? get1(wr, ob + (2 * lane + 1) * 4) : 0.f;
+    const float M = wave_max(mj);
+    const float sj = lane < nblk ? __expf(mj - M) : 0.f;
+    const float Z = wave_sum(sj * lj);
+    if (lane < nblk) ssc[lane] = sj / Z;
+    if (shift) {
+      shift_taps(a.shift_logits + (long)b * a.K, a.K, sw, lane);
+      if (a.wsm && lane < a.K) a.wsm[(long)b * a.K + lane] = sw[lane];
     }
-    reinterpret_cast<float4*>(a.wctx + (long)b * a.D)[d4] = s;
+  }
+  __syncthreads();
+  for (int n = t; n < N; n += blockDim.x) {
+    const float sc = ssc[n / RB];
+    const int en = a.o_ee + ((b * N + n) * 2) * 4;
+    if (a.probs) a.probs[(long)b * N + n] = get1(wr, en) * sc;
+    if (a.shifted) a.shifted[(long)b * N + n] = get1(wr, en + 4) * sc;
+  }
+  if (a.wctx && t < D4) {
+    const int pb = a.o_part + (b * nblk * a.D + 4 * t) * 4;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = 0; i < nblk; ++i) fma4(ssc[i], get4(wr, pb + i * a.D * 4), acc);
+    reinterpret_cast<float4*>(a.wctx + (long)b * a.D)[t] = acc;
   }
 }
 
@@ -148,141 +264,222 @@ struct BwdArgs {
   const float* shifted;   // a' [B][N] (shift only)
   const float* wsm;       // w [B][K] (shift only)
   int K;
-  const float* dp;        // ctx.dwctx [B][N] or NULL
   const float* dwctx;     // [B][D] or NULL
   const float* dscores;   // [B][N] or NULL
   float* dq; float* dctx; int accumulate;
   float* dshift;          // [B][K] (shift only)
-  int B, N, D;
+  int N, D, nblk;
+  unsigned* cnt1; unsigned* cnt2; float* ds; float* pw;   // workspace (ds / pw: read by the next launch)
+  float* ws; int o_dp, o_part;                            // byte offsets of the in-launch partials
 };
 
-// Backward slab kernel: ds (softmax / shift backward, recomputed per block), then
-// dq[slab] = sum_n ds[n] ctx[n][slab]; dctx[n][slab] (+)= pw[n]*dwctx[slab] + ds[n]*q[slab].
-__global__ __launch_bounds__(256) void apply_bwd_kernel(BwdArgs a) {
-  __shared__ float sds[kMaxN];
-  __shared__ float spw[kMaxN];
-  __shared__ float sda[kMaxN];
-  __shared__ float sdw[kMaxK];
-  __shared__ float4 red[4][64];
-  const int b = blockIdx.x, N = a.N;
+// Launch 1: dp = ctx . dwctx per row block; the last arriver does the softmax / shift backward.
+template <int RB>
+__global__ __launch_bounds__(1024) void attn_bwd_dp_kernel(BwdArgs a) {
+  __shared__ float red[kMaxW][16];
+  __shared__ float sdp[kMaxN], sda[kMaxN];
+  __shared__ int s_flag;
+  const int j = blockIdx.x, b = blockIdx.y, t = threadIdx.x, lane = t & 63;
+  const int N = a.N, D4 = a.D >> 2, r0 = j * RB, nr = min(RB, N - r0);
+  const float* rows = a.ctx + ((long)b * N + r0) * a.ldn;
+  float4 x[RB];
+  const float s = block_row_dots<RB>(rows, a.ldn, nr, a.dwctx + (long)b * a.D, D4, x, red);
+  const __amdgpu_buffer_rsrc_t wr = ws_rsrc(a.ws);
+  if (t < 64 && lane < nr) pub1(wr, a.o_dp + (b * N + r0 + lane) * 4, s);
+  if (!last_arriver(a.cnt1 + b, a.nblk, &s_flag)) return;
+  if (t >= 64) return;
   const float* p = a.probs + (long)b * N;
-  const bool shift = a.wsm != nullptr;
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    // da = grad wrt the (pre-shift) softmax output
-    if (shift) {
-      const float* w = a.wsm + (long)b * a.K;
-      const float* dap = a.dp + (long)b * N;  // grad wrt a'
-      const int P = a.K / 2;
-      for (int v = lane; v < N; v += 64) {
-        const int r = v / 12, i = v % 12;
-        float s = 0.f;
-        for (int k = 0; k < a.K; ++k) {
-          int j = i - k + P;
-          j = ((j % 12) + 12) % 12;
-          s = fmaf(w[k], dap[r * 12 + j], s);
-        }
-        sda[v] = s;
-        spw[v] = a.shifted[(long)b * N + v];
-      }
-      // dw[k] = sum_{r,j} da'[r][j] * a[r][(j+k-P) mod 12]; softmax backward over K taps.
-      float dwk = 0.f;
-      if (lane < a.K) {
-        for (int v = 0; v < N; ++v) {
-          const int r = v / 12, j = v % 12;
-          int jj = j + lane - P;
-          jj = ((jj % 12) + 12) % 12;
-          dwk = fmaf(dap[v], p[r * 12 + jj], dwk);
-        }
-      }
-      const float wk = lane < a.K ? w[lane] : 0.f;
-      const float dot = wave_sum(wk * dwk);
-      if (lane < a.K) {
-        sdw[lane] = wk * (dwk - dot);
-        a.dshift[(long)b * a.K + lane] = sdw[lane];
-      }
-    } else {
-      for (int v = lane; v < N; v += 64) {
-        sda[v] = a.dp ? a.dp[(long)b * N + v] : 0.f;
-        spw[v] = p[v];
-      }
-    }
-    float dot = 0.f;
-    for (int v = lane; v < N; v += 64) dot = fmaf(p[v], sda[v], dot);
-    dot = wave_sum(dot);
+  for (int n = lane; n < N; n += 64) sdp[n] = get1(wr, a.o_dp + (b * N + n) * 4);
+  lds_wave_sync();
+  if (a.wsm) {
+    // da[v] = sum_k w_k dp'[r][(i - k + P) mod 12] (transpose of the forward correlation);
+    // dw[k] = sum_v dp'[v] a[r][(j + k - P) mod 12]; softmax backward over the K taps.
+    const float* w = a.wsm + (long)b * a.K;
+    const int P = a.K / 2;
     for (int v = lane; v < N; v += 64) {
-      float ds = p[v] * (sda[v] - dot);
-      if (a.dscores) ds += a.dscores[(long)b * N + v];
-      sds[v] = ds;
+      const int r = v / 12, i = v % 12;
+      float acc = 0.f;
+      for (int k = 0; k < a.K; ++k) {
+        int jj = i - k + P;
+        jj = ((jj % 12) + 12) % 12;
+        acc = fmaf(w[k], sdp[r * 12 + jj], acc);
+      }
+      sda[v] = acc;
+      a.pw[(long)b * N + v] = a.shifted[(long)b * N + v];
     }
-  }
-  __syncthreads();
-  (void)sdw;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int d4 = blockIdx.y * 64 + lane;
-  const int D4 = a.D >> 2;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (d4 < D4) {
-    const float* base = a.ctx + (long)b * N * a.ldn;
-    float* dbase = a.dctx ? a.dctx + (long)b * N * a.ldn : nullptr;
-    const float4 qv = reinterpret_cast<const float4*>(a.q + (long)b * a.D)[d4];
-    const float4 gv = a.dwctx ? reinterpret_cast<const float4*>(a.dwctx + (long)b * a.D)[d4]
-                              : make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int n = w; n < N; n += 4) {
-      const float ds = sds[n], pn = spw[n];
-      const float4 c = reinterpret_cast<const float4*>(base + (long)n * a.ldn)[d4];
-      acc.x = fmaf(ds, c.x, acc.x);
-      acc.y = fmaf(ds, c.y, acc.y);
-      acc.z = fmaf(ds, c.z, acc.z);
-      acc.w = fmaf(ds, c.w, acc.w);
-      if (dbase) {
-        float4* dp4 = reinterpret_cast<float4*>(dbase + (long)n * a.ldn) + d4;
-        float4 g;
-        g.x = pn * gv.x + ds * qv.x;
-        g.y = pn * gv.y + ds * qv.y;
-        g.z = pn * gv.z + ds * qv.z;
-        g.w = pn * gv.w + ds * qv.w;
-        if (a.accumulate) {
-          const float4 o = *dp4;
-          g.x += o.x; g.y += o.y; g.z += o.z; g.w += o.w;
-        }
-        *dp4 = g;
+    float dwk = 0.f;
+    if (lane < a.K) {
+      for (int v = 0; v < N; ++v) {
+        const int r = v / 12, jx = v % 12;
+        int jj = jx + lane - P;
+        jj = ((jj % 12) + 12) % 12;
+        dwk = fmaf(sdp[v], p[r * 12 + jj], dwk);
       }
     }
-  }
-  red[w][lane] = acc;
-  __syncthreads();
-  if (w == 0 && d4 < D4 && a.dq) {
-    float4 s = red[0][lane];
-#pragma unroll
-    for (int i = 1; i < 4; ++i) {
-      s.x += red[i][lane].x; s.y += red[i][lane].y; s.z += red[i][lane].z; s.w += red[i][lane].w;
+    const float wk = lane < a.K ? w[lane] : 0.f;
+    const float dot = wave_sum(wk * dwk);
+    if (lane < a.K) a.dshift[(long)b * a.K + lane] = wk * (dwk - dot);
+  } else {
+    for (int v = lane; v < N; v += 64) {
+      sda[v] = sdp[v];
+      a.pw[(long)b * N + v] = p[v];
     }
-    reinterpret_cast<float4*>(a.dq + (long)b * a.D)[d4] = s;
+  }
+  lds_wave_sync();
+  float dot = 0.f;
+  for (int v = lane; v < N; v += 64) dot = fmaf(p[v], sda[v], dot);
+  dot = wave_sum(dot);
+  for (int v = lane; v < N; v += 64) {
+    float g = p[v] * (sda[v] - dot);
+    if (a.dscores) g += a.dscores[(long)b * N + v];
+    a.ds[(long)b * N + v] = g;
+  }
+}
+
+// Launch 2: dctx rows (+)= pw dwctx + ds q and a partial dq = sum_r ds_r ctx_r per row block; the
+// last arriver sums the partials. ds / pw come from launch 1 (or ds = dscores, pw unused, when the
+// caller has no dwctx: the candidate-logit backward).
+template <int RB>
+__global__ __launch_bounds__(1024) void attn_bwd_apply_kernel(BwdArgs a) {
+  __shared__ float sds[16], spw[16];
+  __shared__ int s_flag;
+  const int j = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  const int N = a.N, D4 = a.D >> 2, r0 = j * RB, nr = min(RB, N - r0), nblk = a.nblk;
+  const float* rows = a.ctx + ((long)b * N + r0) * a.ldn;
+  const bool gdw = a.dwctx != nullptr;
+  if (t < RB) {
+    const int n = r0 + min(t, nr - 1);
+    const float* dsp = gdw ? a.ds : a.dscores;
+    sds[t] = t < nr ? dsp[(long)b * N + n] : 0.f;
+    spw[t] = (t < nr && gdw) ? a.pw[(long)b * N + n] : 0.f;
+  }
+  __syncthreads();
+  float* drows = a.dctx ? a.dctx + ((long)b * N + r0) * a.ldn : nullptr;
+  const __amdgpu_buffer_rsrc_t wr = ws_rsrc(a.ws);
+  if (t < D4) {
+    const int c = t;
+    float4 x[RB];
+#pragma unroll
+    for (int i = 0; i < RB; ++i) x[i] = reinterpret_cast<const float4*>(rows + (long)min(i, nr - 1) * a.ldn)[c];
+    const float4 qv = reinterpret_cast<const float4*>(a.q + (long)b * a.D)[c];
+    const float4 gv = gdw ? reinterpret_cast<const float4*>(a.dwctx + (long)b * a.D)[c]
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int i = 0; i < RB; ++i) fma4(sds[i], x[i], acc);
+    if (drows) {
+#pragma unroll
+      for (int i = 0; i < RB; ++i) {
+        if (i < nr) {
+          float4* d4 = reinterpret_cast<float4*>(drows + (long)i * a.ldn) + c;
+          float4 g;
+          g.x = fmaf(spw[i], gv.x, sds[i] * qv.x);
+          g.y = fmaf(spw[i], gv.y, sds[i] * qv.y);
+          g.z = fmaf(spw[i], gv.z, sds[i] * qv.z);
+          g.w = fmaf(spw[i], gv.w, sds[i] * qv.w);
+          if (a.accumulate) {
+            const float4 o = *d4;
+            g.x += o.x; g.y += o.y; g.z += o.z; g.w += o.w;
+          }
+          *d4 = g;
+        }
+      }
+    }
+    if (a.dq) {
+      if (nblk == 1) reinterpret_cast<float4*>(a.dq + (long)b * a.D)[c] = acc;
+      else pub4(wr, a.o_part + ((b * nblk + j) * a.D + 4 * c) * 4, acc);
+    }
+  }
+  if (nblk == 1 || !a.dq) return;
+  if (!last_arriver(a.cnt2 + b, nblk, &s_flag)) return;
+  if (t < D4) {
+    const int pb = a.o_part + (b * nblk * a.D + 4 * t) * 4;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = 0; i < nblk; ++i) {
+      const float4 p = get4(wr, pb + i * a.D * 4);
+      acc.x += p.x; acc.y += p.y; acc.z += p.z; acc.w += p.w;
+    }
+    reinterpret_cast<float4*>(a.dq + (long)b * a.D)[t] = acc;
   }
 }
 
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+inline int block_threads(int D) {
+  const int D4 = D >> 2;
+  int T = ((D4 + 63) / 64) * 64;
+  return T > 1024 ? 1024 : (T < 64 ? 64 : T);
+}
+
+inline int rows_per_block(int N, bool shift) { return shift ? 12 : 16; }
+
+// Workspace layout (32-bit words): [cnt1 kMaxB][cnt2 kMaxB] at fixed offsets (so the zero-on-entry
+// counters never overlap another call's data, whatever its shape), then [dp B*N][ds B*N][pw B*N]
+// [ml B*nblk*2][ee B*N*2][part B*nblk*D], the partial blocks 16-B aligned.
+constexpr long kMaxB = 32768;
+struct WsLayout {
+  unsigned* cnt1; unsigned* cnt2; float* ds; float* pw;
+  int o_dp, o_ml, o_ee, o_part;   // byte offsets from the workspace base
+  int64_t bytes;
+};
+
+inline WsLayout ws_layout(void* ws, int B, int N, int D) {
+  const long nblk = (N + 11) / 12;   // the larger block count of the two row splits
+  long off = 0;
+  auto take = [&](long n) { long o = off; off += (n + 3) & ~3L; return o; };
+  const long o1 = take(kMaxB), o2 = take(kMaxB), o3 = take((long)B * N), o4 = take((long)B * N), o5 = take((long)B * N),
+             o6 = take((long)B * nblk * 2), o7 = take((long)B * N * 2), o8 = take((long)B * nblk * D);
+  float* f = (float*)ws;
+  WsLayout L{(unsigned*)(f + o1), (unsigned*)(f + o2), f + o4, f + o5, (int)(o3 * 4), (int)(o6 * 4), (int)(o7 * 4),
+             (int)(o8 * 4), (int64_t)off * 4};
+  return L;
+}
+
+template <int RB>
+int launch_fwd(FwdArgs a, int B, void* ws, hipStream_t st) {
+  a.nblk = (a.N + RB - 1) / RB;
+  WsLayout L = ws_layout(ws, B, a.N, a.D);
+  a.cnt = L.cnt1; a.ws = (float*)ws; a.o_part = L.o_part; a.o_ml = L.o_ml; a.o_ee = L.o_ee;
+  hipLaunchKernelGGL(attn_fwd_kernel<RB>, dim3(a.nblk, B), dim3(block_threads(a.D)), 0, st, a);
+  DASA_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int RB>
+int launch_bwd(BwdArgs a, int B, void* ws, hipStream_t st) {
+  a.nblk = (a.N + RB - 1) / RB;
+  WsLayout L = ws_layout(ws, B, a.N, a.D);
+  a.cnt1 = L.cnt1; a.cnt2 = L.cnt2; a.ds = L.ds; a.pw = L.pw; a.ws = (float*)ws; a.o_dp = L.o_dp;
+  a.o_part = L.o_part;
+  const dim3 grid(a.nblk, B), block(block_threads(a.D));
+  if (a.dwctx) {
+    hipLaunchKernelGGL(attn_bwd_dp_kernel<RB>, grid, block, 0, st, a);
+    DASA_CHECK_LAUNCH();
+  }
+  hipLaunchKernelGGL(attn_bwd_apply_kernel<RB>, grid, block, 0, st, a);
+  DASA_CHECK_LAUNCH();
+  return 0;
+}
+
+bool bad_common(const float* q, const float* ctx, int64_t ldn, int B, int N, int D, const void* ws) {
+  return N > kMaxN || D > 4096 || B > kMaxB || ws_layout(nullptr, B, N, D).bytes >= (1L << 31) || (D & 3) || (ldn & 3) || ldn < D || !aligned16(q) || !aligned16(ctx) || !ws ||
+         !aligned16(ws);
+}
+
 }  // namespace
+
+extern "C" int64_t dasa_attn_workspace(int32_t B, int32_t N, int32_t D) {
+  if (B <= 0 || N <= 0 || D <= 0) return 16;
+  return ws_layout(nullptr, B, N, D).bytes;
+}
 
 extern "C" int dasa_softdot_fwd(const float* q, const float* ctx, int64_t ldn, const uint8_t* mask,
                                 float* scores, float* probs, float* wctx,
-                                int32_t B, int32_t N, int32_t D, void* stream) {
+                                int32_t B, int32_t N, int32_t D, float* ws, void* stream) {
   if (B <= 0 || N <= 0) return 0;
-  if (N > kMaxN || (D & 3) || (ldn & 3) || ldn < D || !scores || !aligned16(q) || !aligned16(ctx))
-    return (int)hipErrorInvalidValue;
-  hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(scores_kernel, dim3((B * N + 3) / 4), dim3(256), 0, st, q, (long)D, ctx, (long)ldn,
-                     scores, B, N, D);
-  DASA_CHECK_LAUNCH();
-  if (probs || wctx) {
-    ApplyArgs a{q, ctx, (long)ldn, scores, mask, nullptr, 0, probs, nullptr, nullptr, wctx, B, N, D};
-    dim3 grid(B, wctx ? (D / 4 + 63) / 64 : 1);
-    hipLaunchKernelGGL(apply_fwd_kernel, grid, dim3(256), 0, st, a);
-    DASA_CHECK_LAUNCH();
-  }
-  return 0;
+  if (bad_common(q, ctx, ldn, B, N, D, ws) || (wctx && !aligned16(wctx))) return (int)hipErrorInvalidValue;
+  FwdArgs a{q, ctx, (long)ldn, mask, nullptr, 0, scores, probs, nullptr, nullptr, wctx, N, D};
+  return launch_fwd<16>(a, B, ws, (hipStream_t)stream);
 }
 
 extern "C" int dasa_softdot_bwd(const float* q, const float* ctx, int64_t ldn, const float* probs,
@@ -290,19 +487,11 @@ extern "C" int dasa_softdot_bwd(const float* q, const float* ctx, int64_t ldn, c
                                 int32_t accumulate, int32_t B, int32_t N, int32_t D, float* ws,
                                 void* stream) {
   if (B <= 0 || N <= 0) return 0;
-  if (N > kMaxN || (D & 3) || (ldn & 3) || ldn < D || !probs || (dwctx && !ws))
+  if (bad_common(q, ctx, ldn, B, N, D, ws) || !probs || (!dwctx && !dscores) || (dwctx && !aligned16(dwctx)) ||
+      (dq && !aligned16(dq)) || (dctx && !aligned16(dctx)))
     return (int)hipErrorInvalidValue;
-  hipStream_t st = (hipStream_t)stream;
-  if (dwctx) {  // dp = ctx . dwctx -> ws[B][N]
-    hipLaunchKernelGGL(scores_kernel, dim3((B * N + 3) / 4), dim3(256), 0, st, dwctx, (long)D, ctx,
-                       (long)ldn, ws, B, N, D);
-    DASA_CHECK_LAUNCH();
-  }
-  BwdArgs a{q, ctx, (long)ldn, probs, nullptr, nullptr, 0, dwctx ? ws : nullptr, dwctx, dscores,
-            dq, dctx, accumulate, nullptr, B, N, D};
-  hipLaunchKernelGGL(apply_bwd_kernel, dim3(B, (D / 4 + 63) / 64), dim3(256), 0, st, a);
-  DASA_CHECK_LAUNCH();
-  return 0;
+  BwdArgs a{q, ctx, (long)ldn, probs, nullptr, nullptr, 0, dwctx, dscores, dq, dctx, accumulate, nullptr, N, D};
+  return launch_bwd<16>(a, B, ws, (hipStream_t)stream);
 }
 
 extern "C" int dasa_shift_attn_fwd(const float* q, const float* ctx, int64_t ldn, const float* shift_logits,
@@ -310,16 +499,10 @@ extern "C" int dasa_shift_attn_fwd(const float* q, const float* ctx, int64_t ldn
                                    int32_t B, int32_t D, int32_t K, float* ws, void* stream) {
   const int N = 36;
   if (B <= 0) return 0;
-  if (K < 1 || K > kMaxK || (D & 3) || (ldn & 3) || ldn < D || !shift_logits || !wctx || !ws)
+  if (K < 1 || K > kMaxK || bad_common(q, ctx, ldn, B, N, D, ws) || !shift_logits || !wctx || !aligned16(wctx))
     return (int)hipErrorInvalidValue;
-  hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(scores_kernel, dim3((B * N + 3) / 4), dim3(256), 0, st, q, (long)D, ctx, (long)ldn,
-                     ws, B, N, D);
-  DASA_CHECK_LAUNCH();
-  ApplyArgs a{q, ctx, (long)ldn, ws, nullptr, shift_logits, K, attn, shifted, wsm, wctx, B, N, D};
-  hipLaunchKernelGGL(apply_fwd_kernel, dim3(B, (D / 4 + 63) / 64), dim3(256), 0, st, a);
-  DASA_CHECK_LAUNCH();
-  return 0;
+  FwdArgs a{q, ctx, (long)ldn, nullptr, shift_logits, K, nullptr, attn, shifted, wsm, wctx, N, D};
+  return launch_fwd<12>(a, B, ws, (hipStream_t)stream);
 }
 
 extern "C" int dasa_shift_attn_bwd(const float* q, const float* ctx, int64_t ldn, const float* attn,
@@ -328,16 +511,10 @@ extern "C" int dasa_shift_attn_bwd(const float* q, const float* ctx, int64_t ldn
                                    int32_t B, int32_t D, int32_t K, float* ws, void* stream) {
   const int N = 36;
   if (B <= 0) return 0;
-  if (K < 1 || K > kMaxK || (D & 3) || (ldn & 3) || ldn < D || !attn || !shifted || !wsm || !dwctx ||
-      !dshift_logits || !ws)
+  if (K < 1 || K > kMaxK || bad_common(q, ctx, ldn, B, N, D, ws) || !attn || !shifted || !wsm || !dwctx ||
+      !dshift_logits || !aligned16(dwctx) || (dq && !aligned16(dq)) || (dctx && !aligned16(dctx)))
     return (int)hipErrorInvalidValue;
-  hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(scores_kernel, dim3((B * N + 3) / 4), dim3(256), 0, st, dwctx, (long)D, ctx,
-                     (long)ldn, ws, B, N, D);
-  DASA_CHECK_LAUNCH();
-  BwdArgs a{q, ctx, (long)ldn, attn, shifted, wsm, K, ws, dwctx, nullptr, dq, dctx, accumulate,
-            dshift_logits, B, N, D};
-  hipLaunchKernelGGL(apply_bwd_kernel, dim3(B, (D / 4 + 63) / 64), dim3(256), 0, st, a);
-  DASA_CHECK_LAUNCH();
-  return 0;
+  BwdArgs a{q, ctx, (long)ldn, attn, shifted, wsm, K, dwctx, nullptr, dq, dctx, accumulate,
+            dshift_logits, N, D};
+  return launch_bwd<12>(a, B, ws, (hipStream_t)stream);
 }

@@ -11,6 +11,9 @@
 #include "common.h"
 #include "../../include/dasa_hip.h"
 
+__attribute__((visibility("hidden"))) bool dasa_dropout_vec(const float* x, long ldx, float* y, long ldy, int rows, int cols, float p, uint64_t seed,
+                      hipStream_t st);   // elem.hip
+
 namespace {
 
 inline int cdivi(long a, long b) { return (int)((a + b - 1) / b); }
@@ -430,9 +433,53 @@ __global__ __launch_bounds__(256) void adain_musigma_kernel(const float* __restr
   }
 }
 
+// Register-resident variant for N = 256 * NV (2048 -> NV = 8): each lane holds its NV float4 of
+// both rows, so content and style are read from HBM exactly once (one round trip per wave).
+template <int NV>
+__global__ __launch_bounds__(256) void adain_musigma_reg_kernel(const float* __restrict__ cnt, long ldc,
+                                                                const float* __restrict__ sty, long lds,
+                                                                float* __restrict__ out, long ldo,
+                                                                float* __restrict__ stats, int M, float eps) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= M) return;
+  constexpr int N = 256 * NV;
+  const float4* c4 = reinterpret_cast<const float4*>(cnt + (long)row * ldc);
+  const float4* s4 = reinterpret_cast<const float4*>(sty + (long)row * lds);
+  float4 c[NV], t[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    c[k] = c4[lane + 64 * k];
+    t[k] = s4[lane + 64 * k];
+  }
+  float sc = 0.f, ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    sc += (c[k].x + c[k].y) + (c[k].z + c[k].w);
+    ss += (t[k].x + t[k].y) + (t[k].z + t[k].w);
+  }
+  const float mc = wave_sum(sc) / N, ms = wave_sum(ss) / N;
+  float vc = 0.f, vs = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const float4 a = make_float4(c[k].x - mc, c[k].y - mc, c[k].z - mc, c[k].w - mc);
+    const float4 b = make_float4(t[k].x - ms, t[k].y - ms, t[k].z - ms, t[k].w - ms);
+    vc += (a.x * a.x + a.y * a.y) + (a.z * a.z + a.w * a.w);
+    vs += (b.x * b.x + b.y * b.y) + (b.z * b.z + b.w * b.w);
+  }
+  const float sdc = sqrtf(wave_sum(vc) / (N - 1) + eps), sds = sqrtf(wave_sum(vs) / (N - 1) + eps);
+  float4* o4 = reinterpret_cast<float4*>(out + (long)row * ldo);
+#pragma unroll
+  for (int k = 0; k < NV; ++k)
+    o4[lane + 64 * k] = make_float4((c[k].x - mc) / sdc * sds + ms, (c[k].y - mc) / sdc * sds + ms,
+                                    (c[k].z - mc) / sdc * sds + ms, (c[k].w - mc) / sdc * sds + ms);
+  if (stats && lane == 0) {
+    stats[4 * row + 0] = mc; stats[4 * row + 1] = sdc; stats[4 * row + 2] = ms; stats[4 * row + 3] = sds;
+  }
+}
+
 }  // namespace
 
-extern "C" int dasa_version(void) { return 1; }
+extern "C" int dasa_version(void) { return 2; }
 extern "C" const char* dasa_build_info(void) { return "libdasa_hip gfx950 (CDNA4) fp32-MFMA v1"; }
 
 #define DASA_VPL_DISPATCH(N, KERNEL, GRID, ...)                                        \
@@ -533,6 +580,10 @@ extern "C" int dasa_reverse_valid(const float* x, const int32_t* lengths, float*
 extern "C" int dasa_dropout_fwd(const float* x, int64_t ldx, float* y, int64_t ldy, int32_t rows, int32_t cols,
                                 float p, uint64_t seed, void* stream) {
   if (rows <= 0 || cols <= 0) return 0;
+  if (dasa_dropout_vec(x, (long)ldx, y, (long)ldy, rows, cols, p, seed, (hipStream_t)stream)) {
+    DASA_CHECK_LAUNCH();
+    return 0;
+  }
   const long total = (long)rows * cols;
   int grid = cdivi(total, 256);
   if (grid > 8192) grid = 8192;
@@ -546,6 +597,13 @@ extern "C" int dasa_adain_musigma_fwd(const float* content, int64_t ldc_, const 
                                       int64_t ldo, float* stats, int32_t M, int32_t N, float eps, void* stream) {
   if (M <= 0) return 0;
   if (N < 2) return (int)hipErrorInvalidValue;
+  const bool al = !(((uintptr_t)content | (uintptr_t)style | (uintptr_t)out) & 15) && !((ldc_ | lds | ldo) & 3);
+  if (al && N == 2048) {
+    hipLaunchKernelGGL(adain_musigma_reg_kernel<8>, dim3(cdivi(M, 4)), dim3(256), 0, (hipStream_t)stream, content,
+                       (long)ldc_, style, (long)lds, out, (long)ldo, stats, M, eps);
+    DASA_CHECK_LAUNCH();
+    return 0;
+  }
   hipLaunchKernelGGL(adain_musigma_kernel, dim3(cdivi(M, 4)), dim3(256), 0, (hipStream_t)stream, content,
                      (long)ldc_, style, (long)lds, out, (long)ldo, stats, M, N, eps);
   DASA_CHECK_LAUNCH();

@@ -325,7 +325,7 @@ def flush_bilstm_backward():
     items, _BPTT.items = _BPTT.items, []
     groups = {}
     for it in items:
-        key = (tuple(id(p) for p in it["params"]), tuple(it["x"].shape))
+        key = (tuple(id(p) for p in it["params"]), tuple(it["x"].shape[1:]))
         groups.setdefault(key, []).append(it)
     for grp in groups.values():
         _batched_bptt(grp)
@@ -336,7 +336,7 @@ def _batched_bptt(grp):
     n = grp[0]["needs"]
     B, L, E = grp[0]["x"].shape
     H = W_hh_f.shape[1]
-    NB = B * len(grp)
+    NB = sum(it["x"].shape[0] for it in grp)
     sa = torch.cat([it["sa"] for it in grp], dim=2)          # [L][2][NB][4H]
     sc = torch.cat([it["sc"] for it in grp], dim=2)          # [L][2][NB][H]
     dout = torch.cat([it["dout"] if it["dout"] is not None else torch.zeros_like(it["out"]) for it in grp], 0)
@@ -344,7 +344,8 @@ def _batched_bptt(grp):
     def carry(k):
         if all(it[k] is None for it in grp):
             return None
-        return torch.cat([it[k] if it[k] is not None else torch.zeros(2, B, H, device=sa.device) for it in grp], 1)
+        return torch.cat([it[k] if it[k] is not None else torch.zeros(2, it["x"].shape[0], H, device=sa.device)
+                          for it in grp], 1)
     lens = torch.cat([it["lens"] for it in grp], 0)
     dgates = ops.bilstm_bwd(W_hh_f, W_hh_b, lens, (sa, sc), dout, carry("dh_n"), carry("dc_n"), H)
     del sa, sc, dout

@@ -1,0 +1,101 @@
+"""Isolated timing of the HBM-bound policy kernels (the depth-guided AdaIN gate, the 36-view shift
+attention, the instruction / candidate SoftDot attention, the mu/sigma AdaIN) at the shapes one
+decision step uses: cfg2 (B=20, the benchmark workload) and cfg5 (B=256, BASELINE.json's HBM/MFMA
+roofline stress config).
+
+Each kernel is launched REPS times back to back inside one captured HIP graph and the replay is
+bracketed by HIP events, so the per-launch time excludes host launch latency (inside the rollout the
+same kernels sit between dependent kernels, where the host is ahead of the GPU). `bytes` is the
+algorithmic (compulsory) traffic per launch: every input read once, every output written once. At B=20
+a launch's working set (3-34 MB) stays resident in the 256 MB Infinity Cache across replays, so those
+rates are cache-assisted; B=256 (80-330 MB per launch) streams from HBM."""
+import torch
+
+from . import ops
+
+HBM_PEAK_GBS = 8000.0
+REPS = 50
+
+
+def _time_graph(fn, reps=REPS):
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            fn()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    best = float("inf")
+    for _ in range(3):
+        e0.record()
+        g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        best = min(best, e0.elapsed_time(e1) / reps)
+    del g
+    return best * 1e3   # us per launch
+
+
+def _cases(B, dev):
+    g = torch.Generator(device=dev).manual_seed(B)
+    D, F, V, C, L, H, K = 2176, 2048, 36, 16, 80, 1024, 5
+
+    def rnd(*shape):
+        return torch.rand(*shape, device=dev, generator=g)
+    cases = []
+    # shift attention over the AdaIN'd panorama [B, 36, 2176] (model.py:318-353)
+    feat, q, z = rnd(B, V, D), rnd(B, D) * 0.05, rnd(B, K)
+    wctx, attn, shifted, wsm = ops.shift_attn_fwd(q, feat, z)
+    dw = rnd(B, D)
+    cases.append(("shift_attn", 4.0 * B * (V * D + 2 * D + 3 * V), lambda: ops.shift_attn_fwd(q, feat, z)))
+    cases.append(("shift_attn_bwd", 4.0 * B * (2 * V * D + 3 * D + 3 * V),
+                  lambda: ops.shift_attn_bwd(q, feat, attn, shifted, wsm, dw)))
+    # instruction attention over ctx [B, 80, 2048] with the padding mask (model.py:268-296)
+    ctx, qi = rnd(B, L, 2 * H), rnd(B, 2 * H) * 0.05
+    mask = torch.zeros(B, L, dtype=torch.bool, device=dev)
+    _, probs, _ = ops.softdot_fwd(qi, ctx, mask)
+    di = rnd(B, 2 * H)
+    cases.append(("softdot", 4.0 * B * (L * 2 * H + 2 * 2 * H + 3 * L), lambda: ops.softdot_fwd(qi, ctx, mask)))
+    cases.append(("softdot_bwd", 4.0 * B * (2 * L * 2 * H + 3 * 2 * H + 3 * L),
+                  lambda: ops.softdot_bwd(qi, ctx, probs, dwctx=di)))
+    # candidate logits over [B, 16, 2176] (scores only, output_prob=False)
+    cand, qc = rnd(B, C, D), rnd(B, D) * 0.05
+    cases.append(("cand_logit", 4.0 * B * (C * D + D + C),
+                  lambda: ops.softdot_fwd(qc, cand, None, want_probs=False, want_wctx=False)))
+    # DGAdaChannel gate epilogue: out = s * f (* noise) on the RGB columns of [B*(36+C), 2176] rows
+    R = B * (V + C)
+    s, f, out, noise = rnd(R, F), rnd(R, D), torch.empty(R, D, device=dev), rnd(F)
+    cases.append(("ada_gate", 12.0 * R * F, lambda: ops.ada_gate_fwd(s, f[:, :F], noise, out[:, :F])))
+    cases.append(("colscale", 8.0 * R * F, lambda: ops.colscale(f[:, :F], noise, out[:, :F])))
+    dout = rnd(R, D)
+    cases.append(("ada_gate_bwd", 16.0 * R * F, lambda: ops.ada_gate_bwd(dout[:, :F], s, f[:, :F], noise)))
+    # mu/sigma AdaIN (adaIn_type default, model.py:1822-1840) on the same rows
+    cases.append(("adain_musigma", 12.0 * R * F, lambda: ops.adain_musigma(f[:, :F], dout[:, :F], out=out[:, :F])))
+    return cases
+
+
+def hbm_kernels(batches=(20, 256)):
+    dev = torch.device("cuda", torch.cuda.current_device())
+    res = {}
+    for B in batches:
+        for name, nbytes, fn in _cases(B, dev):
+            us = _time_graph(fn)
+            gbs = nbytes / (us * 1e-6) / 1e9
+            res.setdefault(name, {})[f"B{B}"] = {"us": round(us, 2), "bytes": int(nbytes), "GB/s": round(gbs, 1),
+                                                  "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    return res
+
+
+if __name__ == "__main__":
+    import json
+    import sys
+    torch.cuda.set_device(0)
+    bs = tuple(int(x) for x in sys.argv[1:]) or (20, 256)
+    print(json.dumps(hbm_kernels(bs), indent=1))

@@ -188,7 +188,8 @@ def colsum(X, out=None, beta=0.0):
 def act_fwd(x, act):
     x = x.contiguous()
     y = torch.empty_like(x)
-    _call("dasa_act_fwd", "elementwise", _lib.lib().dasa_act_fwd, _p(x), _p(y), x.numel(), _ACT_IDS[act], _stream())
+    _call("dasa_act_fwd", "elementwise", _lib.lib().dasa_act_fwd, _p(x), _p(y), x.numel(), _ACT_IDS[act], _stream(),
+          nbytes=8.0 * x.numel())
     return y
 
 
@@ -198,14 +199,15 @@ def add2d(a, b, out=None):
     if out is None:
         out = torch.empty(a.shape, dtype=torch.float32, device=a.device)
     _, ldo = _rows(out)
-    _call("dasa_add2d", "elementwise", _lib.lib().dasa_add2d, _p(a), lda, _p(b), ldb, _p(out), ldo, rows, a.shape[-1], _stream())
+    _call("dasa_add2d", "elementwise", _lib.lib().dasa_add2d, _p(a), lda, _p(b), ldb, _p(out), ldo, rows, a.shape[-1], _stream(),
+          nbytes=12.0 * rows * a.shape[-1])
     return out
 
 
 def act_bwd(y_or_x, dy, act):
     dx = torch.empty_like(dy)
     _call("dasa_act_bwd", "elementwise", _lib.lib().dasa_act_bwd, _p(y_or_x.contiguous()), _p(dy.contiguous()), _p(dx), dy.numel(),
-                                  _ACT_IDS[act], _stream())
+          _ACT_IDS[act], _stream(), nbytes=12.0 * dy.numel())
     return dx
 
 
@@ -217,21 +219,23 @@ def dropout(x, p, seed, out=None):
         out = torch.empty_like(x)
     _, ldy = _rows(out)
     _call("dasa_dropout_fwd", "elementwise", _lib.lib().dasa_dropout_fwd, _p(x), ldx, _p(out), ldy, rows, cols, float(p), int(seed) & (2**64 - 1),
-                                      _stream())
+          _stream(), nbytes=8.0 * rows * cols)
     return out
 
 
 def copy2d(x, out):
     rows, ldx = _rows(x)
     _, ldo = _rows(out)
-    _call("dasa_copy2d", "elementwise", _lib.lib().dasa_copy2d, _p(x), ldx, _p(out), ldo, rows, x.shape[-1], _stream())
+    _call("dasa_copy2d", "elementwise", _lib.lib().dasa_copy2d, _p(x), ldx, _p(out), ldo, rows, x.shape[-1], _stream(),
+          nbytes=8.0 * rows * x.shape[-1])
     return out
 
 
 def colscale(x, scale, out):
     rows, ldx = _rows(x)
     _, ldo = _rows(out)
-    _call("dasa_colscale", "elementwise", _lib.lib().dasa_colscale, _p(x), ldx, _p(scale.contiguous()), _p(out), ldo, rows, x.shape[-1], _stream())
+    _call("dasa_colscale", "elementwise", _lib.lib().dasa_colscale, _p(x), ldx, _p(scale.contiguous()), _p(out), ldo, rows, x.shape[-1], _stream(),
+          nbytes=8.0 * rows * x.shape[-1])
     return out
 
 
@@ -240,7 +244,7 @@ def ada_gate_fwd(s, f, noise, out):
     _, ldf = _rows(f)
     _, ldo = _rows(out)
     _call("dasa_ada_gate_fwd", "ada_gate", _lib.lib().dasa_ada_gate_fwd, _p(s), lds, _p(f), ldf, _p(noise), _p(out), ldo, rows, s.shape[-1],
-                                       _stream())
+          _stream(), nbytes=12.0 * rows * s.shape[-1])
     return out
 
 
@@ -250,7 +254,7 @@ def ada_gate_bwd(dout, s, f, noise):
     _, ldf = _rows(f)
     dz = torch.empty(rows, s.shape[-1], dtype=torch.float32, device=s.device)
     _call("dasa_ada_gate_bwd", "ada_gate", _lib.lib().dasa_ada_gate_bwd, _p(dout), lddo, _p(s), lds, _p(f), ldf, _p(noise), _p(dz), s.shape[-1],
-                                       rows, s.shape[-1], _stream())
+          rows, s.shape[-1], _stream(), nbytes=16.0 * rows * s.shape[-1])
     return dz
 
 
@@ -322,6 +326,22 @@ def mha_bwd(Q, K, V, probs, dout, heads, scale, drop_p=0.0, seed=0):
 
 
 # ------------------------------------------------------------------------------ SoftDot attention
+_AWS = {}
+
+
+def _attn_ws(device, B, N, D):
+    """Attention workspace (include/dasa_hip.h dasa_attn_workspace): one zero-initialised buffer per
+    (device, stream), grown on demand. Its leading arrival counters are left zero by every call, so
+    the buffer is zeroed only when (re)allocated; calls on one stream never overlap."""
+    need = int(_lib.lib().dasa_attn_workspace(int(B), int(N), int(D)))
+    key = (device.index, _stream())
+    buf = _AWS.get(key)
+    if buf is None or buf.numel() * 4 < need:
+        buf = torch.zeros(max(need, 1 << 20) // 4 + 4, dtype=torch.float32, device=device)
+        _AWS[key] = buf
+    return buf
+
+
 def softdot_fwd(q, ctx, mask=None, want_scores=True, want_probs=True, want_wctx=True):
     """q [B, D]; ctx [B, N, D] (rows may be strided, e.g. a 2176 block); mask [B, N] bool."""
     B, N, D = ctx.shape
@@ -332,8 +352,10 @@ def softdot_fwd(q, ctx, mask=None, want_scores=True, want_probs=True, want_wctx=
     probs = torch.empty(B, N, dtype=torch.float32, device=q.device) if want_probs else None
     wctx = torch.empty(B, D, dtype=torch.float32, device=q.device) if want_wctx else None
     m = mask.to(torch.uint8).contiguous() if mask is not None else None
-    _call("dasa_softdot_fwd", "softdot", _lib.lib().dasa_softdot_fwd, _p(q), _p(ctx), ldn, _p(m), _p(scores), _p(probs),
-          _p(wctx), B, N, D, _stream(),
+    ws = _attn_ws(q.device, B, N, D)
+    fam = "softdot" if (probs is not None or wctx is not None) else "cand_logit"
+    _call("dasa_softdot_fwd", fam, _lib.lib().dasa_softdot_fwd, _p(q), _p(ctx), ldn, _p(m), _p(scores), _p(probs),
+          _p(wctx), B, N, D, _p(ws), _stream(),
           nbytes=4.0 * B * (N * D + D + (D if wctx is not None else 0) + 2 * N))
     return scores, probs, wctx
 
@@ -343,14 +365,15 @@ def softdot_bwd(q, ctx, probs, dwctx=None, dscores=None, want_dctx=True):
     ldn = ctx.stride(1)
     dq = torch.empty(B, D, dtype=torch.float32, device=q.device)
     dctx = torch.empty(B, N, D, dtype=torch.float32, device=q.device) if want_dctx else None
-    ws = torch.empty(B * N, dtype=torch.float32, device=q.device)
+    ws = _attn_ws(q.device, B, N, D)
     if dctx is not None:
         assert ldn == D, "dctx is written dense; pass a contiguous ctx for backward"
-    _call("dasa_softdot_bwd", "softdot_bwd", _lib.lib().dasa_softdot_bwd, _p(q.contiguous()), _p(ctx), ldn, _p(probs),
+    fam = "softdot_bwd" if dwctx is not None else "cand_logit_bwd"
+    _call("dasa_softdot_bwd", fam, _lib.lib().dasa_softdot_bwd, _p(q.contiguous()), _p(ctx), ldn, _p(probs),
           _p(dwctx.contiguous() if dwctx is not None else None),
           _p(dscores.contiguous() if dscores is not None else None), _p(dq), _p(dctx), 0,
           B, N, D, _p(ws), _stream(),
-          nbytes=4.0 * B * (N * D * (2 if dwctx is not None else 1) + (N * D if dctx is not None else 0) + 3 * D))
+          nbytes=4.0 * B * (N * D + (N * D if dctx is not None else 0) + 3 * D + 3 * N))
     return dq, dctx
 
 
@@ -364,10 +387,10 @@ def shift_attn_fwd(q, ctx, shift_logits):
     shifted = torch.empty_like(attn)
     wsm = torch.empty(B, K, dtype=torch.float32, device=q.device)
     wctx = torch.empty(B, D, dtype=torch.float32, device=q.device)
-    ws = torch.empty(B * N, dtype=torch.float32, device=q.device)
+    ws = _attn_ws(q.device, B, N, D)
     _call("dasa_shift_attn_fwd", "shift_attn", _lib.lib().dasa_shift_attn_fwd, _p(q.contiguous()), _p(ctx), ldn,
           _p(shift_logits.contiguous()), _p(attn), _p(shifted), _p(wsm), _p(wctx), B, D, K, _p(ws), _stream(),
-          nbytes=4.0 * B * (N * D + 2 * D))
+          nbytes=4.0 * B * (N * D + 2 * D + 3 * N))
     return wctx, attn, shifted, wsm
 
 
@@ -380,10 +403,10 @@ def shift_attn_bwd(q, ctx, attn, shifted, wsm, dwctx, want_dctx=True):
     if dctx is not None:
         assert ldn == D, "dctx is written dense; pass a contiguous ctx for backward"
     dz = torch.empty(B, K, dtype=torch.float32, device=q.device)
-    ws = torch.empty(B * N, dtype=torch.float32, device=q.device)
+    ws = _attn_ws(q.device, B, N, D)
     _call("dasa_shift_attn_bwd", "shift_attn_bwd", _lib.lib().dasa_shift_attn_bwd, _p(q.contiguous()), _p(ctx), ldn,
           _p(attn), _p(shifted), _p(wsm), _p(dwctx.contiguous()), _p(dq), _p(dctx), _p(dz), 0, B, D, K, _p(ws),
-          _stream(), nbytes=4.0 * B * (N * D * (3 if dctx is not None else 2) + 3 * D))
+          _stream(), nbytes=4.0 * B * (N * D + (N * D if dctx is not None else 0) + 3 * D + 3 * N))
     return dq, dctx, dz
 
 
@@ -395,7 +418,7 @@ def lstm_cell_fwd(gates, c_prev, save=False):
     c = torch.empty_like(h)
     act = torch.empty_like(gates) if save else None
     _call("dasa_lstm_cell_fwd", "lstm_cell", _lib.lib().dasa_lstm_cell_fwd, _p(gates.contiguous()), _p(c_prev.contiguous()), _p(h), _p(c), _p(act), B, H,
-                                        _stream())
+          _stream(), nbytes=4.0 * B * (4 * H + H + 2 * H + (4 * H if act is not None else 0)))
     return h, c, act
 
 
@@ -406,7 +429,7 @@ def lstm_cell_bwd(act, c_prev, c, dh, dc):
     dc_prev = torch.empty(B, H, dtype=torch.float32, device=act.device)
     _call("dasa_lstm_cell_bwd", "lstm_cell", _lib.lib().dasa_lstm_cell_bwd, _p(act), _p(c_prev.contiguous()), _p(c), _p(dh.contiguous() if dh is not None else None),
                                         _p(dc.contiguous() if dc is not None else None), _p(dgates), _p(dc_prev), B, H,
-                                        _stream())
+          _stream(), nbytes=4.0 * B * (4 * H + 4 * H + H + 3 * H))
     return dgates, dc_prev
 
 

@@ -13,10 +13,12 @@ FAMILIES = {
     "gemm": ("mfma", "gemm_f32_kernel"),
     "bilstm": ("mfma", "bilstm_step_fused_kernel"),
     "bilstm_bptt": ("mfma", "bilstm_bptt_step_kernel"),
-    "shift_attn": ("hbm", "scores_kernel+apply_fwd_kernel"),
-    "shift_attn_bwd": ("hbm", "scores_kernel+apply_bwd_kernel"),
-    "softdot": ("hbm", "scores_kernel+apply_fwd_kernel"),
-    "softdot_bwd": ("hbm", "scores_kernel+apply_bwd_kernel"),
+    "shift_attn": ("hbm", "attn_fwd_kernel<12>"),
+    "shift_attn_bwd": ("hbm", "attn_bwd_dp_kernel<12>+attn_bwd_apply_kernel<12>"),
+    "softdot": ("hbm", "attn_fwd_kernel<16>"),
+    "softdot_bwd": ("hbm", "attn_bwd_dp_kernel<16>+attn_bwd_apply_kernel<16>"),
+    "cand_logit": ("hbm", "attn_fwd_kernel<16>"),
+    "cand_logit_bwd": ("hbm", "attn_bwd_apply_kernel<16>"),
     "mha": ("mfma", "mha_fwd_kernel"),
     "layernorm": ("hbm", "ln_fwd_kernel"),
     "embed": ("hbm", "embed_kernel"),

@@ -327,6 +327,140 @@ class Seq2SeqAgent(BaseAgent):
         ops.copy2d(x[..., -args.angle_feat_size:], out[..., -args.angle_feat_size:])
         return out
 
+    def _batch_teacher_ok(self):
+        """Teacher-forced rollouts are encoded for all steps at once unless a per-step host decision
+        needs the policy (--submit's visited masks) or it is switched off (DASA_TEACHER_BATCH=0)."""
+        return not args.submit and os.environ.get("DASA_TEACHER_BATCH", "1") != "0"
+
+    def _step_reward(self, perm_obs, cpu_a_t, ended, last_dist):
+        """agent_dg.py:900-925: reward / mask of one step; updates last_dist in place."""
+        batch_size = len(perm_obs)
+        dist = np.zeros(batch_size, np.float32)
+        reward = np.zeros(batch_size, np.float32)
+        mask = np.ones(batch_size, np.float32)
+        for i, ob in enumerate(perm_obs):
+            dist[i] = ob["distance"]
+            if ended[i]:
+                reward[i] = 0.0
+                mask[i] = 0.0
+            else:
+                action_idx = cpu_a_t[i]
+                if action_idx == -1:
+                    reward[i] = 2.0 if dist[i] < 3 else -2.0
+                else:
+                    reward[i] = -(dist[i] - last_dist[i])
+                    if reward[i] > 0:
+                        reward[i] = 1
+                    elif reward[i] < 0:
+                        reward[i] = -1
+                    else:
+                        raise NameError("The action doesn't change the move")
+        last_dist[:] = dist
+        return reward, mask
+
+    def _teacher_plan(self, perm_obs, perm_idx, ended, last_dist, traj, n_steps):
+        """Steps the env through up to n_steps teacher-forced steps ahead of the policy work (the
+        reference interleaves the same env calls with the decoder, agent_dg.py:832-936; the teacher
+        action depends only on the observation and `ended`, :325-344). Returns one record per step
+        (observations, teacher targets, ended-before-step, reward, mask) and the final observations;
+        `ended`, `last_dist` and `traj` are advanced in place exactly as the step loop advances them.
+        Stops early when every row has ended."""
+        plan = []
+        for _ in range(n_steps):
+            if ended.all():
+                break
+            target_np = self._teacher_action_np(perm_obs, ended)
+            rec = {"obs": perm_obs, "target_np": target_np, "ended": ended.copy()}
+            cpu_a_t = target_np.copy()
+            for i, next_id in enumerate(cpu_a_t):
+                if next_id == len(perm_obs[i]["candidate"]) or next_id == args.ignoreid:
+                    cpu_a_t[i] = -1
+            self.make_equiv_action(cpu_a_t, perm_obs, perm_idx, traj)
+            obs = np.array(self.env._get_obs())
+            perm_obs = obs[perm_idx]
+            rec["reward"], rec["mask"] = self._step_reward(perm_obs, cpu_a_t, ended, last_dist)
+            plan.append(rec)
+            ended[:] = np.logical_or(ended, (cpu_a_t == -1))
+            if ended.all():
+                break
+        return plan, perm_obs
+
+    def _step_inputs(self, obs_steps):
+        """get_input_feat for several steps, stacked along the batch (step-major); the candidates of
+        all steps as flat rows [R, F] with cinfo[t] = (first row, C_t, candidate lengths)."""
+        if hasattr(self.env, "device_input_feat_steps"):
+            return self.env.device_input_feat_steps(obs_steps, self.device)
+        parts = [self.get_input_feat(o) for o in obs_steps]
+        cinfo, row = [], 0
+        for p in parts:
+            cinfo.append((row, p[3].shape[1], p[5]))
+            row += p[3].shape[0] * p[3].shape[1]
+        cat = (lambda ts: ts[0] if len(ts) == 1 else torch.cat(ts, 0))
+        return (cat([p[0] for p in parts]), cat([p[1] for p in parts]), cat([p[2] for p in parts]),
+                cat([p[3].reshape(-1, p[3].shape[-1]) for p in parts]),
+                cat([p[4].reshape(-1, p[4].shape[-1]) for p in parts]), cinfo)
+
+    def _encode_steps(self, obs_steps, seq, seq_mask, lens_dev, noise, consistent_drop):
+        """Feature stage of the step loop (agent_dg.py:725-805): features -> env drop -> AdaIN ->
+        DicEncoder, for one or several steps' observations at once (every op in it is per row, so
+        stacking T steps along the batch computes each step's values; dropout draws stay independent
+        per row and step). Returns per step: angle input, AdaIN'd panorama, AdaIN'd candidates,
+        candidate lengths, ctx and the encoder's decoder-init states."""
+        T = len(obs_steps)
+        B = len(obs_steps[0])
+        angle = args.angle_feat_size
+        input_a_t, f_t, d_t, candidate_feat, candidate_dfeat, cinfo = self._step_inputs(obs_steps)
+        stage = args.env_drop_stage
+        use_noise = consistent_drop and noise is not None
+        all_img_feats = f_t                  # the raw panorama (agent_dg.py:730)
+        df_t = f_t                           # df_t = f_t.clone() (agent_dg.py:728), copied lazily below
+        if use_noise and stage == "before_adain":     # agent_dg.py:731-736
+            candidate_feat = self._noise_mult(candidate_feat, noise)
+            f_t = self._noise_mult(f_t, noise)
+            if args.depth_drop:
+                candidate_dfeat = self._noise_mult(candidate_dfeat, noise)
+                df_t = f_t
+        after = use_noise and stage == "after_adain"
+        if args.adaIn_type in ("channel", "rgb_channel"):            # agent_dg.py:748-768
+            style_v = f_t if args.adaIn_type == "rgb_channel" else d_t
+            style_c = candidate_feat if args.adaIn_type == "rgb_channel" else candidate_dfeat
+            # df_t's angle columns are df_t's own (== f_t's); its RGB columns are replaced
+            df_t = self.adaIn.feature(f_t, style_v, noise if (after and args.depth_drop) else None)
+            candidate_feat = self.adaIn.feature(candidate_feat, style_c, noise if after else None)
+            if after:
+                f_t = self._noise_mult(f_t, noise)
+        elif args.adaIn_type == "default":                             # agent_dg.py:774-777
+            f_t = f_t.clone()
+            model.adaptive_instance_normalization(f_t[..., :-angle], d_t[..., :-angle], out=f_t[..., :-angle])
+            candidate_feat = candidate_feat.clone()
+            model.adaptive_instance_normalization(candidate_feat[..., :-angle], candidate_dfeat[..., :-angle],
+                                                  out=candidate_feat[..., :-angle])
+            if after:                                                  # agent_dg.py:780-785
+                candidate_feat = self._noise_mult(candidate_feat, noise)
+                f_t = self._noise_mult(f_t, noise)
+                if args.depth_drop:
+                    df_t = self._noise_mult(df_t, noise)
+        elif after:
+            candidate_feat = self._noise_mult(candidate_feat, noise)
+            f_t = self._noise_mult(f_t, noise)
+            if args.depth_drop:
+                df_t = self._noise_mult(df_t, noise)
+        img = f_t if args.use_dropout_vision else all_img_feats
+        if T == 1:
+            ctx, en_ht, en_ct, _, ctx_v = self.encoder(seq, mask=seq_mask, lengths=lens_dev, f_t_all=img)
+        else:
+            ctx, en_ht, en_ct, _, ctx_v = self.encoder(seq.repeat(T, 1), mask=seq_mask.repeat(T, 1),
+                                                       lengths=lens_dev.repeat(T), f_t_all=img)
+        if args.ctx_v:
+            df_t = df_t + ctx_v
+        out = []
+        for t in range(T):
+            sl = slice(t * B, (t + 1) * B)
+            off, C, leng = cinfo[t]
+            out.append({"a": input_a_t[sl], "df": df_t[sl], "cand": candidate_feat[off:off + B * C].view(B, C, -1),
+                        "leng": leng, "ctx": ctx[sl], "en_ht": en_ht[sl], "en_ct": en_ct[sl]})
+        return out
+
     def vl_rollout(self, train_ml=None, train_rl=True, reset=True, speaker=None):
         """agent_dg.py:633-1033."""
         if self.feedback == "teacher" or self.feedback == "argmax":
@@ -375,129 +509,106 @@ class Seq2SeqAgent(BaseAgent):
         consistent_drop = args.consistent_drop or (speaker is not None)
         if args.decoder_consistent_drop:
             self.decoder.init_noise((seq.shape[0], args.d_enc_hidden_size))
-        self.encoder.cache_language(not self.encoder.training, steps=self.episode_len)
-        angle = args.angle_feat_size
+        enc_args = (seq, seq_mask, lens_dev, noise, consistent_drop)
         h_t = c_t = h1 = ctx = None
-        for t in range(self.episode_len):
-            input_a_t, f_t, d_t, candidate_feat, candidate_dfeat, candidate_leng = self.get_input_feat(perm_obs)
-            # host-side inputs of the step's loss/action stage, copied up front without a sync (the
-            # reference builds them after the decoder with blocking copies; same values)
-            target_np = self._teacher_action_np(perm_obs, ended)
-            target = self._to_dev(target_np)
-            candidate_mask = utils.length2mask(candidate_leng, device=self.device)
-            stage = args.env_drop_stage
-            use_noise = consistent_drop and noise is not None
-            all_img_feats = f_t                  # the raw panorama (agent_dg.py:730)
-            df_t = f_t                           # df_t = f_t.clone() (agent_dg.py:728), copied lazily below
-            if use_noise and stage == "before_adain":     # agent_dg.py:731-736
-                candidate_feat = self._noise_mult(candidate_feat, noise)
-                f_t = self._noise_mult(f_t, noise)
-                if args.depth_drop:
-                    candidate_dfeat = self._noise_mult(candidate_dfeat, noise)
-                    df_t = f_t
-            after = use_noise and stage == "after_adain"
-            if args.adaIn_type in ("channel", "rgb_channel"):            # agent_dg.py:748-768
-                style_v = f_t if args.adaIn_type == "rgb_channel" else d_t
-                style_c = candidate_feat if args.adaIn_type == "rgb_channel" else candidate_dfeat
-                # df_t's angle columns are df_t's own (== f_t's); its RGB columns are replaced
-                df_t = self.adaIn.feature(f_t, style_v, noise if (after and args.depth_drop) else None)
-                candidate_feat = self.adaIn.feature(candidate_feat, style_c, noise if after else None)
-                if after:
-                    f_t = self._noise_mult(f_t, noise)
-            elif args.adaIn_type == "default":                             # agent_dg.py:774-777
-                f_t = f_t.clone()
-                model.adaptive_instance_normalization(f_t[..., :-angle], d_t[..., :-angle], out=f_t[..., :-angle])
-                candidate_feat = candidate_feat.clone()
-                model.adaptive_instance_normalization(candidate_feat[..., :-angle], candidate_dfeat[..., :-angle],
-                                                      out=candidate_feat[..., :-angle])
-                if after:                                                  # agent_dg.py:780-785
-                    candidate_feat = self._noise_mult(candidate_feat, noise)
-                    f_t = self._noise_mult(f_t, noise)
-                    if args.depth_drop:
-                        df_t = self._noise_mult(df_t, noise)
-            elif after:
-                candidate_feat = self._noise_mult(candidate_feat, noise)
-                f_t = self._noise_mult(f_t, noise)
-                if args.depth_drop:
-                    df_t = self._noise_mult(df_t, noise)
-            img = f_t if args.use_dropout_vision else all_img_feats
-            ctx, en_ht, en_ct, _, ctx_v = self.encoder(seq, mask=seq_mask, lengths=lens_dev, f_t_all=img)
-            if args.ctx_v:
-                df_t = df_t + ctx_v
-            if t == 0:
-                h_t, c_t, logit, h1, aux_outputs = self.decoder(input_a_t, df_t, candidate_feat, en_ht, en_ht, en_ct,
-                                                                ctx, ctx_mask, already_dropfeat=consistent_drop)
-            else:
-                h_t, c_t, logit, h1, aux_outputs = self.decoder(input_a_t, df_t, candidate_feat, h_t, h1, c_t, ctx,
-                                                                ctx_mask, already_dropfeat=consistent_drop)
-            hidden_states.append(h_t)
-            if args.submit:
-                cm = candidate_mask.cpu()
-                for ob_id, ob in enumerate(perm_obs):
-                    visited[ob_id].add(ob["viewpoint"])
-                    for c_id, c in enumerate(ob["candidate"]):
-                        if c["viewpointId"] in visited[ob_id]:
-                            cm[ob_id][c_id] = 1
-                candidate_mask = cm.to(self.device)
-            logit = logit.masked_fill(candidate_mask, -float("inf"))
-            forth_loss = self.criterion(logit, target)
-            total_forth_loss += forth_loss
-            if args.pred_back:
-                back_logit = aux_outputs["back_logit"].masked_fill(candidate_mask, -float("inf"))
-                total_back_loss += self.criterion(back_logit, self._back_teacher_action(perm_obs, ended))
-            if self.feedback == "teacher":
-                a_t = target
-            elif self.feedback == "argmax":
-                _, a_t = logit.max(1)
-                a_t = a_t.detach()
-                policy_log_probs.append(F.log_softmax(logit, 1).gather(1, a_t.unsqueeze(1)))
-            elif self.feedback == "sample":
-                probs = F.softmax(logit, 1)
-                c = torch.distributions.Categorical(probs, validate_args=False)   # (validation = a host sync)
-                ent = c.entropy()
-                deferred["entropy"].append(ent.sum().detach())
-                entropys.append(ent)
-                a_t = (self.sample_fn(probs) if self.sample_fn is not None else c.sample()).detach()
-                policy_log_probs.append(c.log_prob(a_t))
-            else:
-                sys.exit("Invalid feedback option")
-            if self.feedback == "teacher":
-                cpu_a_t = target_np.copy()           # a_t is target: its host copy, no device round trip
-            else:
-                cpu_a_t = a_t.cpu().numpy().copy()  # the step's one device->host sync
-            self.encoder.lang_pump(2)                 # GPU work for the coming steps while the host steps the env
-            for i, next_id in enumerate(cpu_a_t):
-                if next_id == (candidate_leng[i] - 1) or next_id == args.ignoreid:
-                    cpu_a_t[i] = -1
-            self.make_equiv_action(cpu_a_t, perm_obs, perm_idx, traj)
-            obs = np.array(self.env._get_obs())
-            perm_obs = obs[perm_idx]
-            dist = np.zeros(batch_size, np.float32)
-            reward = np.zeros(batch_size, np.float32)
-            mask = np.ones(batch_size, np.float32)
-            for i, ob in enumerate(perm_obs):
-                dist[i] = ob["distance"]
-                if ended[i]:
-                    reward[i] = 0.0
-                    mask[i] = 0.0
-                else:
-                    action_idx = cpu_a_t[i]
-                    if action_idx == -1:
-                        reward[i] = 2.0 if dist[i] < 3 else -2.0
+        if self.feedback == "teacher" and self._batch_teacher_ok():
+            # Teacher forcing: the actions (and so every observation of the episode) do not depend
+            # on the policy, so the env is stepped first and the encoder runs once for all steps.
+            # Chunked: the host steps the env for chunk k+1 while the GPU encodes and decodes chunk k.
+            self.encoder.cache_language(not self.encoder.training, steps=0)
+            chunk = max(1, int(os.environ.get("DASA_TEACHER_CHUNK", "8")))
+            t = 0
+            while t < self.episode_len and not ended.all():
+                n = min(chunk if t else max(1, chunk // 2), self.episode_len - t)
+                plan, perm_obs = self._teacher_plan(perm_obs, perm_idx, ended, last_dist, traj, n)
+                enc = self._encode_steps([s["obs"] for s in plan], *enc_args)
+                targets = self._to_dev(np.stack([s["target_np"] for s in plan]))
+                for i, (s, e) in enumerate(zip(plan, enc)):
+                    if t == 0:
+                        h_t, c_t, logit, h1, aux = self.decoder(e["a"], e["df"], e["cand"], e["en_ht"], e["en_ht"],
+                                                                e["en_ct"], e["ctx"], ctx_mask,
+                                                                already_dropfeat=consistent_drop)
                     else:
-                        reward[i] = -(dist[i] - last_dist[i])
-                        if reward[i] > 0:
-                            reward[i] = 1
-                        elif reward[i] < 0:
-                            reward[i] = -1
-                        else:
-                            raise NameError("The action doesn't change the move")
-            rewards.append(reward)
-            masks.append(mask)
-            last_dist[:] = dist
-            ended[:] = np.logical_or(ended, (cpu_a_t == -1))
-            if ended.all():
-                break
+                        h_t, c_t, logit, h1, aux = self.decoder(e["a"], e["df"], e["cand"], h_t, h1, c_t, e["ctx"],
+                                                                ctx_mask, already_dropfeat=consistent_drop)
+                    t += 1
+                    ctx = e["ctx"]
+                    hidden_states.append(h_t)
+                    candidate_mask = utils.length2mask(e["leng"], device=self.device)
+                    logit = logit.masked_fill(candidate_mask, -float("inf"))
+                    total_forth_loss += self.criterion(logit, targets[i])
+                    if args.pred_back:
+                        back_logit = aux["back_logit"].masked_fill(candidate_mask, -float("inf"))
+                        total_back_loss += self.criterion(back_logit,
+                                                          self._back_teacher_action(s["obs"], s["ended"]))
+                    rewards.append(s["reward"])
+                    masks.append(s["mask"])
+        else:
+            self.encoder.cache_language(not self.encoder.training, steps=self.episode_len)
+            for t in range(self.episode_len):
+                # host-side inputs of the step's loss/action stage, copied up front without a sync (the
+                # reference builds them after the decoder with blocking copies; same values)
+                target_np = self._teacher_action_np(perm_obs, ended)
+                target = self._to_dev(target_np)
+                (e,) = self._encode_steps([perm_obs], *enc_args)
+                candidate_leng = e["leng"]
+                candidate_mask = utils.length2mask(candidate_leng, device=self.device)
+                ctx = e["ctx"]
+                if t == 0:
+                    h_t, c_t, logit, h1, aux_outputs = self.decoder(e["a"], e["df"], e["cand"], e["en_ht"],
+                                                                    e["en_ht"], e["en_ct"], ctx, ctx_mask,
+                                                                    already_dropfeat=consistent_drop)
+                else:
+                    h_t, c_t, logit, h1, aux_outputs = self.decoder(e["a"], e["df"], e["cand"], h_t, h1, c_t, ctx,
+                                                                    ctx_mask, already_dropfeat=consistent_drop)
+                hidden_states.append(h_t)
+                if args.submit:
+                    cm = candidate_mask.cpu()
+                    for ob_id, ob in enumerate(perm_obs):
+                        visited[ob_id].add(ob["viewpoint"])
+                        for c_id, c in enumerate(ob["candidate"]):
+                            if c["viewpointId"] in visited[ob_id]:
+                                cm[ob_id][c_id] = 1
+                    candidate_mask = cm.to(self.device)
+                logit = logit.masked_fill(candidate_mask, -float("inf"))
+                forth_loss = self.criterion(logit, target)
+                total_forth_loss += forth_loss
+                if args.pred_back:
+                    back_logit = aux_outputs["back_logit"].masked_fill(candidate_mask, -float("inf"))
+                    total_back_loss += self.criterion(back_logit, self._back_teacher_action(perm_obs, ended))
+                if self.feedback == "teacher":
+                    a_t = target
+                elif self.feedback == "argmax":
+                    _, a_t = logit.max(1)
+                    a_t = a_t.detach()
+                    policy_log_probs.append(F.log_softmax(logit, 1).gather(1, a_t.unsqueeze(1)))
+                elif self.feedback == "sample":
+                    probs = F.softmax(logit, 1)
+                    c = torch.distributions.Categorical(probs, validate_args=False)   # (validation = a host sync)
+                    ent = c.entropy()
+                    deferred["entropy"].append(ent.sum().detach())
+                    entropys.append(ent)
+                    a_t = (self.sample_fn(probs) if self.sample_fn is not None else c.sample()).detach()
+                    policy_log_probs.append(c.log_prob(a_t))
+                else:
+                    sys.exit("Invalid feedback option")
+                if self.feedback == "teacher":
+                    cpu_a_t = target_np.copy()           # a_t is target: its host copy, no device round trip
+                else:
+                    cpu_a_t = a_t.cpu().numpy().copy()  # the step's one device->host sync
+                self.encoder.lang_pump(2)                 # GPU work for the coming steps while the host steps the env
+                for i, next_id in enumerate(cpu_a_t):
+                    if next_id == (candidate_leng[i] - 1) or next_id == args.ignoreid:
+                        cpu_a_t[i] = -1
+                self.make_equiv_action(cpu_a_t, perm_obs, perm_idx, traj)
+                obs = np.array(self.env._get_obs())
+                perm_obs = obs[perm_idx]
+                reward, mask = self._step_reward(perm_obs, cpu_a_t, ended, last_dist)
+                rewards.append(reward)
+                masks.append(mask)
+                ended[:] = np.logical_or(ended, (cpu_a_t == -1))
+                if ended.all():
+                    break
 
         if train_rl:
             input_a_t, f_t, d_t, candidate_feat, candidate_dfeat, candidate_leng = self.get_input_feat(perm_obs)

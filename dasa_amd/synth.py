@@ -128,6 +128,7 @@ class SynthWorld:
         self.pos = g.random((P, 3)) * 20.0
         self.ids = ["vp%03d" % i for i in range(P)]
         self.index = {v: i for i, v in enumerate(self.ids)}
+        self._nav_cache, self._loc_cache = {}, {}
         self.neighbors = []   # per vp: list of (nbr index, pointId, dheading, delevation)
         for v in range(P):
             n = int(g.integers(1, max_neighbors + 1))
@@ -142,6 +143,13 @@ class SynthWorld:
         self.next_hop = np.full((P, P), -1, dtype=np.int64)
         for s in range(P):
             self._dijkstra(s)
+
+    def loc(self, v):
+        """Shared MatterSim Location record of viewpoint v (read-only for callers)."""
+        lc = self._loc_cache.get(v)
+        if lc is None:
+            lc = self._loc_cache[v] = _Loc(self.ids[v])
+        return lc
 
     def _edge(self, a, b):
         return float(np.linalg.norm(self.pos[a] - self.pos[b]))
@@ -236,7 +244,10 @@ class SynthSim:
         self._set_heading_elevation(heading, elevation)
 
     def navigable(self):
-        return [self.vp] + [u for (u, _, _, _) in self.world.neighbors[self.vp]]
+        nav = self.world._nav_cache.get(self.vp)
+        if nav is None:
+            nav = self.world._nav_cache[self.vp] = [self.vp] + [u for (u, _, _, _) in self.world.neighbors[self.vp]]
+        return nav
 
     def makeAction(self, index, heading, elevation):
         nav = self.navigable()
@@ -257,7 +268,7 @@ class SynthSim:
     def getState(self):
         s = _State()
         s.scanId = "synth"
-        s.location = _Loc(self.world.ids[self.vp])
+        s.location = self.world.loc(self.vp)
         s.viewIndex = self.view_index
         s.heading = self.heading
         s.elevation = self.elevation
@@ -301,6 +312,8 @@ class SynthR2RBatch:
         # assembles the tensors on the device (device_input_feat), as a device-resident feature store would.
         self.lazy_features = lazy_features
         self._store = None
+        self._cand_cache = {}
+        self._dist_cache = {}
 
     # -- episodes
     def _new_batch(self):
@@ -341,6 +354,17 @@ class SynthR2RBatch:
 
     # -- observations
     def _candidates(self, v, base_view):
+        if self.lazy_features:
+            # the world is static, so a viewpoint's candidate list depends only on (v, heading step):
+            # memoised (the agent never mutates candidates)
+            key = (v, base_view % 12)
+            c = self._cand_cache.get(key)
+            if c is None:
+                c = self._cand_cache[key] = self._make_candidates(v, base_view)
+            return c
+        return self._make_candidates(v, base_view)
+
+    def _make_candidates(self, v, base_view):
         w = self.world
         base_heading = (base_view % 12) * HEADING_INC
         out = []
@@ -378,7 +402,10 @@ class SynthR2RBatch:
         w = self.world
         if self.mode == "goal":
             return float(w.dist[sim.vp, w.index[item["path"][-1]]])
-        return float(np.linalg.norm(w.pos[sim.vp] - self.virtual_goal))
+        d = self._dist_cache.get(sim.vp)
+        if d is None:
+            d = self._dist_cache[sim.vp] = float(np.linalg.norm(w.pos[sim.vp] - self.virtual_goal))
+        return d
 
     def _get_obs(self):
         obs = []
@@ -428,46 +455,70 @@ class DeviceFeatureStore:
         self.A = angle_feat_size
 
     def input_feat(self, obs):
+        a_t, f_t, d_t, cf, cd, cinfo = self.input_feat_steps([obs])
+        _, C, leng = cinfo[0]
+        B = len(obs)
+        return a_t, f_t, d_t, cf.view(B, C, -1), cd.view(B, C, -1), leng
+
+    def input_feat_steps(self, obs_steps):
+        """The input blocks of several rollout steps stacked along the batch (step-major): a_t [T*B, A],
+        panoramas f_t / d_t [T*B, 36, F], and the candidates of every step as flat rows cf / cd [R, F]
+        with cinfo[t] = (first row, C_t, lengths_t) — step t's block is rows [off, off + B*C_t) viewed
+        as [B, C_t, F]. One gather launch per tensor for all steps."""
         import torch
         from . import ops
-        B = len(obs)
         A = self.A
-        leng = [len(ob["candidate"]) + 1 for ob in obs]
-        C = max(leng)
-        vp = np.array([ob["_vp_index"] for ob in obs], np.int64)
-        view = np.array([ob["viewIndex"] for ob in obs], np.int64)
+        ia_v, ib_v, ia_c, ib_c, cangs, a_ts, cinfo = [], [], [], [], [], [], []
         r36 = np.arange(NUM_VIEWS)
-        ia_v = (vp[:, None] * NUM_VIEWS + r36[None]).astype(np.int32).reshape(-1)
-        ib_v = (view[:, None] * NUM_VIEWS + r36[None]).astype(np.int32).reshape(-1)
-        ia_c = np.full((B, C), -1, np.int32)
-        ib_c = np.full((B, C), -1, np.int32)
-        cang = np.zeros((B, C, A), np.float32)
-        a_t = np.zeros((B, A), np.float32)
-        for i, ob in enumerate(obs):
-            a_t[i] = angle_feature(ob["heading"], ob["elevation"], A)
-            for j, c in enumerate(ob["candidate"]):
-                ia_c[i, j] = vp[i] * NUM_VIEWS + c["pointId"]
-                ib_c[i, j] = i * C + j
-                cang[i, j] = c["angle"] if "angle" in c else c["feature"][-A:]
-        ints = torch.from_numpy(np.concatenate([ia_v, ib_v, ia_c.reshape(-1), ib_c.reshape(-1)])).pin_memory()
+        row = 0
+        for obs in obs_steps:
+            B = len(obs)
+            leng = [len(ob["candidate"]) + 1 for ob in obs]
+            C = max(leng)
+            vp = np.array([ob["_vp_index"] for ob in obs], np.int64)
+            view = np.array([ob["viewIndex"] for ob in obs], np.int64)
+            ia_v.append((vp[:, None] * NUM_VIEWS + r36[None]).astype(np.int32).reshape(-1))
+            ib_v.append((view[:, None] * NUM_VIEWS + r36[None]).astype(np.int32).reshape(-1))
+            iac = np.full((B, C), -1, np.int32)
+            ibc = np.full((B, C), -1, np.int32)
+            cang = np.zeros((B, C, A), np.float32)
+            a_t = np.zeros((B, A), np.float32)
+            base = sum(x.shape[0] for x in cangs)
+            for i, ob in enumerate(obs):
+                a_t[i] = angle_feature(ob["heading"], ob["elevation"], A)
+                for j, c in enumerate(ob["candidate"]):
+                    iac[i, j] = vp[i] * NUM_VIEWS + c["pointId"]
+                    ibc[i, j] = base + i * C + j
+                    cang[i, j] = c["angle"] if "angle" in c else c["feature"][-A:]
+            ia_c.append(iac.reshape(-1))
+            ib_c.append(ibc.reshape(-1))
+            cangs.append(cang.reshape(B * C, A))
+            a_ts.append(a_t)
+            cinfo.append((row, C, leng))
+            row += B * C
+        ia_v, ib_v = np.concatenate(ia_v), np.concatenate(ib_v)
+        ia_c, ib_c = np.concatenate(ia_c), np.concatenate(ib_c)
+        a_t, cang = np.concatenate(a_ts), np.concatenate(cangs)
+        ints = torch.from_numpy(np.concatenate([ia_v, ib_v, ia_c, ib_c])).pin_memory()
         flts = torch.from_numpy(np.concatenate([a_t.reshape(-1), cang.reshape(-1)])).pin_memory()
         ints = ints.to(self.device, non_blocking=True)
         flts = flts.to(self.device, non_blocking=True)
-        n = B * NUM_VIEWS
+        N, R = a_t.shape[0], ia_c.shape[0]
+        n = N * NUM_VIEWS
         ia_v_d, ib_v_d = ints[:n], ints[n:2 * n]
-        ia_c_d, ib_c_d = ints[2 * n:2 * n + B * C], ints[2 * n + B * C:]
-        a_t_d = flts[:B * A].view(B, A)
-        cang_d = flts[B * A:].view(B * C, A)
+        ia_c_d, ib_c_d = ints[2 * n:2 * n + R], ints[2 * n + R:]
+        a_t_d = flts[:N * A].view(N, A)
+        cang_d = flts[N * A:].view(R, A)
         F = FEATURE_SIZE + A
-        f_t = torch.empty(B, NUM_VIEWS, F, dtype=torch.float32, device=self.device)
+        f_t = torch.empty(N, NUM_VIEWS, F, dtype=torch.float32, device=self.device)
         d_t = torch.empty_like(f_t)
-        cf = torch.empty(B, C, F, dtype=torch.float32, device=self.device)
+        cf = torch.empty(R, F, dtype=torch.float32, device=self.device)
         cd = torch.empty_like(cf)
         ops.gather_rows(self.rgb, ia_v_d, self.angles, ib_v_d, f_t)
         ops.gather_rows(self.depth, ia_v_d, self.angles, ib_v_d, d_t)
         ops.gather_rows(self.rgb, ia_c_d, cang_d, ib_c_d, cf)
         ops.gather_rows(self.depth, ia_c_d, cang_d, ib_c_d, cd)
-        return a_t_d, f_t, d_t, cf, cd, leng
+        return a_t_d, f_t, d_t, cf, cd, cinfo
 
 
 def _device_input_feat(self, obs, device):
@@ -476,4 +527,11 @@ def _device_input_feat(self, obs, device):
     return self._store.input_feat(obs)
 
 
+def _device_input_feat_steps(self, obs_steps, device):
+    if self._store is None or self._store.device != device:
+        self._store = DeviceFeatureStore(self.world, device, self.angle_feat_size)
+    return self._store.input_feat_steps(obs_steps)
+
+
 SynthR2RBatch.device_input_feat = _device_input_feat
+SynthR2RBatch.device_input_feat_steps = _device_input_feat_steps

@@ -92,11 +92,15 @@ int dasa_mha_bwd(const float* Q, int64_t ldq, const float* K, int64_t ldk, const
 
 /* ---- SoftDot / ShiftSoftDot attention (model.py:253-353) ------------------------------------
  * q [B][D] is linear_in(h) (computed by dasa_gemm_f32); ctx [B][N][ldn] (ldn >= D, batch stride
- * N*ldn); mask [B][N] uint8 (1 = masked -> -inf) or NULL. Outputs any of scores [B][N] (raw
- * logits, output_prob=False), probs [B][N], wctx [B][D].                                         */
+ * N*ldn, D <= 4096); mask [B][N] uint8 (1 = masked -> -inf) or NULL. Outputs any of scores [B][N]
+ * (raw logits, output_prob=False), probs [B][N], wctx [B][D].
+ * ws: dasa_attn_workspace(B, N, D) bytes, 16-B aligned, shared by the four calls below (B <= 32768);
+ * its first 65536 32-bit words are arrival counters that must be ZERO on entry (calls leave them
+ * zero), so a caller zeroes the buffer once and reuses it on one stream for calls of any shape.  */
+int64_t dasa_attn_workspace(int32_t B, int32_t N, int32_t D);
 int dasa_softdot_fwd(const float* q, const float* ctx, int64_t ldn, const uint8_t* mask,
                      float* scores, float* probs, float* wctx,
-                     int32_t B, int32_t N, int32_t D, void* stream);
+                     int32_t B, int32_t N, int32_t D, float* ws, void* stream);
 /* Backward. dwctx [B][D] and/or dscores [B][N] (grad of raw logits); writes dq [B][D] and
  * dctx [B][N][ldn] (dctx += if accumulate; either may be NULL). probs are the forward's saved
  * softmax (for output_prob=False callers pass the softmax anyway; only dscores flows then).     */
@@ -113,7 +117,6 @@ int dasa_shift_attn_bwd(const float* q, const float* ctx, int64_t ldn, const flo
                         const float* shifted, const float* wsm, const float* dwctx,
                         float* dq, float* dctx, float* dshift_logits, int32_t accumulate,
                         int32_t B, int32_t D, int32_t K, float* ws, void* stream);
-/* Workspace for the three calls above: B*N floats (N = 36 for the shift attention). */
 
 /* ---- LSTM (model.py:437 nn.LSTMCell, r2rmodel.py:2241 nn.LSTM) ------------------------------ */
 /* gates [B][4H] = x W_ih^T + b_ih + h W_hh^T + b_hh (PyTorch order i,f,g,o) -> h, c.

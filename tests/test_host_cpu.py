@@ -123,3 +123,56 @@ def test_dropin_launcher_binds_reference_module_names(tmp_path, monkeypatch):
                        cwd=str(tmp_path), capture_output=True, text=True, timeout=300,
                        env=dict(os.environ, PYTHONPATH=ROOT))
     assert r.returncode == 0 and "DROPIN-OK" in r.stdout, r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("mode,seed", [("goal", 8), ("wander", 1000)])
+def test_teacher_plan_matches_stepwise_oracle(mode, seed):
+    """Seq2SeqAgent._teacher_plan (env stepped through a whole teacher-forced episode before the
+    batched encoder runs) yields, step by step, the targets, ended flags, rewards and masks of the
+    oracle's interleaved loop (agent_dg.py:832-936 restated in oracle/policy.py)."""
+    from dasa_amd.r2r import param
+    from dasa_amd.r2r.agent_dg import Seq2SeqAgent
+    from dasa_amd.synth import SynthR2RBatch, SynthWorld
+    from oracle import policy as O
+    param.readme_train(["--d_vl_layers", "1", "--batchSize", "6", "--maxAction", "8"])
+    world = SynthWorld(24, 0, 3)
+    env = SynthR2RBatch(world, 6, seed=seed, mode=mode, instr_len=80, variable_len=True)
+    env2 = SynthR2RBatch(world, 6, seed=seed, mode=mode, instr_len=80, variable_len=True)
+    ag = object.__new__(Seq2SeqAgent)
+    ag.env, ag.episode_len = env, 8
+    obs = np.array(env.reset())
+    _, _, _, perm_idx = O.sort_batch(obs)
+    perm_obs = obs[perm_idx]
+    last = np.array([ob["distance"] for ob in perm_obs], np.float32)
+    ended = np.zeros(6, bool)
+    traj = [{"path": []} for _ in perm_obs]
+    plan, final_obs = ag._teacher_plan(perm_obs, list(perm_idx), ended, last, traj, 3)
+    more, final_obs = ag._teacher_plan(final_obs, list(perm_idx), ended, last, traj, 5)
+    plan = plan + more
+    # the oracle's loop, teacher feedback
+    obs2 = np.array(env2.reset())
+    po = obs2[perm_idx]
+    last2 = np.array([ob["distance"] for ob in po], np.float32)
+    ended2 = np.zeros(6, bool)
+    for t in range(8):
+        tgt = O.teacher_action(po, ended2).numpy()
+        assert t < len(plan)
+        np.testing.assert_array_equal(plan[t]["target_np"], tgt)
+        np.testing.assert_array_equal(plan[t]["ended"], ended2)
+        cpu_a = tgt.copy()
+        for i, nid in enumerate(cpu_a):
+            if nid == len(po[i]["candidate"]) or nid == -100:
+                cpu_a[i] = -1
+        O.make_equiv_action(env2, cpu_a, po, perm_idx, [[ob["viewpoint"]] for ob in po])
+        po = np.array(env2._get_obs())[perm_idx]
+        d = np.array([ob["distance"] for ob in po], np.float32)
+        rew = np.where(ended2, 0.0, np.where(cpu_a == -1, np.where(d < 3, 2.0, -2.0), np.sign(last2 - d)))
+        np.testing.assert_array_equal(plan[t]["reward"], rew.astype(np.float32))
+        np.testing.assert_array_equal(plan[t]["mask"], (~ended2).astype(np.float32))
+        last2 = d
+        ended2 = ended2 | (cpu_a == -1)
+        if ended2.all():
+            break
+    assert len(plan) == t + 1
+    np.testing.assert_array_equal(ended, ended2)
+    assert [ob["viewpoint"] for ob in final_obs] == [ob["viewpoint"] for ob in po]

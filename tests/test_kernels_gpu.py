@@ -192,6 +192,40 @@ def test_softdot_shift_backward(dev):
     assert (dctx.cpu() - c2.grad).abs().max() < 1e-5 * max(1, c2.grad.abs().max())
 
 
+@pytest.mark.parametrize("B,N,D,ldn", [(1, 1, 2176, 2176), (3, 7, 2048, 2176), (37, 16, 2176, 2176),
+                                         (2, 80, 2048, 2048), (2, 100, 1024, 1024), (2, 9, 4096, 4096),
+                                         (4, 36, 2176, 2176)])
+def test_softdot_fused_shapes(dev, B, N, D, ldn):
+    """The one-launch SoftDot kernels over row counts around the 12/16-row passes, N > 64, strided
+    rows (a 2048-column view of 2176-float rows), D = 4096 (1024 threads), B = 1."""
+    from dasa_amd import ops
+    g = torch.Generator().manual_seed(N * 1000 + D)
+    q = _rand(B, D, g=g, scale=0.05).double()
+    full = torch.rand(B, N, ldn, generator=g).double()
+    ctx = full[:, :, :D]
+    mask = torch.rand(B, N, generator=g) < 0.3
+    mask[:, 0] = False
+    gw, gs = _rand(B, D, g=g).double(), _rand(B, N, g=g).double()
+    qr, cr = q.clone().requires_grad_(), ctx.clone().requires_grad_()
+    s = torch.einsum("bnd,bd->bn", cr, qr)
+    p = torch.softmax(s.masked_fill(mask, -float("inf")), 1)
+    w = torch.einsum("bn,bnd->bd", p, cr)
+    ((w * gw).sum() + (s * gs).sum()).backward()
+    fd = full.float().to(dev)
+    cd = fd[:, :, :D]
+    sc, pr, wc = ops.softdot_fwd(q.float().to(dev), cd, mask.to(dev))
+    assert (sc.cpu().double() - s).abs().max() < 1e-4
+    assert (pr.cpu().double() - p).abs().max() < 1e-5
+    assert (wc.cpu().double() - w).abs().max() < 1e-4
+    cc = cd.contiguous()
+    dq, dctx = ops.softdot_bwd(q.float().to(dev), cc, pr, dwctx=gw.float().to(dev), dscores=gs.float().to(dev))
+    assert (dq.cpu().double() - qr.grad).abs().max() < 2e-4 * max(1, qr.grad.abs().max())
+    assert (dctx.cpu().double() - cr.grad).abs().max() < 1e-5 * max(1, cr.grad.abs().max())
+    # scores only (the candidate-logit path) and its dscores-only backward
+    sc2, _, _ = ops.softdot_fwd(q.float().to(dev), cd, None, want_probs=False, want_wctx=False)
+    assert (sc2.cpu().double() - s.detach()).abs().max() < 1e-4
+
+
 def test_lstm_cell(dev):
     from dasa_amd import ops
     g = torch.Generator().manual_seed(17)
@@ -291,3 +325,19 @@ def test_adain_musigma_reverse_dropout(dev):
     assert abs(keep - 0.6) < 0.01 and torch.allclose(y[y > 0], torch.full_like(y[y > 0], 1 / 0.6))
     y2 = ops.dropout(torch.ones(100, 1000, device=dev), 0.4, 1234).cpu()
     assert torch.equal(y, y2)
+    # the float4 path and the scalar path (misaligned rows) draw the same (seed, r * cols + c) mask
+    buf = torch.ones(100, 1008, device=dev)
+    y3 = ops.dropout(buf[:, 1:1001], 0.4, 1234).cpu()
+    assert torch.equal(y, y3)
+    # mu/sigma AdaIN on strided 2176-float rows (the register path) and a non-2048 width (generic path)
+    cf, sf = torch.rand(40, 2176, generator=g), torch.rand(40, 2176, generator=g)
+    mc, sc = ms(cf[:, :2048])
+    mss, sss = ms(sf[:, :2048])
+    outf = torch.zeros(40, 2176, device=dev)
+    ops.adain_musigma(cf.to(dev)[:, :2048], sf.to(dev)[:, :2048], out=outf[:, :2048])
+    assert (outf[:, :2048].cpu() - ((cf[:, :2048] - mc) / sc * sss + mss)).abs().max() < 1e-4
+    assert (outf[:, 2048:] == 0).all()
+    c3, s3 = torch.rand(5, 1000, generator=g), torch.rand(5, 1000, generator=g)
+    mc, sc = ms(c3)
+    mss, sss = ms(s3)
+    assert (ops.adain_musigma(c3.to(dev), s3.to(dev)).cpu() - ((c3 - mc) / sc * sss + mss)).abs().max() < 1e-4

@@ -232,6 +232,47 @@ def test_train_iteration_grads(R, dev, deferred):
     assert n == 30
 
 
+@pytest.mark.parametrize("batched", ["1", "0"])
+def test_cfg2_teacher_rollout_vs_oracle(R, dev, monkeypatch, batched):
+    """A 3-step teacher-forced eval rollout at the cfg2 shape (B=20, L=80, vl=3, C<=16) against the CPU
+    oracle, per step. batched=1: the encoder runs once over all steps (the train path's teacher
+    rollout); batched=0: the step-by-step loop."""
+    from oracle import policy as O
+    from tests.helpers import oracle_weights
+    monkeypatch.setenv("DASA_TEACHER_BATCH", batched)
+    param = R[0]
+    param.readme_train(["--d_vl_layers", "3"])
+    T = 3
+    try:
+        world = SynthWorld(32, 0, 5)
+        env = SynthR2RBatch(world, 20, seed=11, mode="wander", instr_len=80)
+        env2 = SynthR2RBatch(world, 20, seed=11, mode="wander", instr_len=80)
+        ag = _agent(R, env, T)
+        W = oracle_weights(3)
+        rec = {"logit": [], "h_tilde": []}
+        fwd = ag.decoder.forward
+
+        def wrap(*a, **k):
+            r = fwd(*a, **k)
+            rec["logit"].append(r[2].detach().cpu())
+            rec["h_tilde"].append(r[3].detach().cpu())
+            return r
+        ag.decoder.forward = wrap
+        ag.loss = 0
+        ag.feedback = "teacher"
+        for m in (ag.encoder, ag.decoder, ag.critic):
+            m.eval()
+        with torch.no_grad():
+            ag.vl_rollout(train_ml=None, train_rl=False, reset=True)
+            r = O.vl_rollout(W, env2, "teacher", la_layers=9, vl_layers=3, episode_len=T)
+        assert len(rec["logit"]) == r["steps"] == T
+        for t in range(T):
+            close(rec["logit"][t], r["logits"][t], TOL, f"cfg2 logit {t}")
+            close(rec["h_tilde"][t], r["states"][t][2], TOL, f"cfg2 h_tilde {t}")
+    finally:
+        param.readme_train(["--d_vl_layers", "1", "--batchSize", "2", "--maxAction", "5"])
+
+
 def test_cfg2_step_vs_oracle(R, dev):
     """One eval policy step at the cfg2 shape (B=20, L=80, vl=3, C<=16) against the CPU oracle."""
     from oracle import policy as O
