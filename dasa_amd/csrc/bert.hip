@@ -214,59 +214,75 @@ struct MhaArgs {
   int B, heads, Lq, Lk; float scale; float p; uint64_t seed;
 };
 
-// Forward on matrix cores (v_mfma_f32_32x32x2_f32), one wave per (batch, head, 32-query tile), no
-// LDS and no workgroup barriers. The wave computes S^T = K Q^T (keys on the rows/registers, queries
-// on the lanes), so the softmax over keys is an in-lane reduction plus one cross-half shuffle, and
-// the probability tile, as it sits in the accumulator, is directly the A operand of O = P V (an
-// MFMA summing over the accumulator's row index takes it with no lane movement: register r of lane
-// half hh holds key (r&3) + 8(r>>2) + 4hh, and the V operand is loaded for exactly that key).
-// NKT = ceil(Lk / 32) key tiles (Lk <= 128).
+// Forward on matrix cores (v_mfma_f32_32x32x2_f32): one workgroup per (batch, head), one wave per
+// 32-query tile. The head's K and V rows ([Lk][64] each, <= 48 KB) are staged in LDS once by the whole
+// workgroup with float4 loads (rows padded to 68 floats: conflict-free ds_read_b128 fragments) and
+// shared by the query-tile waves; the per-MFMA operand reads of K (S^T) and V (P V) are then LDS reads
+// instead of dependent global loads. Each wave computes S^T = K Q^T (keys on the accumulator rows,
+// queries on the lanes), so the softmax over keys is an in-lane reduction plus one cross-half
+// shuffle, and the probability tile as it sits in the accumulator is directly the A operand of
+// O = P V (register r of lane half hh holds key (r&3) + 8(r>>2) + 4hh; the V operand is read for
+// exactly that key). NKT = ceil(Lk / 32) key tiles (Lk <= 128).
 __device__ __forceinline__ int acc_row(int r, int hh) { return (r & 3) + 8 * (r >> 2) + 4 * hh; }
+
+constexpr int kKvLd = kDh + 4;   // LDS row stride of the staged K / V (floats)
 
 template <int NKT>
 __global__ __launch_bounds__(256) void mha_fwd_kernel(MhaArgs a, int nqt) {
+  __shared__ __attribute__((aligned(16))) float kv[2 * NKT * 32 * kKvLd + NKT * 32];
+  float* Ks = kv;
+  float* Vs = kv + NKT * 32 * kKvLd;
+  float* Ms = kv + 2 * NKT * 32 * kKvLd;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const long wid = (long)blockIdx.x * 4 + w;
-  if (wid >= (long)a.B * a.heads * nqt) return;   // whole waves only; no barriers below
-  const int qt = (int)(wid % nqt);
-  const long bh = wid / nqt;
-  const int h = (int)(bh % a.heads), b = (int)(bh / a.heads);
-  const int Lq = a.Lq, Lk = a.Lk, q0 = qt * 32;
+  const int bh = blockIdx.x;
+  const int h = bh % a.heads, b = bh / a.heads;
+  const int Lq = a.Lq, Lk = a.Lk;
+  // stage K / V rows (zero past Lk) and the additive key mask
+  for (int idx = threadIdx.x; idx < NKT * 32 * (kDh / 4); idx += blockDim.x) {
+    const int row = idx / (kDh / 4), c4 = idx % (kDh / 4);
+    float4 kx = make_float4(0.f, 0.f, 0.f, 0.f), vx = kx;
+    if (row < Lk) {
+      kx = reinterpret_cast<const float4*>(a.K + ((long)b * Lk + row) * a.ldk + h * kDh)[c4];
+      vx = reinterpret_cast<const float4*>(a.V + ((long)b * Lk + row) * a.ldv + h * kDh)[c4];
+    }
+    *reinterpret_cast<float4*>(Ks + row * kKvLd + 4 * c4) = kx;
+    *reinterpret_cast<float4*>(Vs + row * kKvLd + 4 * c4) = vx;
+  }
+  for (int k = threadIdx.x; k < NKT * 32; k += blockDim.x)
+    Ms[k] = k < Lk ? (a.mask ? a.mask[(long)b * Lk + k] : 0.f) : -INFINITY;
+  const int qt = w, q0 = qt * 32;
   const int j = lane & 31, hh = lane >> 5;
   // B operand of S^T: Q^T, lane (query j, half hh) holds Q[q0 + j][8g + 4hh .. +3] (K-permuted)
   const float* qp = a.Q + ((long)b * Lq + min(q0 + j, Lq - 1)) * a.ldq + h * kDh + 4 * hh;
   float4 qf[8];
 #pragma unroll
   for (int g = 0; g < 8; ++g) qf[g] = *reinterpret_cast<const float4*>(qp + 8 * g);
+  __syncthreads();
+  if (qt >= nqt) return;   // (no barrier below)
   floatx16 st[NKT];
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt) {
-    const float* kp = a.K + ((long)b * Lk + min(kt * 32 + j, Lk - 1)) * a.ldk + h * kDh + 4 * hh;
-    float4 kf[8];
-#pragma unroll
-    for (int g = 0; g < 8; ++g) kf[g] = *reinterpret_cast<const float4*>(kp + 8 * g);
+    const float* kp = Ks + (kt * 32 + j) * kKvLd + 4 * hh;
     floatx16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 #pragma unroll
     for (int g = 0; g < 8; ++g) {
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(kf[g].x, qf[g].x, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(kf[g].y, qf[g].y, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(kf[g].z, qf[g].z, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(kf[g].w, qf[g].w, acc, 0, 0, 0);
+      const float4 kf = *reinterpret_cast<const float4*>(kp + 8 * g);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(kf.x, qf[g].x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(kf.y, qf[g].y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(kf.z, qf[g].z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(kf.w, qf[g].w, acc, 0, 0, 0);
     }
     st[kt] = acc;
   }
   // scale + additive key mask; keys past Lk -> -inf
-  const float* mrow = a.mask ? a.mask + (long)b * Lk : nullptr;
   float m = -INFINITY;
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int key = kt * 32 + acc_row(r, hh);
-      const float mk = mrow ? mrow[min(key, Lk - 1)] : 0.f;
-      const float v = key < Lk ? st[kt][r] * a.scale + mk : -INFINITY;
+      const float v = st[kt][r] * a.scale + Ms[kt * 32 + acc_row(r, hh)];
       st[kt][r] = v;
       m = fmaxf(m, v);
     }
@@ -283,7 +299,7 @@ __global__ __launch_bounds__(256) void mha_fwd_kernel(MhaArgs a, int nqt) {
   sum += __shfl_xor(sum, 32);
   const float inv = 1.f / sum;
   const int q = q0 + j;
-  const long prow = (bh * Lq + q) * (long)Lk;   // probs / dropout index base of this query row
+  const long prow = ((long)bh * Lq + q) * (long)Lk;   // probs / dropout index base of this query row
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
@@ -298,12 +314,11 @@ __global__ __launch_bounds__(256) void mha_fwd_kernel(MhaArgs a, int nqt) {
   floatx16 o0, o1;
 #pragma unroll
   for (int r = 0; r < 16; ++r) { o0[r] = 0.f; o1[r] = 0.f; }
-  const float* vb = a.V + (long)b * Lk * a.ldv + h * kDh + j;
 #pragma unroll
   for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float* vr = vb + (long)min(kt * 32 + acc_row(r, hh), Lk - 1) * a.ldv;
+      const float* vr = Vs + (kt * 32 + acc_row(r, hh)) * kKvLd + j;
       o0 = __builtin_amdgcn_mfma_f32_32x32x2f32(st[kt][r], vr[0], o0, 0, 0, 0);
       o1 = __builtin_amdgcn_mfma_f32_32x32x2f32(st[kt][r], vr[32], o1, 0, 0, 0);
     }
@@ -536,10 +551,13 @@ extern "C" int dasa_mha_fwd(const float* Q, int64_t ldq, const float* K, int64_t
                             int32_t Lq, int32_t Lk, int32_t dh, float scale, float drop_p, uint64_t seed,
                             void* stream) {
   if (B <= 0 || Lq <= 0) return 0;
-  if (dh != kDh || Lk <= 0 || Lk > kMaxLk) return (int)hipErrorInvalidValue;
+  if (dh != kDh || Lk <= 0 || Lk > kMaxLk || ((ldq | ldk | ldv) & 3) ||
+      (((uintptr_t)Q | (uintptr_t)K | (uintptr_t)V) & 15))
+    return (int)hipErrorInvalidValue;
   MhaArgs a{Q, ldq, K, ldk, V, ldv, addmask, out, ldo, probs, B, heads, Lq, Lk, scale, drop_p, seed};
   const int nqt = cdivi(Lq, 32);
-  const dim3 grid(cdivi((long)B * heads * nqt, 4)), block(256);
+  if (nqt > 4) return (int)hipErrorInvalidValue;   // one wave per 32-query tile, Lq <= 128
+  const dim3 grid(B * heads), block(64 * nqt);
   hipStream_t st = (hipStream_t)stream;
   switch (cdivi(Lk, 32)) {
     case 1: hipLaunchKernelGGL(mha_fwd_kernel<1>, grid, block, 0, st, a, nqt); break;

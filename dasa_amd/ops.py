@@ -433,6 +433,23 @@ def lstm_cell_bwd(act, c_prev, c, dh, dc):
     return dgates, dc_prev
 
 
+_CONCURRENT = []
+
+
+def register_concurrent_stream(st):
+    """A stream that may run kernels beside the main stream (the train-mode language pipe). The
+    persistent bi-LSTM kernels need every CU, so their launches first join every such stream."""
+    if all(st is not s for s in _CONCURRENT):
+        _CONCURRENT.append(st)
+
+
+def _exclusive(dev):
+    cur = torch.cuda.current_stream(dev)
+    for st in _CONCURRENT:
+        if st.device == dev and st != cur:
+            cur.wait_stream(st)
+
+
 def bilstm_fwd(xproj, whh_f, whh_b, lengths_i32, H, save=False):
     """xproj [B, L, 2, 4H]; whh_f/whh_b [4H, H]; lengths int32 [B] (device). Returns out [B, L, 2H],
     h_n [2, B, H], c_n [2, B, H], saved (act, c) or None."""
@@ -447,6 +464,7 @@ def bilstm_fwd(xproj, whh_f, whh_b, lengths_i32, H, save=False):
         sc = torch.empty(L, 2, B, H, dtype=torch.float32, device=dev)
     L_ = _lib.lib()
     ws = torch.empty(L_.dasa_bilstm_workspace(B, H) // 4, dtype=torch.float32, device=dev)
+    _exclusive(dev)
     _call("dasa_bilstm_fwd", "bilstm", L_.dasa_bilstm_fwd, _p(xproj.contiguous()), _p(whh_f.contiguous()),
           _p(whh_b.contiguous()), _p(lengths_i32), _p(out), _p(h_n), _p(c_n), _p(sa), _p(sc), B, L, H, _p(ws), _stream(),
           flops=2.0 * 2 * L * B * 4 * H * H, nbytes=4.0 * L * 2 * 4 * H * H)
@@ -459,6 +477,7 @@ def bilstm_bwd(whh_f, whh_b, lengths_i32, saved, dout, dh_n, dc_n, H):
     dev = sa.device
     dgates = torch.empty(B, L, 2, 4 * H, dtype=torch.float32, device=dev)
     ws = torch.empty(_lib.lib().dasa_bilstm_bwd_workspace(B, H) // 4 + 4, dtype=torch.float32, device=dev)
+    _exclusive(dev)
     _call("dasa_bilstm_bwd", "bilstm_bptt", _lib.lib().dasa_bilstm_bwd, _p(whh_f.contiguous()), _p(whh_b.contiguous()),
           _p(lengths_i32), _p(sa), _p(sc), _p(dout.contiguous()),
           _p(dh_n.contiguous() if dh_n is not None else None),

@@ -596,7 +596,6 @@ class Seq2SeqAgent(BaseAgent):
                     cpu_a_t = target_np.copy()           # a_t is target: its host copy, no device round trip
                 else:
                     cpu_a_t = a_t.cpu().numpy().copy()  # the step's one device->host sync
-                self.encoder.lang_pump(2)                 # GPU work for the coming steps while the host steps the env
                 for i, next_id in enumerate(cpu_a_t):
                     if next_id == (candidate_leng[i] - 1) or next_id == args.ignoreid:
                         cpu_a_t[i] = -1

@@ -31,9 +31,27 @@ class ReverseFn(torch.autograd.Function):
         return ops.reverse_valid(dy.contiguous(), lens), None
 
 
+_LANG_STREAMS = {}
+
+
+def _lang_stream(device):
+    st = _LANG_STREAMS.get(device.index)
+    if st is None:
+        st = torch.cuda.Stream(device=device)
+        _LANG_STREAMS[device.index] = st
+        ops.register_concurrent_stream(st)   # joined before every persistent bi-LSTM launch
+    return st
+
+
 class _LangPipe:
     """Language stack of the coming rollout steps, computed in chunks of `chunk` steps, one unit
-    (embeddings, then each BertLayer) per pump() call. Outputs come out in step order."""
+    (embeddings, then each BertLayer) per pump() call. Outputs come out in step order.
+
+    The units run on their own HIP stream, gated behind an event the encoder records after it
+    launched the step's bi-LSTM: they overlap the decoder, the host's env step and the next step's
+    latency-bound LXRT layers instead of sitting between them on the main stream. Every bi-LSTM
+    launch joins the pipe stream first (ops.register_concurrent_stream), because the persistent
+    recurrence kernel must have every CU to itself."""
 
     def __init__(self, bert, ids, att_mask, steps, chunk):
         self.bert = bert
@@ -41,16 +59,20 @@ class _LangPipe:
         self.ext = ((1.0 - att_mask.float()) * -10000.0).unsqueeze(1).unsqueeze(2)
         self.budget = steps
         self.chunk = chunk
-        self.ready = []
+        self.ready = []          # (output [B, L, H], event recorded on the pipe stream)
         self.cur = None
+        self.stream = _lang_stream(ids.device)
+        self.stream.wait_stream(torch.cuda.current_stream())
 
-    def pump(self, units):
+    def pump(self, units, gate=None):
         bert = self.bert
-        with torch.no_grad():
+        if gate is not None:
+            self.stream.wait_event(gate)
+        with torch.no_grad(), torch.cuda.stream(self.stream):
             while units > 0:
                 if self.cur is None:
                     if self.budget <= 0:
-                        return
+                        break
                     S = min(self.chunk, self.budget)
                     self.budget -= S
                     self.cur = [S, None, 0, self.ids.repeat(S, 1), self.ext.repeat(S, 1, 1, 1)]
@@ -60,7 +82,9 @@ class _LangPipe:
                 units -= 1
                 if k == len(bert.lalayer) + 1:
                     B, L = self.ids.shape
-                    self.ready.extend(x.view(S, B, L, x.shape[-1]).unbind(0))
+                    ev = torch.cuda.Event()
+                    ev.record(self.stream)
+                    self.ready.extend((o, ev) for o in x.view(S, B, L, x.shape[-1]).unbind(0))
                     self.cur = None
                 else:
                     self.cur = [S, x, k, ids, ext]
@@ -70,7 +94,11 @@ class _LangPipe:
             if self.cur is None and self.budget <= 0:
                 return None
             self.pump(1)
-        return self.ready.pop(0)
+        out, ev = self.ready.pop(0)
+        main = torch.cuda.current_stream()
+        main.wait_event(ev)
+        out.record_stream(main)
+        return out
 
 
 class DicEncoder(nn.Module):
@@ -117,6 +145,7 @@ class DicEncoder(nn.Module):
         self._lang_cache = None
         # train-mode language pipeline (see cache_language)
         self.lang_chunk = int(os.environ.get("DASA_LANG_CHUNK", "8"))
+        self.lang_units = int(os.environ.get("DASA_LANG_UNITS", "2"))   # pipe units pumped per encoder call
         self._lang_steps = 0
         self._lang_pipe = None
 
@@ -135,6 +164,8 @@ class DicEncoder(nn.Module):
         self._lang_pipe = None
 
     def lang_pump(self, units=2):
+        """Advance the train-mode language pipe by `units` (kept for callers; the encoder itself pumps
+        two units behind every bi-LSTM launch)."""
         if self._lang_pipe is not None:
             self._lang_pipe.pump(units)
 
@@ -172,9 +203,14 @@ class DicEncoder(nn.Module):
         if self.reverse_input:
             embeds = ReverseFn.apply(embeds.contiguous(), lens_i32)
         l = self.lstm
+        pipe = self._lang_pipe
         out, h_n, c_n = DF.BiLSTMFn.apply(embeds.contiguous(), lens_i32, l.weight_ih_l0, l.weight_hh_l0, l.bias_ih_l0,
                                           l.bias_hh_l0, l.weight_ih_l0_reverse, l.weight_hh_l0_reverse,
                                           l.bias_ih_l0_reverse, l.bias_hh_l0_reverse)
+        if pipe is not None:
+            gate = torch.cuda.Event()
+            gate.record(torch.cuda.current_stream())
+            pipe.pump(self.lang_units, gate)
         h_t = torch.cat((h_n[1], h_n[0]), 1)          # (enc_h_t[-1], enc_h_t[-2]) = [bwd, fwd]
         c_t = torch.cat((c_n[1], c_n[0]), 1)
         decoder_init = DF.linear(h_t, self.encoder_lstm2decoder_ht.weight, self.encoder_lstm2decoder_ht.bias, "tanh")

@@ -78,7 +78,8 @@ int dasa_bert_embed_fwd(const int64_t* ids, const float* word, const float* pos,
 
 /* Masked multi-head attention core (BertSelfAttention / BertOutAttention, vilmodel.py:214-236,
  * 481-506): ctx = softmax(Q K^T * scale + addmask[b, k]) V per head; Q/K/V/out row-major with
- * heads interleaved as [.., heads*dh]. addmask: [B][Lk] additive (-10000 for pads) or NULL. */
+ * heads interleaved as [.., heads*dh]. addmask: [B][Lk] additive (-10000 for pads) or NULL.
+ * dh = 64, Lq <= 128, Lk <= 128; Q/K/V 16-B aligned with ld % 4 == 0.                       */
 int dasa_mha_fwd(const float* Q, int64_t ldq, const float* K, int64_t ldk, const float* V, int64_t ldv,
                  const float* addmask, float* out, int64_t ldo, float* probs,
                  int32_t B, int32_t heads, int32_t Lq, int32_t Lk, int32_t dh, float scale,
