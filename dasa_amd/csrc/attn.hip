@@ -79,7 +79,6 @@ __device__ __forceinline__ float reduce_scatter16(const float (&v)[16], int lane
 // Partials handed to another workgroup of the same launch are stored write-through (sc1) and every
 // load of them is sc1, so the hand-off needs no L2-wide release / acquire fence (gfx950's L2 is
 // per XCD): writers drain vmcnt, then one lane takes a relaxed agent-scope ticket.
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t ws_rsrc(float* ws) {
   return __builtin_amdgcn_make_buffer_rsrc(ws, 0, 0x7fffffff, 0x00020000);
 }

@@ -7,6 +7,7 @@
 #define DASA_WAVE 64
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 #define DASA_CHECK_LAUNCH()                                   \

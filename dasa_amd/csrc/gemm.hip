@@ -11,6 +11,7 @@
 // Split-K over gridDim.z with a deterministic fixed-order reduce for skinny (M<=64) decoder GEMMs.
 #include "common.h"
 #include <cstdlib>
+#include <type_traits>
 #include "../../include/dasa_hip.h"
 
 namespace {
@@ -156,6 +157,94 @@ __device__ __forceinline__ float f4get(const float4& v, int e) {
   return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w;
 }
 
+// Fused epilogue of one wave's TM x TN accumulators of MF x MF MFMA tiles (MF = 32: floatx16,
+// MF = 16: floatx4) at block origin (m0, n0), wave offset (wm, wn). C/D map: col = lane & (MF-1);
+// row = (r&3) + 8*(r>>2) + 4*(lane>>5) for 32x32, row = 4*(lane>>4) + r for 16x16.
+// Every optional operand is fetched with unconditional clamped loads inside ONE uniform branch per
+// operand (a per-element branch around a load makes hipcc wait vmcnt(0) per element).
+template <int MF, int TM, int TN, int BM, int BN, typename AccT>
+__device__ __forceinline__ void store_tile_mf(const GemmP& p, AccT (&acc)[TM][TN], int b, int split, int m0,
+                                              int n0, int wm, int wn, int lane) {
+  constexpr int NR = MF == 32 ? 16 : 4;
+  const bool full_tile = (m0 + BM <= p.M) && (n0 + BN <= p.N);
+  auto rowof = [&](int rbase, int r) { return MF == 32 ? rbase + (r & 3) + 8 * (r >> 2) : rbase + r; };
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + wn + j * MF + (lane & (MF - 1));
+    const int colc = min(col, p.N - 1);
+    float bj = 0.f, cs = 1.f;
+    if (p.splitk == 1) {
+      if (p.bias) bj = p.bias[colc];
+      if (p.colscale) cs = p.colscale[colc];
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int rbase = m0 + wm + i * MF + (MF == 32 ? 4 * (lane >> 5) : 4 * (lane >> 4));
+      if (p.splitk > 1) {
+        float* ws = p.ws + ((long)split * p.batch + b) * p.M * p.N;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          const int row = rowof(rbase, r);
+          if (full_tile || (row < p.M && col < p.N)) ws[(long)row * p.N + col] = acc[i][j][r];
+        }
+        continue;
+      }
+      float v[NR];
+#pragma unroll
+      for (int r = 0; r < NR; ++r) v[r] = p.alpha * acc[i][j][r] + bj;
+      switch (p.act) {   // one uniform branch per tile, not per element
+        case DASA_ACT_RELU:
+#pragma unroll
+          for (int r = 0; r < NR; ++r) v[r] = fmaxf(v[r], 0.f);
+          break;
+        case DASA_ACT_GELU:
+#pragma unroll
+          for (int r = 0; r < NR; ++r) v[r] = gelu_erf(v[r]);
+          break;
+        case DASA_ACT_TANH:
+#pragma unroll
+          for (int r = 0; r < NR; ++r) v[r] = tanhf(v[r]);
+          break;
+        case DASA_ACT_SIGMOID:
+#pragma unroll
+          for (int r = 0; r < NR; ++r) v[r] = sigmoidf_(v[r]);
+          break;
+        default:
+          break;
+      }
+      if (p.aux) {
+        const float* ab = p.aux + (long)b * p.sAux;
+        float av[NR];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) av[r] = ab[(long)min(rowof(rbase, r), p.M - 1) * p.ld_aux + colc];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) v[r] *= av[r];
+      }
+#pragma unroll
+      for (int r = 0; r < NR; ++r) v[r] *= cs;
+      float* cb = p.C + (long)b * p.sC;
+      if (p.beta != 0.f) {
+        float cv[NR];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) cv[r] = cb[(long)min(rowof(rbase, r), p.M - 1) * p.ldc + colc];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) v[r] += p.beta * cv[r];
+      }
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        const int row = rowof(rbase, r);
+        if (full_tile || (row < p.M && col < p.N)) cb[(long)row * p.ldc + col] = v[r];
+      }
+    }
+  }
+}
+
+template <int TM, int TN, int BM, int BN>
+__device__ __forceinline__ void store_tile(const GemmP& p, floatx16 (&acc)[TM][TN], int b, int split, int m0,
+                                           int n0, int wm, int wn, int lane) {
+  store_tile_mf<32, TM, TN, BM, BN>(p, acc, b, split, m0, n0, wm, wn, lane);
+}
+
 // KW > 1 splits every 32-deep K-tile between KW wave groups that own the same output sub-tiles
 // (in-block split-K): more waves per block for mid-size GEMMs, reduced through LDS at the end.
 template <int BM, int BN, int WM, int WN, int KW, bool AKC, bool BKC, bool VEC, int BKT>
@@ -295,85 +384,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN) * KW) void gemm_f32_kern
           for (int r = 0; r < 16; ++r)
             acc[i][j][r] += red[((((g - 1) * NWG + wt) * TM + i) * TN + j) * 1024 + r * 64 + lane];
   }
-  // C/D map of the 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
-  // Epilogue: every optional operand is fetched with unconditional clamped loads inside ONE uniform
-  // branch per operand (a per-element branch around a load makes hipcc wait vmcnt(0) per element).
-  const bool full_tile = (m0 + BM <= p.M) && (n0 + BN <= p.N);
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int col = n0 + wn + j * 32 + rl;
-    const int colc = min(col, p.N - 1);
-    float bj = 0.f, cs = 1.f;
-    if (p.splitk == 1) {
-      if (p.bias) bj = p.bias[colc];
-      if (p.colscale) cs = p.colscale[colc];
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int rbase = m0 + wm + i * 32 + 4 * hl;
-      if (p.splitk > 1) {
-        float* ws = p.ws + ((long)split * p.batch + b) * p.M * p.N;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = rbase + (r & 3) + 8 * (r >> 2);
-          if (full_tile || (row < p.M && col < p.N)) ws[(long)row * p.N + col] = acc[i][j][r];
-        }
-        continue;
-      }
-      float v[16];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] = p.alpha * acc[i][j][r] + bj;
-      switch (p.act) {   // one uniform branch per tile, not per element
-        case DASA_ACT_RELU:
-#pragma unroll
-          for (int r = 0; r < 16; ++r) v[r] = fmaxf(v[r], 0.f);
-          break;
-        case DASA_ACT_GELU:
-#pragma unroll
-          for (int r = 0; r < 16; ++r) v[r] = gelu_erf(v[r]);
-          break;
-        case DASA_ACT_TANH:
-#pragma unroll
-          for (int r = 0; r < 16; ++r) v[r] = tanhf(v[r]);
-          break;
-        case DASA_ACT_SIGMOID:
-#pragma unroll
-          for (int r = 0; r < 16; ++r) v[r] = sigmoidf_(v[r]);
-          break;
-        default:
-          break;
-      }
-      if (p.aux) {
-        const float* ab = p.aux + (long)b * p.sAux;
-        float av[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = min(rbase + (r & 3) + 8 * (r >> 2), p.M - 1);
-          av[r] = ab[(long)row * p.ld_aux + colc];
-        }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) v[r] *= av[r];
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] *= cs;
-      float* cb = p.C + (long)b * p.sC;
-      if (p.beta != 0.f) {
-        float cv[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = min(rbase + (r & 3) + 8 * (r >> 2), p.M - 1);
-          cv[r] = cb[(long)row * p.ldc + colc];
-        }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) v[r] += p.beta * cv[r];
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = rbase + (r & 3) + 8 * (r >> 2);
-        if (full_tile || (row < p.M && col < p.N)) cb[(long)row * p.ldc + col] = v[r];
-      }
-    }
-  }
+  store_tile<TM, TN, BM, BN>(p, acc, b, split, m0, n0, wm, wn, lane);
 }
 
 __global__ void splitk_reduce_kernel(GemmP p) {
@@ -390,6 +401,361 @@ __global__ void splitk_reduce_kernel(GemmP p) {
   }
 }
 
+// ---- NT GEMM with LDS-DMA staging (C = A[M,K] . B[N,K]^T, both operands K-contiguous) ----------
+// The nn.Linear forward shape (x . W^T), which carries most of the policy's FLOPs. Operand tiles
+// (rows x 32 floats = 128-B rows) are moved HBM/L2 -> LDS by global_load_lds_dwordx4 (1 KiB per
+// wave-instruction: 8 rows x 8 quads, lane-linear in LDS), so staging costs no VGPRs and no
+// ds_write pass. The LDS image keeps the XOR swizzle of TileLoader<KC, BK=32> (quad q of row r at
+// slot q ^ ((r>>1)&7)) by permuting the per-lane SOURCE address; the fragment reads apply the same
+// involution. Two stages: tile t+1 is in flight while tile t feeds the MFMAs; one vmcnt(0) +
+// barrier per 32-deep K-tile. Requires K (and the split-K chunk) % 32 == 0, 16-B aligned rows.
+template <int BM, int BN, int WAVES_M, int WAVES_N>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_nt_glds_kernel(GemmP p) {
+  constexpr int NW = WAVES_M * WAVES_N;
+  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
+  constexpr int TM = WM / 32, TN = WN / 32;
+  constexpr int IA = BM / 8 / NW, IB = BN / 8 / NW;       // 1-KiB glds instructions per wave per stage
+  static_assert(IA * 8 * NW == BM && IB * 8 * NW == BN, "tile rows must split into 8-row pieces per wave");
+  constexpr int A_FL = BM * 32, B_FL = BN * 32, STAGE_FL = A_FL + B_FL;
+  __shared__ __attribute__((aligned(1024))) float smem[2 * STAGE_FL];
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = (wave / WAVES_N) * WM, wn = (wave % WAVES_N) * WN;
+  int n0, m0;
+  {
+    const int gx = gridDim.x, nwg = gx * gridDim.y;
+    const int orig = blockIdx.y * gx + blockIdx.x;
+    const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+    const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+    n0 = (wgid % gx) * BN;
+    m0 = (wgid / gx) * BM;
+  }
+  const int b = blockIdx.z / p.splitk, split = blockIdx.z % p.splitk;
+  const int kbeg = split * p.kchunk;
+  const int kend = min(p.K, kbeg + p.kchunk);
+  const int ntiles = kend > kbeg ? (kend - kbeg) / 32 : 0;
+
+  // per-lane source rows (clamped: rows past M / N re-read the last row; their outputs are dropped)
+  const float* srcA[IA];
+  const float* srcB[IB];
+  {
+    const int rsub = lane >> 3, slot = lane & 7;
+#pragma unroll
+    for (int j = 0; j < IA; ++j) {
+      const int R = 8 * (wave * IA + j) + rsub;
+      const int qd = slot ^ ((R >> 1) & 7);
+      srcA[j] = p.A + (long)b * p.sA + (long)min(m0 + R, p.M - 1) * p.lda + kbeg + 4 * qd;
+    }
+#pragma unroll
+    for (int j = 0; j < IB; ++j) {
+      const int R = 8 * (wave * IB + j) + rsub;
+      const int qd = slot ^ ((R >> 1) & 7);
+      srcB[j] = p.B + (long)b * p.sB + (long)min(n0 + R, p.N - 1) * p.ldb + kbeg + 4 * qd;
+    }
+  }
+  auto stage = [&](int st, int t) {
+    float* base = smem + st * STAGE_FL;
+    const int ko = 32 * t;
+#pragma unroll
+    for (int j = 0; j < IA; ++j)
+      __builtin_amdgcn_global_load_lds((const void*)(srcA[j] + ko),
+                                       (__attribute__((address_space(3))) void*)(base + (wave * IA + j) * 256),
+                                       16, 0, 0);
+#pragma unroll
+    for (int j = 0; j < IB; ++j)
+      __builtin_amdgcn_global_load_lds((const void*)(srcB[j] + ko),
+                                       (__attribute__((address_space(3))) void*)(base + A_FL + (wave * IB + j) * 256),
+                                       16, 0, 0);
+  };
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int hl = lane >> 5, rl = lane & 31;
+  if (ntiles > 0) {
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    const float* As = smem + cur * STAGE_FL;
+    const float* Bs = As + A_FL;
+    // every fragment of this K-tile is read BEFORE the next tile's LDS-DMA is issued: a ds_read
+    // after an in-flight glds into the same array makes hipcc drain vmcnt(0) first
+    float4 af[4][TM], bf[4][TN];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int q = 2 * g + hl;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm + i * 32 + rl;
+        af[g][i] = *reinterpret_cast<const float4*>(As + row * 32 + 4 * (q ^ ((row >> 1) & 7)));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn + j * 32 + rl;
+        bf[g][j] = *reinterpret_cast<const float4*>(Bs + row * 32 + 4 * (q ^ ((row >> 1) & 7)));
+      }
+    }
+    if (t + 1 < ntiles) stage(cur ^ 1, t + 1);
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(af[g][i], e), f4get(bf[g][j], e),
+                                                             acc[i][j], 0, 0, 0);
+    // keep the MFMAs ahead of the wait: hipcc otherwise sinks them past the barrier, so the wait
+    // for tile t+1's DMA would sit in front of tile t's MFMAs instead of behind them
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  store_tile<TM, TN, BM, BN>(p, acc, b, split, m0, n0, wm, wn, lane);
+}
+
+// ---- NT GEMM, 64-deep K tiles (C = A[M,K] . B[N,K]^T, both operands K-contiguous) --------------
+// BK = 64 floats (256-B LDS rows, quad q of row r stored at slot q ^ (r & 15): the 16-lane groups
+// of a ds_read_b128 fragment read hit 16 distinct slots). Tile t+1 is loaded into registers while
+// tile t feeds the MFMAs; NSTAGE = 1 keeps one LDS image (write after a barrier, 2 barriers per
+// tile, ~64 KiB at 128x128 so two workgroups share a CU), NSTAGE = 2 double-buffers it (1 barrier).
+// MF = 16 uses v_mfma_f32_16x16x4_f32 (4 lane groups carry 4 k each: group g supplies
+// k = 16s + 4g + e to MFMA e), MF = 32 uses v_mfma_f32_32x32x2_f32 (halves h: k = 8s + 4h + e).
+// Requires K (and the split-K chunk) % 64 == 0 and 16-B aligned rows.
+//
+// SK = stream-K: a grid of G <= #CUs workgroups. The first sk_dp tiles are dealt whole (tile lw,
+// lw + G, ...); the MAC iterations (64-deep K steps) of the remaining tiles are split evenly over
+// the G workgroups, so every CU gets the same work whatever the tile count. A tile finished in
+// one piece is stored directly; pieces of a split tile are stored write-through (sc1) to a slab per
+// (workgroup, first|last piece) and the LAST piece to arrive (agent-scope ticket on the tile's
+// counter, re-armed to 0) sums all pieces in workgroup order (deterministic) and runs the epilogue.
+// No workgroup ever waits for another, so residency is never assumed.
+struct SkP { int grid, dp, tiles, ipt, tiles_n, tiles_mn; unsigned* cnt; float* slab; };
+
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+template <int BM, int BN, int WAVES_M, int WAVES_N, int MF, int NSTAGE, bool SK>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_nt_k64_kernel(GemmP p, SkP sk) {
+  constexpr int BK = 64;
+  constexpr int NT = 64 * WAVES_M * WAVES_N;
+  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
+  constexpr int TM = WM / MF, TN = WN / MF;
+  constexpr int A_FL = BM * BK, B_FL = BN * BK, STAGE_FL = A_FL + B_FL;
+  constexpr int KG = MF == 32 ? BK / 8 : BK / 16;       // K-groups (one float4 per lane) per tile
+  using AccT = typename std::conditional<MF == 32, floatx16, floatx4>::type;
+  constexpr int NR = MF == 32 ? 16 : 4;
+  __shared__ __attribute__((aligned(16))) float smem[NSTAGE * STAGE_FL];
+  __shared__ int s_last;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave / WAVES_N) * WM, wn = (wave % WAVES_N) * WN;
+  using LA = TileLoader<BM, true, true, NT, BK>;
+  using LB = TileLoader<BN, true, true, NT, BK>;
+  LA la;
+  LB lb;
+  AccT acc[TM][TN];
+  const int fr = MF == 32 ? (lane & 31) : (lane & 15);   // fragment row within an MF tile
+  const int fg = MF == 32 ? (lane >> 5) : (lane >> 4);   // lane group: which 4 k of a K-group
+
+  auto compute = [&](const float* S) {
+    const float* As = S;
+    const float* Bs = S + A_FL;
+#pragma unroll
+    for (int g = 0; g < KG; ++g) {
+      const int q = (MF == 32 ? 2 : 4) * g + fg;
+      float4 af[TM], bf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm + i * MF + fr;
+        af[i] = *reinterpret_cast<const float4*>(As + row * BK + 4 * (q ^ (row & 15)));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn + j * MF + fr;
+        bf[j] = *reinterpret_cast<const float4*>(Bs + row * BK + 4 * (q ^ (row & 15)));
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            if constexpr (MF == 32)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(af[i], e), f4get(bf[j], e), acc[i][j], 0, 0, 0);
+            else
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(f4get(af[i], e), f4get(bf[j], e), acc[i][j], 0, 0, 0);
+          }
+    }
+  };
+  // acc = A[m0.., kbeg..kbeg+64n) . B[n0.., same]^T. Starts and ends with every wave past a barrier,
+  // so consecutive calls may restage the LDS image at once.
+  auto mac = [&](const float* Ab, const float* Bb, int m0, int n0, int kbeg, int ntiles) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < NR; ++r) acc[i][j][r] = 0.f;
+    if (ntiles <= 0) return;
+    const int kend = kbeg + BK * ntiles;
+    la.load(Ab, p.lda, m0, p.M, kbeg, kend);
+    lb.load(Bb, p.ldb, n0, p.N, kbeg, kend);
+    la.store(smem);
+    lb.store(smem + A_FL);
+    __syncthreads();
+    // Unconditional staging (the last step re-loads the last tile into a buffer nobody reads): a
+    // conditional load leaves the staging registers live across a branch and hipcc moves them to
+    // scratch memory.
+    for (int t = 0; t < ntiles; ++t) {
+      {
+        const int k0 = kbeg + BK * min(t + 1, ntiles - 1);
+        la.load(Ab, p.lda, m0, p.M, k0, kend);
+        lb.load(Bb, p.ldb, n0, p.N, k0, kend);
+      }
+      float* cur = smem + (NSTAGE == 2 ? (t & 1) * STAGE_FL : 0);
+      compute(cur);
+      if (NSTAGE == 2) {
+        la.store(smem + ((t + 1) & 1) * STAGE_FL);
+        lb.store(smem + ((t + 1) & 1) * STAGE_FL + A_FL);
+        __syncthreads();
+      } else {
+        __syncthreads();
+        la.store(smem);
+        lb.store(smem + A_FL);
+        __syncthreads();
+      }
+    }
+  };
+
+  if constexpr (!SK) {
+    const int wgid = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+    const int n0 = (wgid % gridDim.x) * BN, m0 = (wgid / gridDim.x) * BM;
+    const int b = blockIdx.z / p.splitk, split = blockIdx.z % p.splitk;
+    const int kbeg = split * p.kchunk;
+    const int kend = min(p.K, kbeg + p.kchunk);
+    mac(p.A + (long)b * p.sA, p.B + (long)b * p.sB, m0, n0, kbeg, kend > kbeg ? (kend - kbeg) / BK : 0);
+    store_tile_mf<MF, TM, TN, BM, BN>(p, acc, b, split, m0, n0, wm, wn, lane);
+  } else {
+    const int G = sk.grid, lw = xcd_remap(blockIdx.x, G), ipt = sk.ipt;
+    auto tile_at = [&](int T, int& b, int& m0, int& n0) {
+      b = T / sk.tiles_mn;
+      const int r = T - b * sk.tiles_mn;
+      m0 = (r / sk.tiles_n) * BM;
+      n0 = (r % sk.tiles_n) * BN;
+    };
+    for (int T = lw; T < sk.dp; T += G) {     // whole tiles
+      int b, m0, n0;
+      tile_at(T, b, m0, n0);
+      mac(p.A + (long)b * p.sA, p.B + (long)b * p.sB, m0, n0, 0, ipt);
+      store_tile_mf<MF, TM, TN, BM, BN>(p, acc, b, 0, m0, n0, wm, wn, lane);
+    }
+    const long I = (long)(sk.tiles - sk.dp) * ipt;     // split iterations, I >= G (host guarantees)
+    auto start_of = [&](int w) { return (long)w * I / G; };
+    auto owner_of = [&](long i) { return (int)(((i + 1) * G + I - 1) / I - 1); };
+    long it = start_of(lw);
+    const long end = start_of(lw + 1);
+    const int first_tile = (int)(it / ipt);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(sk.slab, 0, 0x7fffffff, 0x00020000);
+    constexpr int SLAB_B = BM * BN * 4;
+    while (it < end) {
+      const int Ts = (int)(it / ipt), kt0 = (int)(it % ipt);
+      const int kt1 = (int)min((long)ipt, kt0 + (end - it));
+      int b, m0, n0;
+      tile_at(sk.dp + Ts, b, m0, n0);
+      mac(p.A + (long)b * p.sA, p.B + (long)b * p.sB, m0, n0, BK * kt0, kt1 - kt0);
+      if (kt0 == 0 && kt1 == ipt) {
+        store_tile_mf<MF, TM, TN, BM, BN>(p, acc, b, 0, m0, n0, wm, wn, lane);
+      } else {
+        const int slot = 2 * lw + (Ts == first_tile ? 0 : 1);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r4 = 0; r4 < NR / 4; ++r4) {
+              const int off = slot * SLAB_B + (((i * TN + j) * (NR / 4) + r4) * NT + tid) * 16;
+              const u32x4 u = {__float_as_uint(acc[i][j][4 * r4]), __float_as_uint(acc[i][j][4 * r4 + 1]),
+                               __float_as_uint(acc[i][j][4 * r4 + 2]), __float_as_uint(acc[i][j][4 * r4 + 3])};
+              __builtin_amdgcn_raw_buffer_store_b128(u, rs, off, 0, 16);   // sc1: write-through
+            }
+        const long ia = (long)Ts * ipt;
+        const int w0 = owner_of(ia), w1 = owner_of(ia + ipt - 1);
+        // ticket: every wave's write-through stores have landed before one lane takes it
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0)
+          s_last = __hip_atomic_fetch_add(sk.cnt + Ts, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                   (unsigned)(w1 - w0);
+        __syncthreads();
+        if (s_last) {
+          if (tid == 0) __hip_atomic_store(sk.cnt + Ts, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler-only: sc1 loads below the ticket
+          // every piece (this workgroup's own included) is re-read from its slab and summed into the
+          // accumulator registers in workgroup order
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+              for (int r = 0; r < NR; ++r) acc[i][j][r] = 0.f;
+          for (int w = w0; w <= w1; ++w) {      // fixed order: deterministic whoever arrives last
+            const int ws = 2 * w + ((long)Ts == start_of(w) / ipt ? 0 : 1);
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+              for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r4 = 0; r4 < NR / 4; ++r4) {
+                  const int off = ws * SLAB_B + (((i * TN + j) * (NR / 4) + r4) * NT + tid) * 16;
+                  const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);   // sc1
+                  acc[i][j][4 * r4] += __uint_as_float(u.x);
+                  acc[i][j][4 * r4 + 1] += __uint_as_float(u.y);
+                  acc[i][j][4 * r4 + 2] += __uint_as_float(u.z);
+                  acc[i][j][4 * r4 + 3] += __uint_as_float(u.w);
+                }
+          }
+          store_tile_mf<MF, TM, TN, BM, BN>(p, acc, b, 0, m0, n0, wm, wn, lane);
+        }
+      }
+      it += kt1 - kt0;
+    }
+  }
+}
+
+template <int BM, int BN, int WAVES_M, int WAVES_N, int MF, int NSTAGE>
+int launch_k64(const GemmP& p, const SkP* sk, hipStream_t st) {
+  if (sk) {
+    hipLaunchKernelGGL((gemm_nt_k64_kernel<BM, BN, WAVES_M, WAVES_N, MF, NSTAGE, true>), dim3(sk->grid),
+                       dim3(64 * WAVES_M * WAVES_N), 0, st, p, *sk);
+  } else {
+    dim3 grid((p.N + BN - 1) / BN, (p.M + BM - 1) / BM, p.batch * p.splitk);
+    hipLaunchKernelGGL((gemm_nt_k64_kernel<BM, BN, WAVES_M, WAVES_N, MF, NSTAGE, false>), grid,
+                       dim3(64 * WAVES_M * WAVES_N), 0, st, p, SkP{});
+  }
+  DASA_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int BM, int BN, int WAVES_M, int WAVES_N>
+int launch_glds(const GemmP& p, hipStream_t st) {
+  dim3 grid((p.N + BN - 1) / BN, (p.M + BM - 1) / BM, p.batch * p.splitk);
+  hipLaunchKernelGGL((gemm_nt_glds_kernel<BM, BN, WAVES_M, WAVES_N>), grid, dim3(64 * WAVES_M * WAVES_N), 0, st, p);
+  DASA_CHECK_LAUNCH();
+  return 0;
+}
+
 template <int BM, int BN, int WM, int WN, int KW, bool VEC, int BK = 32>
 int launch_tile(const GemmP& p, int opA, int opB, hipStream_t st) {
   dim3 grid((p.N + BN - 1) / BN, (p.M + BM - 1) / BM, p.batch * p.splitk);
@@ -404,7 +770,7 @@ int launch_tile(const GemmP& p, int opA, int opB, hipStream_t st) {
 }
 
 // Tile configurations: {BM, BN, WM, WN, KW}
-struct TileCfg { int bm, bn, wm, wn, kw; };
+struct TileCfg { int bm, bn, wm, wn, kw; bool glds = false; bool sk = false; };
 constexpr TileCfg kCfgs[] = {
     {128, 128, 64, 64, 1},  // 0: large GEMMs
     {64, 128, 32, 64, 1},   // 1
@@ -421,10 +787,78 @@ constexpr TileCfg kCfgs[] = {
     {32, 64, 32, 32, 2},    // 12: BK = 64
     {128, 64, 64, 32, 1},   // 13: BK = 64
     {64, 128, 32, 64, 2},   // 14: BK = 64
+    // LDS-DMA NT kernels (gemm_nt_glds_kernel): {BM, BN, WM, WN} with kw unused
+    {128, 128, 64, 64, 1, true},  // 15
+    {256, 128, 64, 64, 1, true},  // 16: 8 waves
+    {128, 64, 64, 32, 1, true},   // 17
+    {64, 64, 32, 32, 1, true},    // 18
+    {128, 128, 32, 64, 1, true},  // 19: 8 waves
+    {64, 128, 32, 64, 1, true},   // 20
+    // 64-deep K tiles (gemm_nt_k64_kernel): {BM, BN, WM, WN, MF | NSTAGE << 8}
+    {128, 128, 64, 64, 16 | 1 << 8, true},   // 21
+    {128, 128, 64, 64, 32 | 1 << 8, true},   // 22
+    {128, 128, 64, 64, 16 | 2 << 8, true},   // 23
+    {128, 64, 64, 32, 16 | 1 << 8, true},    // 24
+    {64, 128, 32, 64, 16 | 1 << 8, true},    // 25
+    {64, 64, 32, 32, 16 | 1 << 8, true},     // 26
+    {128, 128, 32, 64, 16 | 1 << 8, true},   // 27: 8 waves
+    {256, 128, 64, 64, 16 | 1 << 8, true},   // 28: 8 waves
+    {64, 64, 32, 32, 16 | 2 << 8, true},     // 29
+    {128, 64, 64, 32, 16 | 2 << 8, true},    // 30
+    // stream-K forms of the 64-deep K kernels (grid = CUs x occupancy, see SkP)
+    {128, 128, 64, 64, 16 | 1 << 8, true, true},   // 31
+    {128, 64, 64, 32, 16 | 1 << 8, true, true},    // 32
+    {64, 128, 32, 64, 16 | 1 << 8, true, true},    // 33
+    {64, 64, 32, 32, 16 | 1 << 8, true, true},     // 34
+    {128, 128, 32, 64, 16 | 1 << 8, true, true},   // 35: 8 waves
 };
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
-int launch_cfg(int cfg, bool vec, const GemmP& p, int opA, int opB, hipStream_t st) {
+// Non-glds stand-in for a glds configuration whose operands do not qualify (same tile).
+int glds_fallback(int cfg) {
+  switch (cfg) {
+    case 15: return 0;
+    case 16: return 0;
+    case 17: return 6;
+    case 18: return 2;
+    case 19: return 0;
+    case 20: return 1;
+    case 21: case 22: case 23: case 27: case 28: return 0;
+    case 24: case 30: return 6;
+    case 25: case 33: return 1;
+    case 31: case 35: return 0;
+    case 32: return 6;
+    default: return 2;
+  }
+}
+
+int launch_cfg(int cfg, bool vec, bool glds_ok, const GemmP& p, const SkP* sk, int opA, int opB, hipStream_t st) {
+  if (kCfgs[cfg].glds) {
+    if (!glds_ok) cfg = glds_fallback(cfg);
+    else switch (cfg) {
+      case 15: return launch_glds<128, 128, 2, 2>(p, st);
+      case 16: return launch_glds<256, 128, 4, 2>(p, st);
+      case 17: return launch_glds<128, 64, 2, 2>(p, st);
+      case 18: return launch_glds<64, 64, 2, 2>(p, st);
+      case 19: return launch_glds<128, 128, 4, 2>(p, st);
+      case 20: return launch_glds<64, 128, 2, 2>(p, st);
+      case 21: return launch_k64<128, 128, 2, 2, 16, 1>(p, nullptr, st);
+      case 22: return launch_k64<128, 128, 2, 2, 32, 1>(p, nullptr, st);
+      case 23: return launch_k64<128, 128, 2, 2, 16, 2>(p, nullptr, st);
+      case 24: return launch_k64<128, 64, 2, 2, 16, 1>(p, nullptr, st);
+      case 25: return launch_k64<64, 128, 2, 2, 16, 1>(p, nullptr, st);
+      case 26: return launch_k64<64, 64, 2, 2, 16, 1>(p, nullptr, st);
+      case 27: return launch_k64<128, 128, 4, 2, 16, 1>(p, nullptr, st);
+      case 28: return launch_k64<256, 128, 4, 2, 16, 1>(p, nullptr, st);
+      case 29: return launch_k64<64, 64, 2, 2, 16, 2>(p, nullptr, st);
+      case 30: return launch_k64<128, 64, 2, 2, 16, 2>(p, nullptr, st);
+      case 31: return launch_k64<128, 128, 2, 2, 16, 1>(p, sk, st);
+      case 32: return launch_k64<128, 64, 2, 2, 16, 1>(p, sk, st);
+      case 33: return launch_k64<64, 128, 2, 2, 16, 1>(p, sk, st);
+      case 34: return launch_k64<64, 64, 2, 2, 16, 1>(p, sk, st);
+      default: return launch_k64<128, 128, 4, 2, 16, 1>(p, sk, st);
+    }
+  }
   if (!vec) {
     return kCfgs[cfg].bm == 32 ? launch_tile<32, 128, 32, 32, 1, false>(p, opA, opB, st)
                                : launch_tile<64, 64, 32, 32, 1, false>(p, opA, opB, st);
@@ -452,7 +886,36 @@ inline long cdiv(long a, long b) { return (a + b - 1) / b; }
 
 }  // namespace
 
-struct Plan { int cfg, splitk, kchunk; int64_t ws; };
+struct Plan { int cfg, splitk, kchunk; int64_t ws; int sk_grid, sk_dp, sk_tiles, sk_ipt; };
+
+// Leading words of every GEMM workspace: stream-K arrival counters (zero on allocation, re-armed
+// to zero by each call). Split-K partials and stream-K slabs follow.
+constexpr int64_t kCntWords = 16384;
+constexpr int64_t kCntBytes = kCntWords * 4;
+
+static int num_cus() {
+  static int n[64] = {0};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 64) dev = 0;
+  if (n[dev] == 0) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    n[dev] = v;
+  }
+  return n[dev];
+}
+
+// non-stream-K twin of a stream-K configuration (same tile and kernel body)
+static int sk_twin(int cfg) {
+  switch (cfg) {
+    case 31: return 21;
+    case 32: return 24;
+    case 33: return 25;
+    case 34: return 26;
+    default: return 27;
+  }
+}
 
 static int g_force_cfg = -2;   // DASA_GEMM_CFG=<index> pins a tile config (tuning sweeps)
 
@@ -469,7 +932,14 @@ static Plan make_plan(const dasa_gemm_desc* d) {
   // long-K problems, 32x64 tiles for mid-size ones, split-K when there are too few tiles to fill the
   // 256 CUs; the skinny decoder GEMMs (M <= 32) are weight-streaming and split K widely.
   const long t64 = tiles(64, 64);
-  if (M <= 32) pl.cfg = 5;
+  // NT operands with K % 64 == 0 (the nn.Linear forward) take the 64-deep K kernels where they win
+  // (profiles/r01c/gemm_k64_sk.txt): 128x128 / 64x128 tiles on large problems, and stream-K 64x64
+  // tiles at four workgroups per CU on mid-size long-K problems (no quantisation tail).
+  const bool nt64 = d->opA == 0 && d->opB == 1 && K % 64 == 0 && M > 32;
+  int sk_occ = 1;
+  if (nt64 && t64 >= 2048) pl.cfg = N >= 2048 ? 27 : 25;
+  else if (nt64 && K >= 1536 && t64 >= 128) { pl.cfg = 34; sk_occ = 4; }
+  else if (M <= 32) pl.cfg = 5;
   else if (d->opA == 1 && K >= 8192 && t64 >= 256) pl.cfg = 8;   // weight grads over many rows
   else if (t64 >= 2048) pl.cfg = 6;                              // profiles/r01/gemm_grid_v4.txt
   else if (t64 >= 800) pl.cfg = 4;
@@ -500,6 +970,27 @@ static Plan make_plan(const dasa_gemm_desc* d) {
   pl.splitk = splitk;
   pl.kchunk = kchunk;
   pl.ws = splitk > 1 ? (int64_t)splitk * batch * M * N * (int64_t)sizeof(float) : 0;
+  pl.sk_grid = pl.sk_dp = pl.sk_tiles = pl.sk_ipt = 0;
+  if (kCfgs[pl.cfg].sk) {
+    const int ipt = K / 64;
+    const long nt = blocks;
+    int G = num_cus() * (fsplit > 0 ? fsplit : sk_occ);
+    long dp = nt >= 2L * G ? (nt / G - 1) * G : 0;
+    const long I = (nt - dp) * ipt;
+    if (G > I) G = (int)I;
+    if (K % 64 != 0 || ipt == 0 || nt - dp > kCntWords || G <= 0) {
+      pl.cfg = sk_twin(pl.cfg);    // not stream-K-able: the same tile, one workgroup per tile
+    } else {
+      pl.splitk = 1;
+      pl.kchunk = K;
+      pl.sk_grid = G;
+      pl.sk_dp = (int)dp;
+      pl.sk_tiles = (int)nt;
+      pl.sk_ipt = ipt;
+      pl.ws = 2LL * G * bm * bn * (int64_t)sizeof(float);
+    }
+  }
+  pl.ws += kCntBytes;
   return pl;
 }
 
@@ -518,9 +1009,11 @@ extern "C" int dasa_gemm_f32(const dasa_gemm_desc* d, void* ws, int64_t ws_bytes
   const int M = d->M, N = d->N, K = d->K, batch = d->batch < 1 ? 1 : d->batch;
   if (M < 0 || N < 0 || K < 0) return (int)hipErrorInvalidValue;
   Plan pl = make_plan(d);
-  if (pl.splitk > 1 && (ws == nullptr || ws_bytes < pl.ws)) {  // no workspace: single pass
+  if (ws == nullptr || ws_bytes < pl.ws) {  // no (or too small a) workspace: single pass, no stream-K
     pl.splitk = 1;
     pl.kchunk = K > 0 ? (int)(cdiv(K, 64) * 64) : 64;
+    if (kCfgs[pl.cfg].sk) pl.cfg = sk_twin(pl.cfg);
+    pl.sk_grid = 0;
   }
   if (M == 0 || N == 0) return 0;
   // float4 operand loads need 16-B aligned rows; anything else takes the scalar-load variant
@@ -542,10 +1035,23 @@ extern "C" int dasa_gemm_f32(const dasa_gemm_desc* d, void* ws, int64_t ws_bytes
   p.bias = d->bias; p.act = d->act;
   p.aux = d->aux; p.ld_aux = d->ld_aux; p.sAux = d->strideAux;
   p.colscale = d->colscale; p.alpha = d->alpha; p.beta = d->beta;
-  p.ws = (float*)ws;
+  p.ws = ws ? (float*)((char*)ws + kCntBytes) : nullptr;
+  SkP sk{};
+  if (pl.sk_grid > 0) {
+    sk.grid = pl.sk_grid;
+    sk.dp = pl.sk_dp;
+    sk.tiles = pl.sk_tiles;
+    sk.ipt = pl.sk_ipt;
+    sk.tiles_n = (int)cdiv(N, kCfgs[pl.cfg].bn);
+    sk.tiles_mn = (int)(cdiv(M, kCfgs[pl.cfg].bm) * sk.tiles_n);
+    sk.cnt = (unsigned*)ws;
+    sk.slab = p.ws;
+  }
   hipStream_t st = (hipStream_t)stream;
   int rc;
-  rc = launch_cfg(pl.cfg, vec, p, d->opA, d->opB, st);
+  const int kalign = pl.cfg >= 21 ? 63 : 31;
+  const bool glds_ok = vec && d->opA == 0 && d->opB == 1 && (K & kalign) == 0 && (pl.kchunk & kalign) == 0;
+  rc = launch_cfg(pl.cfg, vec, glds_ok, p, pl.sk_grid > 0 ? &sk : nullptr, d->opA, d->opB, st);
   if (rc) return rc;
   if (pl.splitk > 1) {
     const long total = (long)batch * M * N;

@@ -80,24 +80,26 @@ def _rows(t):
 
 # ------------------------------------------------------------------------------------------ GEMM
 _WS = {}
-_WS_MIN = 32 << 20
+_WS_SK = (64 << 10) + 2 * 512 * 128 * 128 * 4    # counters + stream-K slabs (<= 512 workgroups)
+_WS_MIN = max(32 << 20, _WS_SK)
 
 
 def _gemm_ws(device, d):
-    """Split-K partials workspace: one buffer per (device, stream), grown on demand and reused by every
-    GEMM on that stream (a GEMM's split-K pass and its reduce run back to back on the stream, so a later
-    GEMM on the same stream cannot overwrite partials still in use). Saves a workspace query and an
-    allocation per launch; falls back to the exact query when the buffer is too small."""
+    """GEMM workspace (include/dasa_hip.h dasa_gemm_f32_workspace): one zero-initialised buffer per
+    (device, stream), grown on demand and reused by every GEMM on that stream. Its leading stream-K
+    arrival counters are left zero by every call (so it is zeroed only on allocation); split-K
+    partials / stream-K slabs follow them, and calls on one stream never overlap. The buffer starts
+    large enough for every stream-K plan, so most calls skip the workspace query."""
     key = (device.index, _stream())
     buf = _WS.get(key)
     if buf is None:
-        buf = torch.empty(_WS_MIN // 4, dtype=torch.float32, device=device)
+        buf = torch.zeros(_WS_MIN // 4, dtype=torch.float32, device=device)
         _WS[key] = buf
     nbytes = buf.numel() * 4
-    if d.M * d.N * max(1, d.batch) * 16 * 4 > nbytes:   # split-K is at most 16-way
+    if d.M * d.N * max(1, d.batch) * 16 * 4 + _WS_SK > nbytes:   # split-K is at most 16-way
         need = _lib.lib().dasa_gemm_f32_workspace(ctypes.byref(d))
         if need > nbytes:
-            buf = torch.empty(need // 4 + 1, dtype=torch.float32, device=device)
+            buf = torch.zeros(need // 4 + 1, dtype=torch.float32, device=device)
             _WS[key] = buf
             nbytes = buf.numel() * 4
     return buf.data_ptr(), nbytes

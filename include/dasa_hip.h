@@ -49,8 +49,11 @@ typedef struct dasa_gemm_desc {
   const float* colscale;   /* [N] or NULL (shared env-drop noise, agent_dg.py:780-785) */
   float alpha, beta;
 } dasa_gemm_desc;
-/* Workspace for split-K partials (skinny-M decoder GEMMs): bytes needed for this descriptor.
- * Passing ws == NULL (or too small) runs the GEMM without split-K instead. */
+/* Workspace bytes for this descriptor: 64 KiB of stream-K arrival counters, then split-K partials
+ * (skinny-M decoder GEMMs) or stream-K partial-tile slabs (mid-size GEMMs that do not fill the CUs).
+ * The buffer must be ZERO-FILLED when first allocated; every call leaves the counters zero again,
+ * so one buffer can be reused by consecutive calls on one stream (never by overlapping calls).
+ * Passing ws == NULL (or too small) runs the GEMM without split-K / stream-K instead. */
 int64_t dasa_gemm_f32_workspace(const dasa_gemm_desc* d);
 /* Tuning hook: pin tile configuration `cfg % 64` (and, when cfg >= 64, split-K = cfg / 64) for
  * subsequent calls (-1 = automatic choice).

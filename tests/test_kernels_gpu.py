@@ -72,7 +72,9 @@ def test_gemm_every_config(dev):
     lib = _lib.lib()
     ncfg = lib.dasa_gemm_force_config(-1)
     g = torch.Generator().manual_seed(11)
-    shapes = [(37, 45, 100), (130, 200, 36), (64, 128, 1024), (257, 96, 2100)]
+    # K % 64 == 0 shapes reach the 64-deep K kernels and their stream-K forms (split tiles summed
+    # by the last arriving workgroup)
+    shapes = [(37, 45, 100), (130, 200, 36), (64, 128, 1024), (257, 96, 2100), (300, 136, 1536), (520, 64, 4096)]
     try:
         for cfg in range(ncfg):
             lib.dasa_gemm_force_config(cfg)
