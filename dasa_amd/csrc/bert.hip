@@ -24,9 +24,11 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
                                                      float* __restrict__ y, float* __restrict__ mean_out,
                                                      float* __restrict__ rstd_out, float* __restrict__ xsum,
-                                                     int M, int N, float eps, float p, uint64_t seed) {
+                                                     int M, int N, float eps, float p, uint64_t seed,
+                                                     const uint64_t* seed_src) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= M) return;
+  if (p > 0.f) seed = eff_seed(seed, seed_src);
   const int N4 = N >> 2;
   const float4* x4 = reinterpret_cast<const float4*>(x + (long)row * N);
   const float4* r4 = res ? reinterpret_cast<const float4*>(res + (long)row * N) : nullptr;
@@ -148,9 +150,10 @@ __global__ __launch_bounds__(256) void embed_kernel(const int64_t* __restrict__ 
                                                     const float* __restrict__ pos, const float* __restrict__ type0,
                                                     const float* __restrict__ gamma, const float* __restrict__ beta,
                                                     float* __restrict__ out, int B, int L, int H, float eps, float p,
-                                                    uint64_t seed) {
+                                                    uint64_t seed, const uint64_t* seed_src) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= B * L) return;
+  if (p > 0.f) seed = eff_seed(seed, seed_src);
   const int t = row % L;
   const long id = ids[row];
   const int H4 = H >> 2;
@@ -212,6 +215,7 @@ struct MhaArgs {
   const float* Q; long ldq; const float* K; long ldk; const float* V; long ldv;
   const float* mask; float* out; long ldo; float* probs;
   int B, heads, Lq, Lk; float scale; float p; uint64_t seed;
+  const uint64_t* seed_src;   // graph-captured forward only (eff_seed); the backward uses plain seeds
 };
 
 // Forward on matrix cores (v_mfma_f32_32x32x2_f32): one workgroup per (batch, head), one wave per
@@ -237,6 +241,7 @@ __global__ __launch_bounds__(256) void mha_fwd_kernel(MhaArgs a, int nqt) {
   const int bh = blockIdx.x;
   const int h = bh % a.heads, b = bh / a.heads;
   const int Lq = a.Lq, Lk = a.Lk;
+  const uint64_t seed = a.p > 0.f ? eff_seed(a.seed, a.seed_src) : 0;
   // stage K / V rows (zero past Lk) and the additive key mask
   for (int idx = threadIdx.x; idx < NKT * 32 * (kDh / 4); idx += blockDim.x) {
     const int row = idx / (kDh / 4), c4 = idx % (kDh / 4);
@@ -307,7 +312,7 @@ __global__ __launch_bounds__(256) void mha_fwd_kernel(MhaArgs a, int nqt) {
       const int key = kt * 32 + acc_row(r, hh);
       float p = st[kt][r] * inv;
       if (a.probs && q < Lq && key < Lk) a.probs[prow + key] = p;
-      if (a.p > 0.f) p *= dasa_dropout_scale(a.p, a.seed, (uint64_t)(prow + key));
+      if (a.p > 0.f) p *= dasa_dropout_scale(a.p, seed, (uint64_t)(prow + key));
       st[kt][r] = p;
     }
   // O = P V: A operand = the probability accumulator (rows = keys), B operand = V[key][d0 + lane]
@@ -414,7 +419,8 @@ __global__ void reverse_valid_kernel(const float* __restrict__ x, const int* __r
 }
 
 __global__ void dropout_kernel(const float* __restrict__ x, long ldx, float* __restrict__ y, long ldy, int rows,
-                               int cols, float p, uint64_t seed) {
+                               int cols, float p, uint64_t seed, const uint64_t* seed_src) {
+  seed = eff_seed(seed, seed_src);
   const long total = (long)rows * cols;
   for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
     const int r = (int)(idx / cols), c = (int)(idx % cols);
@@ -518,7 +524,7 @@ extern "C" int dasa_layernorm_fwd(const float* x, const float* res, const float*
   if ((N & 3) || N > 8192) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   DASA_VPL_DISPATCH(N, ln_fwd_kernel, dim3(cdivi(M, 4)), x, res, gamma, beta, y, mean, rstd, xsum, M, N, eps, drop_p,
-                    seed);
+                    seed, drop_p > 0.f ? dasa_seed_src_host() : nullptr);
   DASA_CHECK_LAUNCH();
   return 0;
 }
@@ -541,7 +547,7 @@ extern "C" int dasa_bert_embed_fwd(const int64_t* ids, const float* word, const 
   if ((H & 3) || H > 8192) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   DASA_VPL_DISPATCH(H, embed_kernel, dim3(cdivi((long)B * L, 4)), ids, word, pos, type0, gamma, beta, out, B, L, H,
-                    eps, drop_p, seed);
+                    eps, drop_p, seed, drop_p > 0.f ? dasa_seed_src_host() : nullptr);
   DASA_CHECK_LAUNCH();
   return 0;
 }
@@ -554,7 +560,8 @@ extern "C" int dasa_mha_fwd(const float* Q, int64_t ldq, const float* K, int64_t
   if (dh != kDh || Lk <= 0 || Lk > kMaxLk || ((ldq | ldk | ldv) & 3) ||
       (((uintptr_t)Q | (uintptr_t)K | (uintptr_t)V) & 15))
     return (int)hipErrorInvalidValue;
-  MhaArgs a{Q, ldq, K, ldk, V, ldv, addmask, out, ldo, probs, B, heads, Lq, Lk, scale, drop_p, seed};
+  MhaArgs a{Q, ldq, K, ldk, V, ldv, addmask, out, ldo, probs, B, heads, Lq, Lk, scale, drop_p, seed,
+            drop_p > 0.f ? dasa_seed_src_host() : nullptr};
   const int nqt = cdivi(Lq, 32);
   if (nqt > 4) return (int)hipErrorInvalidValue;   // one wave per 32-query tile, Lq <= 128
   const dim3 grid(B * heads), block(64 * nqt);
@@ -576,7 +583,7 @@ extern "C" int dasa_mha_bwd(const float* Q, int64_t ldq, const float* K, int64_t
   if (B <= 0 || Lq <= 0) return 0;
   if (dh != kDh || Lk <= 0 || Lk > kMaxLk || !probs) return (int)hipErrorInvalidValue;
   MhaArgs a{Q, ldq, K, ldk, V, ldv, nullptr, nullptr, 0, const_cast<float*>(probs), B, heads, Lq, Lk, scale, drop_p,
-            seed};
+            seed, nullptr};
   hipLaunchKernelGGL(mha_bwd_kernel, dim3(B * heads), dim3(256), 0, (hipStream_t)stream, a, dout, (long)lddo, dQ, dK,
                      dV);
   DASA_CHECK_LAUNCH();
@@ -606,7 +613,7 @@ extern "C" int dasa_dropout_fwd(const float* x, int64_t ldx, float* y, int64_t l
   int grid = cdivi(total, 256);
   if (grid > 8192) grid = 8192;
   hipLaunchKernelGGL(dropout_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, (long)ldx, y, (long)ldy, rows,
-                     cols, p, seed);
+                     cols, p, seed, dasa_seed_src_host());
   DASA_CHECK_LAUNCH();
   return 0;
 }

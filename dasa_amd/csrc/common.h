@@ -60,6 +60,15 @@ __device__ __forceinline__ float dasa_uniform(uint64_t seed, uint64_t idx) {
   z ^= z >> 31;
   return (float)(z >> 40) * (1.0f / 16777216.0f);  // [0,1)
 }
+// Dropout seed of one launch: the host seed, re-keyed by the 64-bit value at `src` when the launch
+// was recorded with a device seed source (dasa_set_seed_source, used around hipGraph capture), so
+// every replay of a captured graph draws fresh masks after dasa_seed_bump advanced the value.
+__device__ __forceinline__ uint64_t eff_seed(uint64_t seed, const uint64_t* src) {
+  return src ? seed ^ (*src * 0xD1B54A32D192ED03ull) : seed;
+}
+// Host side: the seed source recorded into dropout launches (nullptr = plain host seeds).
+__attribute__((visibility("hidden"))) const uint64_t* dasa_seed_src_host();
+
 __device__ __forceinline__ float dasa_dropout_scale(float p, uint64_t seed, uint64_t idx) {
   if (p <= 0.f) return 1.f;
   return dasa_uniform(seed, idx) >= p ? 1.f / (1.f - p) : 0.f;

@@ -27,6 +27,7 @@ struct Ew4Args {
               // functor argument is promoted to per-thread LDS by hipcc and costs 5-10x)
   float p;
   uint64_t seed;
+  const uint64_t* seed_src;   // eff_seed(): device seed source of a graph-captured launch, or null
 };
 
 __device__ __forceinline__ float4 mul4(const float4 a, const float4 b) {
@@ -80,8 +81,9 @@ struct CopyOp {
 struct DropOp {     // same (seed, logical index r * cols + c) mask as the scalar dropout kernel
   template <class A> __device__ float4 operator()(const float4 (&v)[1], int r, int c4, const A& a) const {
     const uint64_t i = (uint64_t)r * a.cols + 4 * c4;
-    return make_float4(v[0].x * dasa_dropout_scale(a.p, a.seed, i), v[0].y * dasa_dropout_scale(a.p, a.seed, i + 1),
-                       v[0].z * dasa_dropout_scale(a.p, a.seed, i + 2), v[0].w * dasa_dropout_scale(a.p, a.seed, i + 3));
+    const uint64_t sd = eff_seed(a.seed, a.seed_src);
+    return make_float4(v[0].x * dasa_dropout_scale(a.p, sd, i), v[0].y * dasa_dropout_scale(a.p, sd, i + 1),
+                       v[0].z * dasa_dropout_scale(a.p, sd, i + 2), v[0].w * dasa_dropout_scale(a.p, sd, i + 3));
   }
 };
 
@@ -96,6 +98,7 @@ bool try_ew4(const float* const (&in)[NIN], const long (&ld)[NIN], float* out, l
   Ew4Args<NIN> a;
   for (int i = 0; i < NIN; ++i) { a.in[i] = in[i]; a.ld[i] = ld[i]; }
   a.out = out; a.ldo = ldo; a.rows = rows; a.cols4 = cols / 4; a.cols = cols; a.p = p; a.seed = seed;
+  a.seed_src = p > 0.f ? dasa_seed_src_host() : nullptr;
   a.flag = flag;
   // 4 rows per thread once there are enough rows to fill the chip several times over; below that
   // one row per thread (more waves in flight beats more loads per wave there)
@@ -328,4 +331,26 @@ __attribute__((visibility("hidden"))) bool dasa_dropout_vec(const float* x, long
   const float* in[1] = {x};
   const long ld[1] = {ldx};
   return try_ew4<1>(in, ld, y, ldy, rows, cols, DropOp{}, st, p, seed);
+}
+
+// ---- device seed source for graph-captured dropout (include/dasa_hip.h) ----------------------------
+namespace {
+const uint64_t* g_seed_src = nullptr;
+__global__ void seed_bump_kernel(uint64_t* ctr) {
+  if (threadIdx.x == 0) ctr[0] += 1;
+}
+}  // namespace
+
+__attribute__((visibility("hidden"))) const uint64_t* dasa_seed_src_host() { return g_seed_src; }
+
+extern "C" int dasa_set_seed_source(const uint64_t* dev_counter) {
+  g_seed_src = dev_counter;
+  return 0;
+}
+
+extern "C" int dasa_seed_bump(uint64_t* dev_counter, void* stream) {
+  if (!dev_counter) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(seed_bump_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, dev_counter);
+  DASA_CHECK_LAUNCH();
+  return 0;
 }

@@ -27,6 +27,82 @@ def _flat(t):
     return t.reshape(-1, t.shape[-1])
 
 
+# ------------------------------------------------------------------- deferred weight gradients
+class _WGradDeferral:
+    """Weight / bias gradients of one backward pass, computed once per parameter at the end.
+
+    The rollout applies the decoder and critic linears once per step (agent_dg.py:725-993), so the
+    backward of one optimizer step produces ~70 skinny products dW_t = dY_t^T X_t (B = 20 rows each)
+    per weight, each followed by an autograd accumulation into .grad. Under defer_weight_grads() the
+    Functions below queue (dY_t, X_t) instead and flush_weight_grads() computes
+    dW = [dY_1; ...; dY_T]^T [X_1; ...; X_T] as ONE MFMA GEMM (K = T*B) per weight, added into .grad.
+    Same sums, in a different order; input / state gradients still flow step by step."""
+
+    def __init__(self):
+        self.active = False
+        self.w = {}      # id(param) -> [param, [dY], [X]]
+        self.b = {}      # id(param) -> [param, [dY]]
+
+
+_WG = _WGradDeferral()
+
+
+@contextlib.contextmanager
+def defer_weight_grads():
+    prev = _WG.active
+    _WG.active = True
+    try:
+        yield
+    finally:
+        _WG.active = prev
+
+
+def _wgrad(W, dz, x):
+    """dW = dz^T x (both [rows, .]), or queued while weight gradients are deferred (returns None)."""
+    if _WG.active:
+        e = _WG.w.get(id(W))
+        if e is None:
+            e = _WG.w[id(W)] = [W, [], []]
+        e[1].append(dz)
+        e[2].append(x)
+        return None
+    return ops.matmul_tn(dz, x)
+
+
+def _bgrad(b, dz):
+    """db = column sums of dz, or queued while weight gradients are deferred (returns None)."""
+    if _WG.active:
+        e = _WG.b.get(id(b))
+        if e is None:
+            e = _WG.b[id(b)] = [b, []]
+        e[1].append(dz)
+        return None
+    return ops.colsum(dz)
+
+
+def _cat_rows(ts):
+    ts = [_flat(t) for t in ts]
+    return ts[0] if len(ts) == 1 else torch.cat(ts, 0)
+
+
+def flush_weight_grads():
+    """Run the queued weight / bias gradient products into .grad (one GEMM / column sum each)."""
+    w, b = _WG.w, _WG.b
+    _WG.w, _WG.b = {}, {}
+    for P, dzs, xs in w.values():
+        dz, x = _cat_rows(dzs), _cat_rows(xs)
+        if P.grad is None:
+            P.grad = ops.matmul_tn(dz, x)
+        else:
+            ops.matmul_tn(dz, x, out=P.grad, beta=1.0)
+    for P, dzs in b.values():
+        dz = _cat_rows(dzs)
+        if P.grad is None:
+            P.grad = ops.colsum(dz)
+        else:
+            ops.colsum(dz, out=P.grad, beta=1.0)
+
+
 # ------------------------------------------------------------------------------------ Linear
 class LinearFn(torch.autograd.Function):
     """y = act(x W^T + b) (nn.Linear + activation), one fused MFMA GEMM."""
@@ -35,6 +111,7 @@ class LinearFn(torch.autograd.Function):
     def forward(ctx, x, W, b, act):
         ctx.act = act
         ctx.has_b = b is not None
+        ctx.params = (W, b)
         need = any(ctx.needs_input_grad)
         if need and act == "gelu":
             z = ops.linear(x, W, b)
@@ -57,9 +134,9 @@ class LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = ops.matmul_nn(dz, W).view(x.shape)
         if ctx.needs_input_grad[1]:
-            dW = ops.matmul_tn(dz, _flat(x))
+            dW = _wgrad(ctx.params[0], dz, _flat(x))
         if ctx.has_b and ctx.needs_input_grad[2]:
-            db = ops.colsum(dz)
+            db = _bgrad(ctx.params[1], dz)
         return dx, dW, db, None
 
 
@@ -163,6 +240,7 @@ class ShiftAttnFn(torch.autograd.Function):
         wctx, attn, shifted, wsm = ops.shift_attn_fwd(q, feat, z)
         if any(ctx.needs_input_grad):
             ctx.save_for_backward(h, feat, q, attn, shifted, wsm, W_in, W_s)
+            ctx.params = (W_in, W_s, b_s)
         ctx.mark_non_differentiable(attn)
         return wctx, attn
 
@@ -176,11 +254,11 @@ class ShiftAttnFn(torch.autograd.Function):
             dh = ops.matmul_nn(dq, W_in)
             ops.matmul_nn(dz, W_s, out=dh, beta=1.0)
         if ctx.needs_input_grad[2]:
-            dWin = ops.matmul_tn(dq, h)
+            dWin = _wgrad(ctx.params[0], dq, h)
         if ctx.needs_input_grad[3]:
-            dWs = ops.matmul_tn(dz, h)
+            dWs = _wgrad(ctx.params[1], dz, h)
         if ctx.needs_input_grad[4]:
-            dbs = ops.colsum(dz)
+            dbs = _bgrad(ctx.params[2], dz)
         return dh, dfeat, dWin, dWs, dbs
 
 
@@ -198,6 +276,7 @@ class SoftDotTildeFn(torch.autograd.Function):
         y = ops.linear(cat, W_out, act="tanh")
         if any(ctx.needs_input_grad):
             ctx.save_for_backward(h, c, q, probs, cat, y, W_in, W_out)
+            ctx.params = (W_in, W_out)
         ctx.mark_non_differentiable(probs)
         return y, probs
 
@@ -208,7 +287,7 @@ class SoftDotTildeFn(torch.autograd.Function):
         D = c.shape[2]
         dh = dc = dWin = dWout = None
         if ctx.needs_input_grad[4]:
-            dWout = ops.matmul_tn(dz, cat)
+            dWout = _wgrad(ctx.params[1], dz, cat)
         dcat = ops.matmul_nn(dz, W_out)
         dq, dc = ops.softdot_bwd(q, c.contiguous(), probs, dwctx=dcat[:, :D].contiguous(),
                                  want_dctx=ctx.needs_input_grad[1])
@@ -216,7 +295,7 @@ class SoftDotTildeFn(torch.autograd.Function):
             dh = dcat[:, D:].contiguous()
             ops.matmul_nn(dq, W_in, out=dh, beta=1.0)
         if ctx.needs_input_grad[3]:
-            dWin = ops.matmul_tn(dq, h)
+            dWin = _wgrad(ctx.params[0], dq, h)
         return dh, dc, None, dWin, dWout
 
 
@@ -230,6 +309,7 @@ class CandLogitFn(torch.autograd.Function):
         scores, _, _ = ops.softdot_fwd(q, cand, None, want_probs=False, want_wctx=False)
         if any(ctx.needs_input_grad):
             ctx.save_for_backward(h, cand, q, scores, W_in)
+            ctx.params = (W_in,)
         return scores
 
     @staticmethod
@@ -239,7 +319,7 @@ class CandLogitFn(torch.autograd.Function):
         dq, dcand = ops.softdot_bwd(q, cand.contiguous(), scores, dscores=dlogit.contiguous(),
                                     want_dctx=ctx.needs_input_grad[1])
         dh = ops.matmul_nn(dq, W_in) if ctx.needs_input_grad[0] else None
-        dW = ops.matmul_tn(dq, h) if ctx.needs_input_grad[2] else None
+        dW = _wgrad(ctx.params[0], dq, h) if ctx.needs_input_grad[2] else None
         return dh, dcand, dW
 
 
@@ -259,6 +339,7 @@ class LSTMCellFn(torch.autograd.Function):
         h1, c1, act = ops.lstm_cell_fwd(gates, c, save=need)
         if need:
             ctx.save_for_backward(xcat, h, c, c1, act, W_ih, W_hh)
+            ctx.params = (W_ih, W_hh, b_ih, b_hh)
         ctx.E = E
         return h1, c1
 
@@ -275,13 +356,20 @@ class LSTMCellFn(torch.autograd.Function):
             dx2 = dxcat[:, E:].contiguous() if n[1] else None
         if n[2]:
             dh = ops.matmul_nn(dgates, W_hh)
+        P = ctx.params
         if n[4]:
-            dW_ih = ops.matmul_tn(dgates, xcat)
+            dW_ih = _wgrad(P[0], dgates, xcat)
         if n[5]:
-            dW_hh = ops.matmul_tn(dgates, h)
-        if n[6] or n[7]:
-            db = ops.colsum(dgates)
-        return da, dx2, dh, (dc_prev if n[3] else None), dW_ih, dW_hh, db, db
+            dW_hh = _wgrad(P[1], dgates, h)
+        db_ih = db_hh = None
+        if _WG.active:
+            if n[6]:
+                _bgrad(P[2], dgates)
+            if n[7]:
+                _bgrad(P[3], dgates)
+        elif n[6] or n[7]:
+            db_ih = db_hh = ops.colsum(dgates)
+        return da, dx2, dh, (dc_prev if n[3] else None), dW_ih, dW_hh, db_ih, db_hh
 
 
 class _BpttDeferral:

@@ -1,0 +1,100 @@
+"""hipGraph capture of forward-only sub-steps of the rollout (BASELINE north star: "agent_dg.py
+rollout inner loop, hipGraph-captured step").
+
+A decision step of `Seq2SeqAgent.vl_rollout` (agent_dg.py:725-936) launches ~100 kernels for the
+vision encoder and the d_vl_layers LXRT cross-attention layers (vilmodel.py:1067-1095, 1014-1064).
+In the README training configuration those layers are not trained (update_add_layer=False,
+vilmodel.py:1408-1410), so they run without autograd, and in evaluation nothing on the step needs
+autograd. `StepGraphs` captures such a region once per input shape into a HIP graph (torch.cuda.CUDAGraph
+over torch's HIP streams, including the LXRT side stream the region forks and joins) and replays it:
+one host call per step instead of ~100 Python-level launches.
+
+Dropout inside a captured region stays random per replay: the region is captured with the library's
+device seed source set (include/dasa_hip.h dasa_set_seed_source), the graph's first node bumps that
+counter (dasa_seed_bump), and every captured dropout kernel keys its mask on (host seed, counter).
+
+Inputs are copied into the graph's static input buffers before a replay; outputs are cloned out of
+the static output buffers (the bi-LSTM that consumes them keeps its input for the deferred backward,
+and the next replay overwrites the static buffers). A captured region is re-captured when any
+parameter of the modules it reads changes (data pointer or in-place version), e.g. after load_state_dict.
+"""
+import ctypes
+import os
+
+import torch
+
+from . import _lib
+from . import prof
+
+ENABLED = os.environ.get("DASA_GRAPH", "1") != "0"
+
+
+class _Entry:
+    __slots__ = ("graph", "static_in", "static_out", "pkey")
+
+
+class StepGraphs:
+    """Per-owner cache of captured forward regions, keyed by the caller's shape key."""
+
+    def __init__(self, modules):
+        self.modules = list(modules)   # the nn.Modules whose parameters the region reads
+        self.entries = {}
+        self.counter = None         # device seed counter (uint64), bumped by every replay
+        self.captures = 0
+        self.replays = 0
+
+    def _param_key(self):
+        return tuple((p.data_ptr(), p._version) for m in self.modules for p in m.parameters())
+
+    def _capture(self, fn, inputs):
+        dev = inputs[0].device
+        if self.counter is None:
+            self.counter = torch.zeros(1, dtype=torch.int64, device=dev)
+        static_in = tuple(torch.empty_strided(x.shape, x.stride(), dtype=x.dtype, device=dev) for x in inputs)
+        for s, x in zip(static_in, inputs):
+            s.copy_(x)
+        # warm-up on a side stream: builds every lazily cached tensor (fused QKV weights, workspaces)
+        # outside the capture, as torch.cuda.graphs requires
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side), torch.no_grad():
+            fn(*static_in)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize(dev)
+        g = torch.cuda.CUDAGraph()
+        L = _lib.lib()
+        ctr = ctypes.c_void_p(self.counter.data_ptr())
+        L.dasa_set_seed_source(ctr)
+        try:
+            with torch.cuda.graph(g), torch.no_grad():
+                _lib.check(L.dasa_seed_bump(ctr, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
+                           "dasa_seed_bump")
+                out = fn(*static_in)
+        finally:
+            L.dasa_set_seed_source(None)
+        e = _Entry()
+        e.graph, e.static_in, e.static_out = g, static_in, out
+        e.pkey = self._param_key()
+        self.captures += 1
+        return e
+
+    def run(self, key, fn, inputs):
+        """fn(*inputs) -> tuple of tensors, forward-only; returns fresh copies of its outputs."""
+        if prof.active():     # per-launch HIP-event profiling (bench.py's kernel table) runs eagerly
+            with torch.no_grad():
+                return fn(*inputs)
+        e = self.entries.get(key)
+        if e is not None and e.pkey != self._param_key():
+            del self.entries[key]
+            e = None
+        if e is None:
+            e = self._capture(fn, inputs)
+            self.entries[key] = e
+        for s, x in zip(e.static_in, inputs):
+            s.copy_(x)
+        e.graph.replay()
+        self.replays += 1
+        return tuple(o.clone() for o in e.static_out)
+
+    def clear(self):
+        self.entries.clear()

@@ -515,14 +515,24 @@ class Seq2SeqAgent(BaseAgent):
             # Teacher forcing: the actions (and so every observation of the episode) do not depend
             # on the policy, so the env is stepped first and the encoder runs once for all steps.
             # Chunked: the host steps the env for chunk k+1 while the GPU encodes and decodes chunk k.
+            # The env is stepped one chunk ahead: chunk k+1 is planned on the host right after chunk
+            # k's encoder is enqueued, while the GPU runs it (the first chunk is half-size so the GPU
+            # starts early).
             self.encoder.cache_language(not self.encoder.training, steps=0)
             chunk = max(1, int(os.environ.get("DASA_TEACHER_CHUNK", "8")))
             t = 0
-            while t < self.episode_len and not ended.all():
-                n = min(chunk if t else max(1, chunk // 2), self.episode_len - t)
-                plan, perm_obs = self._teacher_plan(perm_obs, perm_idx, ended, last_dist, traj, n)
+            plan = []
+            if not ended.all():
+                plan, perm_obs = self._teacher_plan(perm_obs, perm_idx, ended, last_dist, traj,
+                                                    min(max(1, chunk // 2), self.episode_len))
+            while plan:
                 enc = self._encode_steps([s["obs"] for s in plan], *enc_args)
                 targets = self._to_dev(np.stack([s["target_np"] for s in plan]))
+                t_next = t + len(plan)
+                nxt = []
+                if t_next < self.episode_len and not ended.all():
+                    nxt, perm_obs = self._teacher_plan(perm_obs, perm_idx, ended, last_dist, traj,
+                                                       min(chunk, self.episode_len - t_next))
                 for i, (s, e) in enumerate(zip(plan, enc)):
                     if t == 0:
                         h_t, c_t, logit, h1, aux = self.decoder(e["a"], e["df"], e["cand"], e["en_ht"], e["en_ht"],
@@ -543,6 +553,7 @@ class Seq2SeqAgent(BaseAgent):
                                                           self._back_teacher_action(s["obs"], s["ended"]))
                     rewards.append(s["reward"])
                     masks.append(s["mask"])
+                plan = nxt
         else:
             self.encoder.cache_language(not self.encoder.training, steps=self.episode_len)
             for t in range(self.episode_len):
@@ -621,26 +632,34 @@ class Seq2SeqAgent(BaseAgent):
                 f_t = self._noise_mult(f_t, noise)
             last_h_, _, _, _, _ = self.decoder(input_a_t, f_t, candidate_feat, h_t, h1, c_t, ctx, ctx_mask,
                                                speaker is not None)
-            rl_loss = 0.0
             last_value__ = self.critic(last_h_).detach().view(-1).cpu().numpy()
             discount_reward = np.zeros(batch_size, np.float32)
             for i in range(batch_size):
                 if not ended[i]:
                     discount_reward[i] = last_value__[i]
+            # agent_dg.py:955-993 for all steps at once: the discounted returns are accumulated on the
+            # host (same recursion), the critic runs once over the [T*B, 1024] stack of step states
+            # (its dropout draws stay independent per element), and the per-step loss terms are
+            # vectors over T summed in the reference's (reverse-step) order.
             length = len(rewards)
-            total = 0
+            R = np.zeros((length, batch_size), np.float32)
             for t in range(length - 1, -1, -1):
                 discount_reward = discount_reward * args.gamma + rewards[t]
-                mask_ = torch.from_numpy(masks[t]).to(self.device)
-                r_ = torch.from_numpy(discount_reward.copy()).to(self.device)
-                v_ = self.critic(hidden_states[t])
-                a_ = (r_ - v_).detach()
-                rl_loss += (-policy_log_probs[t].view(-1) * a_ * mask_).sum()
-                rl_loss += (((r_ - v_) ** 2) * mask_).sum() * 0.5
-                if self.feedback == "sample":
-                    rl_loss += (-0.01 * entropys[t] * mask_).sum()
-                deferred["critic_loss"].append((((r_ - v_) ** 2) * mask_).sum().detach())
-                total = total + np.sum(masks[t])
+                R[t] = discount_reward
+            Mk = np.stack(masks).astype(np.float32)
+            rm = self._to_dev(np.stack((R, Mk)))
+            r_, mask_ = rm[0], rm[1]
+            H = torch.stack(hidden_states)
+            v_ = self.critic(H.view(length * batch_size, -1)).view(length, batch_size)
+            a_ = (r_ - v_).detach()
+            lp = torch.stack([p.view(-1) for p in policy_log_probs])
+            sq = ((r_ - v_) ** 2) * mask_
+            terms = (-lp * a_ * mask_).sum(1) + sq.sum(1) * 0.5
+            if self.feedback == "sample":
+                terms = terms + (-0.01 * torch.stack(entropys) * mask_).sum(1)
+            rl_loss = terms.flip(0).sum()
+            deferred["critic_loss"].extend(sq.sum(1).detach().flip(0).unbind(0))
+            total = float(Mk.sum())
             self.logs["total"].append(total)
             if args.normalize_loss == "total":
                 rl_loss /= total
@@ -718,9 +737,12 @@ class Seq2SeqAgent(BaseAgent):
 
     def optim_step(self, **kwargs):
         """agent_dg.py:1389-1405 (+ data-parallel gradient all-reduce before clipping)."""
-        with DF.defer_bilstm_backward():     # the encoder's per-step bi-LSTM BPTTs run batched below
+        # the encoder's per-step bi-LSTM BPTTs and the per-step decoder / critic weight gradients run
+        # batched after the backward pass (dasa_amd/functional.py)
+        with DF.defer_bilstm_backward(), DF.defer_weight_grads():
             self.loss.backward()
         DF.flush_bilstm_backward()
+        DF.flush_weight_grads()
         if self.grad_sync is not None:
             self.grad_sync()
         torch.nn.utils.clip_grad_norm_(self.encoder.parameters(), 40.0)

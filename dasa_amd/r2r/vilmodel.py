@@ -13,6 +13,7 @@ import torch
 import torch.nn as nn
 
 from .. import functional as DF
+from .. import graph
 from .. import ops
 from .param import args
 
@@ -68,6 +69,8 @@ def _fused_weights(owner, mods):
     key = tuple((t.data_ptr(), t._version) for t in params)
     cache = getattr(owner, "_fused_cache", None)
     cur = torch.cuda.current_stream()
+    if cache is not None and cache[0] == key and torch.cuda.is_current_stream_capturing():
+        return cache[1], cache[2]    # built by the pre-capture warm-up, which the capture stream follows
     if cache is None or cache[0] != key:
         with torch.no_grad():
             W = torch.cat([m.weight for m in mods], 0).contiguous()
@@ -312,7 +315,8 @@ class LXRTXLayer(nn.Module):
         la = self.lang_self_att(la, lang_attention_mask)[0]
         lang = self.lang_output(self.lang_inter(la), la)
         main.wait_stream(side)
-        visn.record_stream(main)
+        if not torch.cuda.is_current_stream_capturing():
+            visn.record_stream(main)
         return lang, visn
 
 
@@ -349,6 +353,7 @@ class DicModel(nn.Module):
         self.lalayer = nn.ModuleList([BertLayer(config) for _ in range(self.la_layers)])
         self.addlayer = nn.ModuleList([LXRTXLayer(config) for _ in range(self.vl_layers)])
         self.vision_encoder = VisionEncoder(self.config.img_feature_dim, self.config)
+        self._graphs = None     # captured forward-only VL stacks (dasa_amd/graph.py)
         if args.d_v_layers > 0:
             self.vlayer = nn.ModuleList([BertLayer(config) for _ in range(args.d_v_layers)])
         self.init_weights()
@@ -363,6 +368,19 @@ class DicModel(nn.Module):
             elif isinstance(m, nn.LayerNorm):
                 m.weight.data.fill_(1.0)
                 m.bias.data.zero_()
+
+    def _vl_stack(self, text_embeds, ext, img_feats):
+        """VisionEncoder + the vl LXRT layers (vilmodel.py:1383-1406)."""
+        B, V = img_feats.shape[0], img_feats.shape[1]
+        img_mask = torch.zeros(B, 1, 1, V, dtype=torch.float32, device=img_feats.device)
+        lang = text_embeds
+        visn = self.vision_encoder(img_feats)
+        if args.d_v_layers > 0:
+            for layer in self.vlayer:
+                visn = layer(visn, img_mask)[0]
+        for layer in self.addlayer:
+            lang, visn = layer(lang, ext, visn, img_mask)
+        return lang, visn
 
     def language(self, input_ids, ext_mask):
         """Embeddings + the la_layers language BertLayers (vilmodel.py:1366-1372)."""
@@ -385,16 +403,18 @@ class DicModel(nn.Module):
             text_embeds = text_embeds.detach()
         visn_output = None
         if img_feats is not None:
-            with torch.set_grad_enabled(torch.is_grad_enabled() and self.update_add_layer):
-                B, V = img_feats.shape[0], img_feats.shape[1]
-                img_mask = torch.zeros(B, 1, 1, V, dtype=torch.float32, device=img_feats.device)
-                lang = text_embeds
-                visn = self.vision_encoder(img_feats)
-                if args.d_v_layers > 0:
-                    for layer in self.vlayer:
-                        visn = layer(visn, img_mask)[0]
-                for layer in self.addlayer:
-                    lang, visn = layer(lang, ext, visn, img_mask)
+            vl_grad = torch.is_grad_enabled() and self.update_add_layer
+            if not vl_grad and graph.ENABLED and img_feats.is_cuda:
+                # forward-only: one hipGraph replay per step (dasa_amd/graph.py)
+                if self._graphs is None:
+                    mods = [self.vision_encoder, self.addlayer] + ([self.vlayer] if args.d_v_layers > 0 else [])
+                    self._graphs = graph.StepGraphs(mods)
+                key = (tuple(text_embeds.shape), tuple(ext.shape), tuple(img_feats.shape), img_feats.stride(),
+                       self.training)
+                lang, visn = self._graphs.run(key, self._vl_stack, (text_embeds, ext, img_feats))
+            else:
+                with torch.set_grad_enabled(vl_grad):
+                    lang, visn = self._vl_stack(text_embeds, ext, img_feats)
             if not self.update_add_layer:
                 lang, visn = lang.detach(), visn.detach()
             sequence_output = lang

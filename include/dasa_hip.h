@@ -191,6 +191,14 @@ int dasa_gather_rows(const float* ta, const int32_t* ia, int32_t Fa, const float
 /* Reverse the first lengths[b] rows of x [B][L][H] into out (rest zero), r2rmodel.py:2326-2330. */
 int dasa_reverse_valid(const float* x, const int32_t* lengths, float* out, int32_t B, int32_t L,
                        int32_t H, void* stream);
+/* Device seed source for hipGraph capture. While a counter is set (dev_counter != NULL), every
+ * forward dropout launch (layernorm, embeddings, attention probabilities, dropout) records it, and
+ * its mask seed becomes seed ^ mix(*dev_counter) read at run time: a captured graph that starts with
+ * dasa_seed_bump(dev_counter) draws fresh masks on every replay. Host-only setting, not thread-safe;
+ * set it only around capture of forward-only (no-grad) work (backward kernels use plain seeds). */
+int dasa_set_seed_source(const uint64_t* dev_counter);
+int dasa_seed_bump(uint64_t* dev_counter, void* stream);
+
 /* y[i] = x[i] * keep(seed, i) / (1-p) for a [rows][cols] block with row stride ld (in place ok). */
 int dasa_dropout_fwd(const float* x, int64_t ldx, float* y, int64_t ldy, int32_t rows, int32_t cols,
                      float p, uint64_t seed, void* stream);

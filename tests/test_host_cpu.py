@@ -36,7 +36,10 @@ def test_gemm_workspace_query_is_host_only():
     d.M, d.N, d.K, d.batch, d.opA, d.opB = 20, 4096, 2240, 1, 0, 1
     assert _lib.lib().dasa_gemm_f32_workspace(ctypes.byref(d)) > 0      # skinny decoder GEMM: split-K
     d.M, d.N, d.K = 1600, 3072, 768
-    assert _lib.lib().dasa_gemm_f32_workspace(ctypes.byref(d)) == 0     # plenty of tiles: no split
+    cnt = 64 << 10                                                       # stream-K arrival counters
+    assert _lib.lib().dasa_gemm_f32_workspace(ctypes.byref(d)) == cnt   # plenty of tiles: no split
+    d.M, d.N, d.K = 1040, 2048, 2048
+    assert _lib.lib().dasa_gemm_f32_workspace(ctypes.byref(d)) > cnt    # mid-size long K: stream-K slabs
 
 
 def test_product_schema_matches_reference():

@@ -198,7 +198,8 @@ def test_rollout_eval_argmax(R, dev, host_path):
 @pytest.mark.parametrize("deferred", [False, True])
 def test_train_iteration_grads(R, dev, deferred):
     """accumulate_gradient('sample') + backward with every dropout p = 0 and argmax 'sampling'.
-    deferred: the bi-LSTM BPTTs of all encoder calls run as one batched recurrence (optim_step's path)."""
+    deferred: the bi-LSTM BPTTs of all encoder calls run as one batched recurrence and the decoder /
+    critic weight gradients of all steps as one GEMM per parameter (optim_step's path)."""
     from dasa_amd import functional as DF
     param = R[0]
     G = golden("cfg1_rollout")
@@ -220,10 +221,11 @@ def test_train_iteration_grads(R, dev, deferred):
     assert abs(ag.logs["normalized_rl_loss"][-1] - float(G["train/rl_loss"])) < TOL
     assert ag.logs["viewsteps/teacher"][-1] == int(G["train/steps_teacher"])
     assert ag.logs["viewsteps/sample"][-1] == int(G["train/steps_sample"])
-    if deferred:
-        with DF.defer_bilstm_backward():
+    if deferred:    # optim_step's path: batched bi-LSTM BPTT + per-parameter weight-gradient GEMMs
+        with DF.defer_bilstm_backward(), DF.defer_weight_grads():
             ag.loss.backward()
         DF.flush_bilstm_backward()
+        DF.flush_weight_grads()
     else:
         ag.loss.backward()
     n = 0
@@ -305,3 +307,42 @@ def test_cfg2_step_vs_oracle(R, dev):
         close(rec["h_tilde"], r["states"][0][2], TOL, "cfg2 h_tilde")
     finally:
         param.readme_train(["--d_vl_layers", "1", "--batchSize", "2", "--maxAction", "5"])
+
+
+def test_vl_stack_graph_replay(R, dev, monkeypatch):
+    """The forward-only VisionEncoder + LXRT stack as a hipGraph replay (dasa_amd/graph.py): bitwise
+    equal to the eager launches in eval; in train mode every replay draws fresh dropout masks (device
+    seed counter) and stays a proper dropout of the same computation."""
+    from dasa_amd import graph
+    param, vilmodel = R[0], R[4]
+    cfg = vilmodel.BertConfig()
+    cfg.img_feature_dim, cfg.img_feature_type = 2176, ""
+    cfg.update_lang_bert, cfg.update_add_layer, cfg.vl_layers, cfg.la_layers = False, False, 2, 1
+    m = init_params(vilmodel.DicModel(cfg), 77).to(dev)
+    g = torch.Generator().manual_seed(5)
+    B, L = 3, 11
+    ids = torch.randint(1, 1000, (B, L), generator=g).to(dev)
+    att = torch.ones(B, L, dtype=torch.long, device=dev)
+    att[1, 7:] = 0
+    img = torch.rand(B, 36, 2176, generator=g).to(dev)
+    m.eval()
+    with torch.no_grad():
+        monkeypatch.setattr(graph, "ENABLED", False)
+        ref_l, _, ref_v = m(ids, None, att, img_feats=img)
+        monkeypatch.setattr(graph, "ENABLED", True)
+        for _ in range(2):
+            out_l, _, out_v = m(ids, None, att, img_feats=img)
+            assert torch.equal(out_l, ref_l) and torch.equal(out_v, ref_v)
+    assert m._graphs is not None and m._graphs.captures == 1 and m._graphs.replays == 2
+    m.train()
+    text = m.language(ids, ((1.0 - att.float()) * -10000.0)[:, None, None, :]).detach()
+    with torch.no_grad():
+        a = m(ids, None, att, img_feats=img, text_embeds=text)[2]
+        b = m(ids, None, att, img_feats=img, text_embeds=text)[2]
+        monkeypatch.setattr(graph, "ENABLED", False)
+        c = m(ids, None, att, img_feats=img, text_embeds=text)[2]
+    assert torch.isfinite(a).all() and torch.isfinite(b).all()
+    assert not torch.equal(a, b)                        # fresh masks per replay
+    for x in (a, b):                                    # same distribution as the eager dropout draw
+        assert abs(x.std().item() - c.std().item()) < 0.1 * c.std().item()
+        assert (x - c).abs().mean().item() < 2.0 * (c - ref_v).abs().mean().item() + 1e-3

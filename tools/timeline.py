@@ -1,0 +1,63 @@
+"""GPU busy/idle analysis of a rocprofv3 --kernel-trace CSV (one bench run): splits the run at the
+long host-side gaps, then reports per window the wall span, the union of kernel intervals (busy),
+idle gaps by size, and the top kernels by time."""
+import csv
+import sys
+from collections import defaultdict
+
+
+def load(path):
+    rows = []
+    for r in csv.DictReader(open(path)):
+        rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], int(r.get("Stream_Id") or 0)))
+    rows.sort()
+    return rows
+
+
+def union_busy(rows):
+    busy, cur_s, cur_e, gaps = 0, None, None, []
+    for s, e, _, _ in rows:
+        if cur_e is None:
+            cur_s, cur_e = s, e
+        elif s > cur_e:
+            busy += cur_e - cur_s
+            gaps.append(s - cur_e)
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    if cur_e is not None:
+        busy += cur_e - cur_s
+    return busy, gaps
+
+
+def main(path, t_last_ms=None):
+    rows = load(path)
+    t0, t1 = rows[0][0], max(r[1] for r in rows)
+    print(f"kernels {len(rows)}  span {(t1 - t0) / 1e6:.1f} ms")
+    # the last iteration = the window after the last gap > 20 ms before the end, roughly; report the
+    # whole trace's last `t_last_ms` ms if given
+    if t_last_ms:
+        rows = [r for r in rows if r[0] >= t1 - t_last_ms * 1e6]
+    busy, gaps = union_busy(rows)
+    span = max(r[1] for r in rows) - rows[0][0]
+    print(f"window span {span / 1e6:.1f} ms  busy {busy / 1e6:.1f} ms  idle {(span - busy) / 1e6:.1f} ms")
+    hist = defaultdict(lambda: [0, 0])
+    for g in gaps:
+        k = "<2us" if g < 2e3 else "<10us" if g < 1e4 else "<100us" if g < 1e5 else "<1ms" if g < 1e6 else ">=1ms"
+        hist[k][0] += 1
+        hist[k][1] += g
+    for k in ("<2us", "<10us", "<100us", "<1ms", ">=1ms"):
+        print(f"  gaps {k:>7}: {hist[k][0]:6d}  total {hist[k][1] / 1e6:8.2f} ms")
+    big = sorted(gaps, reverse=True)[:15]
+    print("  largest gaps (ms):", " ".join(f"{g / 1e6:.2f}" for g in big))
+    per = defaultdict(lambda: [0, 0])
+    for s, e, n, _ in rows:
+        k = n.split("(")[0][:70]
+        per[k][0] += 1
+        per[k][1] += e - s
+    for k, (c, t) in sorted(per.items(), key=lambda kv: -kv[1][1])[:25]:
+        print(f"  {k:<70} {c:6d} {t / 1e6:9.2f} ms")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], float(sys.argv[2]) if len(sys.argv) > 2 else None)
