@@ -323,6 +323,39 @@ class CandLogitFn(torch.autograd.Function):
         return dh, dcand, dW
 
 
+# ------------------------------------------------------------------------------ policy head
+class PolicyHeadFn(torch.autograd.Function):
+    """agent_dg.py:832-880 in one kernel: logit.masked_fill(cand_mask, -inf) -> CrossEntropyLoss(sum,
+    ignore_index) against the teacher target, and the action (argmax, or a Categorical draw) with its
+    entropy and log-probability. Returns (ce_sum, entropy [B], logp_action [B], action [B] int64)."""
+
+    @staticmethod
+    def forward(ctx, logit, cand_len_i32, target, mode, seed, ignore_index):
+        ce, ent, lpa, action, logp = ops.policy_head_fwd(logit, cand_len_i32, target, mode, seed, ignore_index)
+        ctx.save_for_backward(logp, cand_len_i32, target, action, ent)
+        ctx.ignore = ignore_index
+        if action is None:   # teacher mode: no action drawn
+            action = torch.empty(0, dtype=torch.int64, device=logit.device)
+        ctx.mark_non_differentiable(action)
+        return ce, ent, lpa, action
+
+    @staticmethod
+    def backward(ctx, d_ce, d_ent, d_lpa, _d_action):
+        logp, lens, target, action, ent = ctx.saved_tensors
+        if action is not None and action.numel() == 0:
+            action = None
+        dlogit = ops.policy_head_bwd(logp, lens, target, action, ent,
+                                     d_ce.reshape(1).contiguous() if d_ce is not None else None,
+                                     d_lpa.contiguous() if d_lpa is not None else None,
+                                     d_ent.contiguous() if d_ent is not None else None, ctx.ignore)
+        return dlogit, None, None, None, None, None
+
+
+def policy_head(logit, cand_len_i32, target, mode, ignore_index=-100):
+    seed = new_seed() if mode == "sample" else 0
+    return PolicyHeadFn.apply(logit, cand_len_i32, target, mode, seed, ignore_index)
+
+
 # ----------------------------------------------------------------------------------- LSTM
 class LSTMCellFn(torch.autograd.Function):
     """nn.LSTMCell on the concatenated input [a_emb, attn_feat] (model.py:513-514)."""

@@ -327,6 +327,40 @@ def mha_bwd(Q, K, V, probs, dout, heads, scale, drop_p=0.0, seed=0):
     return dQ, dK, dV
 
 
+# ------------------------------------------------------------------------------ policy head
+POLICY_MODES = {"teacher": 0, "argmax": 1, "sample": 2}
+
+
+def policy_head_fwd(logit, cand_len_i32, target, mode, seed, ignore_index=-100):
+    """One step's candidate mask + CE + action (include/dasa_hip.h dasa_policy_head_fwd).
+    Returns (ce_sum [], ent [B], logp_a [B], action [B] int64 or None, logp [B, C])."""
+    _f32(logit, "policy_head.logit")
+    B, C = logit.shape
+    assert logit.stride(1) == 1
+    dev = logit.device
+    logp = torch.empty(B, C, dtype=torch.float32, device=dev)
+    ce = torch.empty((), dtype=torch.float32, device=dev)
+    ent = torch.empty(B, dtype=torch.float32, device=dev)
+    logp_a = torch.empty(B, dtype=torch.float32, device=dev)
+    m = POLICY_MODES[mode]
+    action = torch.empty(B, dtype=torch.int64, device=dev) if m != 0 else None
+    ws = torch.empty(B, dtype=torch.float32, device=dev)
+    tgt = target.contiguous() if target is not None else None
+    _call("dasa_policy_head_fwd", "policy_head", _lib.lib().dasa_policy_head_fwd, _p(logit), logit.stride(0),
+          _p(cand_len_i32), _p(tgt), B, C, m, int(ignore_index), int(seed), _p(logp), _p(ce), _p(ent),
+          _p(logp_a), _p(action), _p(ws), _stream(), nbytes=4.0 * B * (3 * C + 6))
+    return ce, ent, logp_a, action, logp
+
+
+def policy_head_bwd(logp, cand_len_i32, target, action, ent, d_ce, d_logp_a, d_ent, ignore_index=-100):
+    B, C = logp.shape
+    dlogit = torch.empty(B, C, dtype=torch.float32, device=logp.device)
+    _call("dasa_policy_head_bwd", "policy_head", _lib.lib().dasa_policy_head_bwd, _p(logp), _p(cand_len_i32),
+          _p(target), _p(action), _p(ent), _p(d_ce), _p(d_logp_a), _p(d_ent), _p(dlogit), C, B, C,
+          int(ignore_index), _stream(), nbytes=4.0 * B * 3 * C)
+    return dlogit
+
+
 # ------------------------------------------------------------------------------ SoftDot attention
 _AWS = {}
 

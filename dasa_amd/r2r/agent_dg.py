@@ -218,6 +218,15 @@ class Seq2SeqAgent(BaseAgent):
         return (sorted_tensor.long().to(self.device), mask.bool().to(self.device), list(seq_lengths),
                 list(perm_idx), progresses)
 
+    def _fused_head(self, logit):
+        """The one-kernel policy head (dasa_policy_head_fwd) applies unless a host-side mask edit
+        (--submit), the back-prediction head (its mask is reused) or the sampling test hook is on."""
+        return (not args.submit and not args.pred_back and self.sample_fn is None and logit.shape[1] <= 256
+                and os.environ.get("DASA_FUSED_HEAD", "1") != "0")
+
+    def _lens_dev(self, leng):
+        return self._to_dev(np.asarray(leng, dtype=np.int32))
+
     def _to_dev(self, arr):
         return torch.from_numpy(arr).pin_memory().to(self.device, non_blocking=True)
 
@@ -288,36 +297,47 @@ class Seq2SeqAgent(BaseAgent):
         return torch.from_numpy(a).to(self.device)
 
     def make_equiv_action(self, a_t, perm_obs, perm_idx=None, traj=None):
-        """agent_dg.py:358-391."""
-        def take_action(i, idx, name):
+        """agent_dg.py:358-391. Simulators exposing quick_state() (the synthetic MatterSim stand-in)
+        are polled without building a SimState per turn; same actions, same trajectory."""
+        sims = self.env.env.sims
+
+        def take_action(i, sim, name):
             if type(name) is int:
-                self.env.env.sims[idx].makeAction(name, 0, 0)
+                sim.makeAction(name, 0, 0)
             else:
-                self.env.env.sims[idx].makeAction(*self.env_actions[name])
-            state = self.env.env.sims[idx].getState()
+                sim.makeAction(*self.env_actions[name])
             if traj is not None:
-                traj[i]["path"].append((state.location.viewpointId, state.heading, state.elevation))
+                if hasattr(sim, "quick_state"):
+                    traj[i]["path"].append(sim.quick_state()[:3])
+                else:
+                    state = sim.getState()
+                    traj[i]["path"].append((state.location.viewpointId, state.heading, state.elevation))
+
+        def view_index(sim):
+            return sim.quick_state()[3] if hasattr(sim, "quick_state") else sim.getState().viewIndex
         if perm_idx is None:
             perm_idx = range(len(perm_obs))
         for i, idx in enumerate(perm_idx):
             action = a_t[i]
             if action != -1:
+                sim = sims[idx]
                 select_candidate = perm_obs[i]["candidate"][action]
                 src_point = perm_obs[i]["viewIndex"]
                 trg_point = select_candidate["pointId"]
                 src_level = src_point // 12
                 trg_level = trg_point // 12
                 while src_level < trg_level:
-                    take_action(i, idx, "up")
+                    take_action(i, sim, "up")
                     src_level += 1
                 while src_level > trg_level:
-                    take_action(i, idx, "down")
+                    take_action(i, sim, "down")
                     src_level -= 1
-                while self.env.env.sims[idx].getState().viewIndex != trg_point:
-                    take_action(i, idx, "right")
-                assert select_candidate["viewpointId"] == \
-                    self.env.env.sims[idx].getState().navigableLocations[select_candidate["idx"]].viewpointId
-                take_action(i, idx, select_candidate["idx"])
+                while view_index(sim) != trg_point:
+                    take_action(i, sim, "right")
+                nav_id = (sim.navigable_id(select_candidate["idx"]) if hasattr(sim, "navigable_id") else
+                          sim.getState().navigableLocations[select_candidate["idx"]].viewpointId)
+                assert select_candidate["viewpointId"] == nav_id
+                take_action(i, sim, select_candidate["idx"])
 
     # ------------------------------------------------------------------ the rollout
     def _noise_mult(self, x, noise):
@@ -544,9 +564,12 @@ class Seq2SeqAgent(BaseAgent):
                     t += 1
                     ctx = e["ctx"]
                     hidden_states.append(h_t)
-                    candidate_mask = utils.length2mask(e["leng"], device=self.device)
-                    logit = logit.masked_fill(candidate_mask, -float("inf"))
-                    total_forth_loss += self.criterion(logit, targets[i])
+                    if self._fused_head(logit):
+                        total_forth_loss += DF.policy_head(logit, self._lens_dev(e["leng"]), targets[i], "teacher")[0]
+                    else:
+                        candidate_mask = utils.length2mask(e["leng"], device=self.device)
+                        logit = logit.masked_fill(candidate_mask, -float("inf"))
+                        total_forth_loss += self.criterion(logit, targets[i])
                     if args.pred_back:
                         back_logit = aux["back_logit"].masked_fill(candidate_mask, -float("inf"))
                         total_back_loss += self.criterion(back_logit,
@@ -563,7 +586,6 @@ class Seq2SeqAgent(BaseAgent):
                 target = self._to_dev(target_np)
                 (e,) = self._encode_steps([perm_obs], *enc_args)
                 candidate_leng = e["leng"]
-                candidate_mask = utils.length2mask(candidate_leng, device=self.device)
                 ctx = e["ctx"]
                 if t == 0:
                     h_t, c_t, logit, h1, aux_outputs = self.decoder(e["a"], e["df"], e["cand"], e["en_ht"],
@@ -573,7 +595,23 @@ class Seq2SeqAgent(BaseAgent):
                     h_t, c_t, logit, h1, aux_outputs = self.decoder(e["a"], e["df"], e["cand"], h_t, h1, c_t, ctx,
                                                                     ctx_mask, already_dropfeat=consistent_drop)
                 hidden_states.append(h_t)
-                if args.submit:
+                fused = self._fused_head(logit)
+                if fused:          # mask + CE + action + entropy / log-prob in one kernel (policy.hip)
+                    ce, ent, lpa, a_dev = DF.policy_head(logit, self._lens_dev(candidate_leng), target, self.feedback)
+                    total_forth_loss += ce
+                    if self.feedback == "argmax":
+                        a_t = a_dev
+                        policy_log_probs.append(lpa.unsqueeze(1))
+                    elif self.feedback == "sample":
+                        deferred["entropy"].append(ent.sum().detach())
+                        entropys.append(ent)
+                        a_t = a_dev
+                        policy_log_probs.append(lpa)
+                    else:
+                        a_t = target
+                else:
+                    candidate_mask = utils.length2mask(candidate_leng, device=self.device)
+                if not fused and args.submit:
                     cm = candidate_mask.cpu()
                     for ob_id, ob in enumerate(perm_obs):
                         visited[ob_id].add(ob["viewpoint"])
@@ -581,13 +619,16 @@ class Seq2SeqAgent(BaseAgent):
                             if c["viewpointId"] in visited[ob_id]:
                                 cm[ob_id][c_id] = 1
                     candidate_mask = cm.to(self.device)
-                logit = logit.masked_fill(candidate_mask, -float("inf"))
-                forth_loss = self.criterion(logit, target)
-                total_forth_loss += forth_loss
+                if not fused:
+                    logit = logit.masked_fill(candidate_mask, -float("inf"))
+                    forth_loss = self.criterion(logit, target)
+                    total_forth_loss += forth_loss
                 if args.pred_back:
                     back_logit = aux_outputs["back_logit"].masked_fill(candidate_mask, -float("inf"))
                     total_back_loss += self.criterion(back_logit, self._back_teacher_action(perm_obs, ended))
-                if self.feedback == "teacher":
+                if fused:
+                    pass
+                elif self.feedback == "teacher":
                     a_t = target
                 elif self.feedback == "argmax":
                     _, a_t = logit.max(1)

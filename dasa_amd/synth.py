@@ -265,6 +265,14 @@ class SynthSim:
             elevation = -ELEVATION_INC
         self._set_heading_elevation(self.heading + heading, self.elevation + elevation)
 
+    def quick_state(self):
+        """(viewpointId, heading, elevation, viewIndex) without building a SimState: the agent's turn
+        loop polls the view index after every makeAction (agent_dg.py:376-386)."""
+        return self.world.ids[self.vp], self.heading, self.elevation, self.view_index
+
+    def navigable_id(self, k):
+        return self.world.ids[self.navigable()[k]]
+
     def getState(self):
         s = _State()
         s.scanId = "synth"

@@ -191,6 +191,25 @@ int dasa_gather_rows(const float* ta, const int32_t* ia, int32_t Fa, const float
 /* Reverse the first lengths[b] rows of x [B][L][H] into out (rest zero), r2rmodel.py:2326-2330. */
 int dasa_reverse_valid(const float* x, const int32_t* lengths, float* out, int32_t B, int32_t L,
                        int32_t H, void* stream);
+/* ---- policy head (agent_dg.py:832-886) ------------------------------------------------------- */
+enum dasa_policy_mode { DASA_POLICY_TEACHER = 0, DASA_POLICY_ARGMAX = 1, DASA_POLICY_SAMPLE = 2 };
+/* One decision step's loss/action stage on logit [B][C] (row stride ld): candidates c >= cand_len[b]
+ * are masked (-inf); logp [B][C] = masked log-softmax (saved for backward); ce_sum[0] = sum over rows
+ * with target != ignore_index of -logp[target] (CrossEntropyLoss(reduction='sum')); mode ARGMAX:
+ * action = first argmax; mode SAMPLE: action ~ Categorical(softmax) by inverse CDF on the counter RNG
+ * (seed, row); ent [B] = entropy, logp_a [B] = logp[action] (each optional). target may be NULL (no
+ * CE, ce_sum = 0). C <= 256. ws: B floats of scratch. One launch, deterministic. */
+int dasa_policy_head_fwd(const float* logit, int64_t ld, const int32_t* cand_len, const int64_t* target,
+                         int32_t B, int32_t C, int32_t mode, int32_t ignore_index, uint64_t seed,
+                         float* logp, float* ce_sum, float* ent, float* logp_a, int64_t* action,
+                         float* ws, void* stream);
+/* dlogit[b][c] (row stride ldd) = d_ce * (p - onehot(target)) + d_logp_a[b] * (onehot(action) - p)
+ *   + d_ent[b] * (-p * (logp + ent[b])) over unmasked c, 0 where masked; each d_* may be NULL. */
+int dasa_policy_head_bwd(const float* logp, const int32_t* cand_len, const int64_t* target,
+                         const int64_t* action, const float* ent, const float* d_ce,
+                         const float* d_logp_a, const float* d_ent, float* dlogit, int64_t ldd,
+                         int32_t B, int32_t C, int32_t ignore_index, void* stream);
+
 /* Device seed source for hipGraph capture. While a counter is set (dev_counter != NULL), every
  * forward dropout launch (layernorm, embeddings, attention probabilities, dropout) records it, and
  * its mask seed becomes seed ^ mix(*dev_counter) read at run time: a captured graph that starts with

@@ -343,3 +343,52 @@ def test_adain_musigma_reverse_dropout(dev):
     mc, sc = ms(c3)
     mss, sss = ms(s3)
     assert (ops.adain_musigma(c3.to(dev), s3.to(dev)).cpu() - ((c3 - mc) / sc * sss + mss)).abs().max() < 1e-4
+
+
+def test_policy_head(dev):
+    """dasa_policy_head_fwd/bwd (agent_dg.py:832-880) against the PyTorch ops the reference runs:
+    masked_fill -> CrossEntropyLoss(sum, ignore_index=-100), argmax + log_softmax gather, Categorical
+    entropy / log_prob, and their gradients; the Categorical draw is checked by frequency."""
+    from dasa_amd import functional as DF
+    g = torch.Generator().manual_seed(21)
+    B, C = 37, 19
+    logit = torch.randn(B, C, generator=g) * 3
+    lens = torch.randint(1, C + 1, (B,), generator=g)
+    lens[0] = C
+    target = torch.stack([torch.randint(0, int(n), (1,), generator=g)[0] for n in lens])
+    target[3] = -100
+    mask = torch.arange(C)[None, :] >= lens[:, None]
+    w_ent, w_lp = torch.randn(B, generator=g), torch.randn(B, generator=g)
+    # reference (CPU fp64)
+    x = logit.double().requires_grad_(True)
+    z = x.masked_fill(mask, -float("inf"))
+    ce = torch.nn.CrossEntropyLoss(ignore_index=-100, reduction="sum")(z, target)
+    a_ref = z.max(1)[1]
+    lp_ref = torch.log_softmax(z, 1).gather(1, a_ref[:, None])[:, 0]
+    cat = torch.distributions.Categorical(torch.softmax(z, 1), validate_args=False)
+    ent_ref = cat.entropy()
+    (ce * 0.7 + (ent_ref * w_ent.double()).sum() + (lp_ref * w_lp.double()).sum()).backward()
+    # product
+    xd = logit.to(dev).requires_grad_(True)
+    lens32 = lens.to(torch.int32).to(dev)
+    ce_d, ent_d, lp_d, a_d = DF.policy_head(xd, lens32, target.to(dev), "argmax")
+    (ce_d * 0.7 + (ent_d * w_ent.to(dev)).sum() + (lp_d * w_lp.to(dev)).sum()).backward()
+    assert torch.equal(a_d.cpu(), a_ref)
+    assert abs(ce_d.item() - ce.item()) < 1e-4 * max(1.0, abs(ce.item()))
+    assert (ent_d.cpu().double() - ent_ref).abs().max() < 1e-5
+    assert (lp_d.cpu().double() - lp_ref).abs().max() < 1e-5
+    assert (xd.grad.cpu().double() - x.grad).abs().max() < 1e-5
+    # teacher mode: CE only
+    ce_t = DF.policy_head(logit.to(dev), lens32, target.to(dev), "teacher")[0]
+    assert abs(ce_t.item() - ce.item()) < 1e-4 * max(1.0, abs(ce.item()))
+    # sampling: frequencies of 8192 draws of one row vs its softmax
+    N = 8192
+    row = torch.randn(1, C, generator=g).repeat(N, 1)
+    ln = torch.full((N,), 11, dtype=torch.int32)
+    _, _, lps, acts = DF.policy_head(row.to(dev), ln.to(dev), None, "sample")
+    acts = acts.cpu()
+    assert int(acts.max()) < 11 and int(acts.min()) >= 0
+    p = torch.softmax(row[0, :11].double(), 0)
+    freq = torch.bincount(acts, minlength=11).double() / N
+    assert (freq - p).abs().max() < 0.03
+    assert (lps.cpu().double() - torch.log(p)[acts]).abs().max() < 1e-5
