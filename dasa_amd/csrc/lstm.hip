@@ -443,8 +443,25 @@ extern "C" int dasa_bilstm_fwd(const float* xproj, const float* whh_fwd, const f
   return 0;
 }
 
+// Large-batch BPTT: the per-timestep recurrent product of both directions as ONE batched NT GEMM
+// (rec[dir] = dgates_prev[dir] . W_hh[dir], with W_hh^T staged K-contiguous once per call), so it
+// takes the 64-deep K / stream-K kernels (gemm.hip) with its own zero-counter workspace.
+static dasa_gemm_desc bptt_rec_desc(int B, int L, int H) {
+  dasa_gemm_desc d{};
+  d.M = B; d.N = H; d.K = 4 * H; d.batch = 2; d.opA = 0; d.opB = 1;
+  d.lda = (long)L * 2 * 4 * H; d.ldb = 4 * H; d.ldc = H;
+  d.strideB = 4L * H * H; d.strideC = (long)B * H;
+  d.alpha = 1.f; d.beta = 0.f;
+  return d;
+}
+static long bptt_gemm_ws_floats(int B, int L, int H) {
+  dasa_gemm_desc d = bptt_rec_desc(B, L, H);
+  return (dasa_gemm_f32_workspace(&d) + 15) / 4 + 4;
+}
+
 extern "C" int64_t dasa_bilstm_bwd_workspace(int32_t B, int32_t H) {
-  if (B > 32) return (int64_t)(6L * B * H * sizeof(float));   // carries + rec (GEMM path)
+  if (B > 32)   // carries + rec, W_hh^T of both directions, GEMM workspace (L does not change its size)
+    return (int64_t)((6L * B * H + 8L * H * H + 8 + bptt_gemm_ws_floats(B, 1, H)) * sizeof(float));
   return (int64_t)((4L * B * H + 8L * H * H) * sizeof(float));
 }
 
@@ -469,21 +486,29 @@ extern "C" int dasa_bilstm_bwd(const float* whh_fwd, const float* whh_bwd, const
     if (dc_n) hipLaunchKernelGGL(copy_kernel, dim3(cdivi(S, 256)), dim3(256), 0, st, dc_n, dc, S);
     else hipLaunchKernelGGL(fill_kernel, dim3(cdivi(S, 256)), dim3(256), 0, st, dc, S, 0.f);
     DASA_CHECK_LAUNCH();
+    float* wt = rec + S;
+    wt += (16 - ((uintptr_t)wt & 15) / 4) % 4;            // 16-B aligned W_hh^T [2][H][4H]
+    float* gws = wt + 8L * H * H;
+    gws += (16 - ((uintptr_t)gws & 15) / 4) % 4;
+    const long gws_floats = bptt_gemm_ws_floats(B, L, H) - 4;
+    hipLaunchKernelGGL(fill_kernel, dim3(64), dim3(256), 0, st, gws, 16384L, 0.f);   // GEMM arrival counters
+    DASA_CHECK_LAUNCH();
+    hipLaunchKernelGGL(transpose_kernel, dim3(H / 32, 4 * H / 32), dim3(256), 0, st, whh_fwd, wt, 4 * H, H);
+    DASA_CHECK_LAUNCH();
+    hipLaunchKernelGGL(transpose_kernel, dim3(H / 32, 4 * H / 32), dim3(256), 0, st, whh_bwd, wt + 4L * H * H,
+                       4 * H, H);
+    DASA_CHECK_LAUNCH();
     BpttArgs a{nullptr, nullptr, lengths, save_act, save_c, dout, dgates, dh, dc, B, L, H};
     for (int s = 0; s < L; ++s) {
-      if (s > 0) {
-        for (int dir = 0; dir < 2; ++dir) {
-          const int t = dir == 0 ? (L - 1 - s) : s;
-          const int tp = dir == 0 ? t + 1 : t - 1;
-          dasa_gemm_desc d{};
-          d.M = B; d.N = H; d.K = 4 * H; d.batch = 1; d.opA = 0; d.opB = 0;
-          d.A = dgates + ((long)tp * 2 + dir) * 4 * H; d.lda = (long)L * 2 * 4 * H;
-          d.B = dir ? whh_bwd : whh_fwd; d.ldb = H;
-          d.C = rec + (long)dir * B * H; d.ldc = H;
-          d.alpha = 1.f; d.beta = 0.f;
-          const int rc = dasa_gemm_f32(&d, nullptr, 0, stream);
-          if (rc) return rc;
-        }
+      if (s > 0) {   // both directions in one launch: dir 0 reads step t+1 = L-s, dir 1 step t-1 = s-1
+        dasa_gemm_desc d = bptt_rec_desc(B, L, H);
+        const long a0 = ((long)(L - s) * 2 + 0) * 4 * H, a1 = ((long)(s - 1) * 2 + 1) * 4 * H;
+        d.A = dgates + a0;
+        d.strideA = a1 - a0;
+        d.B = wt;
+        d.C = rec;
+        const int rc = dasa_gemm_f32(&d, gws, gws_floats * (int64_t)sizeof(float), stream);
+        if (rc) return rc;
       }
       hipLaunchKernelGGL(bilstm_bptt_cell_kernel, dim3(cdivi(S, 256)), dim3(256), 0, st, a, (const float*)rec, s);
       DASA_CHECK_LAUNCH();

@@ -246,7 +246,7 @@ def test_lstm_cell(dev):
 
 
 @pytest.mark.parametrize("mode", [1, 2])
-@pytest.mark.parametrize("B,L", [(20, 80), (3, 11), (40, 9)])
+@pytest.mark.parametrize("B,L", [(20, 80), (3, 11), (40, 9), (160, 12)])
 def test_bilstm(dev, B, L, mode):
     """mode 1: one launch per timestep; mode 2: the persistent cooperative recurrence (B <= 32)."""
     from dasa_amd import _lib, ops
