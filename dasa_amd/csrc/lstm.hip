@@ -400,7 +400,7 @@ extern "C" int dasa_bilstm_fwd(const float* xproj, const float* whh_fwd, const f
   hipLaunchKernelGGL(fill_kernel, dim3(cdivi(3 * S, 256)), dim3(256), 0, st, ws, 3 * S, 0.f);
   DASA_CHECK_LAUNCH();
   const int mode = lstm_mode();
-  if (mode != 1 && bilstm_persist_ok(B, H)) {
+  if (mode != 1 && bilstm_persist_fwd_ok(B, H)) {
     // ws: [0, 2S) = the [parity][dir][B][H] state hand-off, ws + 2S = zeroed barrier words
     const int rc = bilstm_persist_fwd(xproj, whh_fwd, whh_bwd, lengths, out, h_n, c_n, save_act, save_c, B, L, H,
                                       ws, reinterpret_cast<unsigned*>(ws + 2 * S), st);

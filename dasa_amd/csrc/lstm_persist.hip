@@ -76,10 +76,14 @@ struct PFwd {
   int B, L, H;
 };
 
-// NG = H / 128: K-groups of 8 per wave (the wave's K slice is H / 16).
-template <int NG>
+// NG = H / 128: K-groups of 8 per wave (the wave's K slice is H / 16). NBT = 32-row batch tiles
+// (B <= 32 * NBT): every timestep runs the MFMA pass, the 16-wave reduction and the cell update once
+// per tile, then ONE direction barrier. Thread i < 256 owns (row i / 8 of every tile, unit i % 8); the
+// c / h state of tiles past the first lives in LDS (registers are capped at 128 per lane here).
+template <int NG, int NBT>
 __global__ __launch_bounds__(1024) void bilstm_persist_fwd_kernel(PFwd a) {
   __shared__ __attribute__((aligned(16))) float smem[PW * 1024 + 4];
+  __shared__ float cst[NBT > 1 ? NBT * 256 : 1], hst[NBT > 1 ? NBT * 256 : 1];
   const int H = a.H, B = a.B, L = a.L, G = H / PU;
   const int dir = blockIdx.x / G, u0 = (blockIdx.x % G) * PU;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -92,67 +96,94 @@ __global__ __launch_bounds__(1024) void bilstm_persist_fwd_kernel(PFwd a) {
 #pragma unroll
   for (int g = 0; g < NG; ++g) wf[g] = *reinterpret_cast<const float4*>(wp + 8 * g);
 
-  const bool owner = threadIdx.x < B * PU;
-  const int ob = threadIdx.x / PU, ou = threadIdx.x % PU, uj = u0 + ou;
-  const int lenb = owner ? a.len[ob] : 0;
-  float c = 0.f, hp = 0.f;
-  const int b = lane & 31, bc = min(b, B - 1);
-  const bool bval = b < B;
+  const bool own = threadIdx.x < 32 * PU;
+  const int oi = threadIdx.x / PU, ou = threadIdx.x % PU, uj = u0 + ou;   // row in tile, unit
+  float c1 = 0.f, h1 = 0.f;   // NBT == 1: the state stays in registers
+  if (NBT > 1 && own) {
+#pragma unroll
+    for (int bt = 0; bt < NBT; ++bt) {
+      cst[bt * 256 + threadIdx.x] = 0.f;
+      hst[bt * 256 + threadIdx.x] = 0.f;
+    }
+  }
+  const int b = lane & 31;
   for (int s = 0; s < L; ++s) {
     const int t = dir == 0 ? s : L - 1 - s;
-    floatx16 acc;
+    const float* hin = a.hbuf + (long)((s & 1) * 2 + dir) * B * H;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)hin, (short)0, B * H * 4, 0x00020000);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    if (s > 0) {   // h_0 = 0: the first step has no recurrent term
-      const float* hin = a.hbuf + (long)((s & 1) * 2 + dir) * B * H;
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)hin, (short)0, B * H * 4, 0x00020000);
-      float4 hf[NG];
+    for (int bt = 0; bt < NBT; ++bt) {
+      if (bt * 32 >= B) break;   // uniform
+      floatx16 acc;
 #pragma unroll
-      for (int g = 0; g < NG; ++g) hf[g] = selz(bval, ld_sc1(rs, (bc * H + k0 + 8 * g + 4 * hh) * 4));
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+      if (s > 0) {   // h_0 = 0: the first step has no recurrent term
+        const int row = bt * 32 + b, bc = min(row, B - 1);
+        const bool bval = row < B;
+        float4 hf[NG];
 #pragma unroll
-      for (int g = 0; g < NG; ++g)
+        for (int g = 0; g < NG; ++g) hf[g] = selz(bval, ld_sc1(rs, (bc * H + k0 + 8 * g + 4 * hh) * 4));
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(f4e(hf[g], e), f4e(wf[g], e), acc, 0, 0, 0);
-    }
-    // C[b][n] partial over this wave's K slice: lane -> col n, reg r -> row (r&3) + 8(r>>2) + 4hh
+        for (int g = 0; g < NG; ++g)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) smem[w * 1024 + r * 64 + lane] = acc[r];
-    __syncthreads();
-    {   // sum the 16 wave partials: thread i owns element i of the 32x32 tile
-      float sum = 0.f;
-#pragma unroll
-      for (int ww = 0; ww < PW; ++ww) sum += smem[ww * 1024 + threadIdx.x];
-      smem[threadIdx.x] = sum;   // only this thread reads or writes index threadIdx.x of slot 0
-    }
-    __syncthreads();
-    if (owner) {
-      const int rr = (ob & 3) + 4 * (ob >> 3), lh = ((ob >> 2) & 1) * 32;
-      const float* xp = a.xproj + (((long)ob * L + t) * 2 + dir) * 4 * H;
-      float gq[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) gq[q] = xp[q * H + uj] + smem[rr * 64 + lh + q * PU + ou];
-      float* outp = a.out + ((long)ob * L + t) * 2 * H + dir * H + uj;
-      float* sa = a.save_act ? a.save_act + (((long)t * 2 + dir) * B + ob) * 4 * H : nullptr;
-      if (t < lenb) {
-        const float i = sigmoidf_(gq[0]), f = sigmoidf_(gq[1]), gg = tanhf(gq[2]), o = sigmoidf_(gq[3]);
-        c = f * c + i * gg;
-        hp = o * tanhf(c);
-        *outp = hp;
-        if (sa) { sa[uj] = i; sa[H + uj] = f; sa[2 * H + uj] = gg; sa[3 * H + uj] = o; }
-      } else {   // packed sequence: state frozen (fwd) / still zero (bwd), output zero
-        *outp = 0.f;
-        if (sa) { sa[uj] = 0.f; sa[H + uj] = 0.f; sa[2 * H + uj] = 0.f; sa[3 * H + uj] = 0.f; }
+          for (int e = 0; e < 4; ++e)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(f4e(hf[g], e), f4e(wf[g], e), acc, 0, 0, 0);
       }
-      if (a.save_c) a.save_c[(((long)t * 2 + dir) * B + ob) * H + uj] = c;
-      if (s + 1 < L) st_sc1(a.hbuf + (long)(((s + 1) & 1) * 2 + dir) * B * H + (long)ob * H + uj, hp);
+      // C[b][n] partial over this wave's K slice: lane -> col n, reg r -> row (r&3) + 8(r>>2) + 4hh
+#pragma unroll
+      for (int r = 0; r < 16; ++r) smem[w * 1024 + r * 64 + lane] = acc[r];
+      __syncthreads();
+      {   // sum the 16 wave partials: thread i owns element i of the 32x32 tile
+        float sum = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < PW; ++ww) sum += smem[ww * 1024 + threadIdx.x];
+        smem[threadIdx.x] = sum;   // only this thread reads or writes index threadIdx.x of slot 0
+      }
+      __syncthreads();
+      const int ob = bt * 32 + oi;
+      if (own && ob < B) {
+        const int rr = (oi & 3) + 4 * (oi >> 3), lh = ((oi >> 2) & 1) * 32;
+        const float* xp = a.xproj + (((long)ob * L + t) * 2 + dir) * 4 * H;
+        float gq[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) gq[q] = xp[q * H + uj] + smem[rr * 64 + lh + q * PU + ou];
+        float* outp = a.out + ((long)ob * L + t) * 2 * H + dir * H + uj;
+        float* sa = a.save_act ? a.save_act + (((long)t * 2 + dir) * B + ob) * 4 * H : nullptr;
+        float c = NBT > 1 ? cst[bt * 256 + threadIdx.x] : c1;
+        float hp = NBT > 1 ? hst[bt * 256 + threadIdx.x] : h1;
+        if (t < a.len[ob]) {
+          const float i = sigmoidf_(gq[0]), f = sigmoidf_(gq[1]), gg = tanhf(gq[2]), o = sigmoidf_(gq[3]);
+          c = f * c + i * gg;
+          hp = o * tanhf(c);
+          *outp = hp;
+          if (sa) { sa[uj] = i; sa[H + uj] = f; sa[2 * H + uj] = gg; sa[3 * H + uj] = o; }
+        } else {   // packed sequence: state frozen (fwd) / still zero (bwd), output zero
+          *outp = 0.f;
+          if (sa) { sa[uj] = 0.f; sa[H + uj] = 0.f; sa[2 * H + uj] = 0.f; sa[3 * H + uj] = 0.f; }
+        }
+        if (a.save_c) a.save_c[(((long)t * 2 + dir) * B + ob) * H + uj] = c;
+        if (s + 1 < L) st_sc1(a.hbuf + (long)(((s + 1) & 1) * 2 + dir) * B * H + (long)ob * H + uj, hp);
+        if (NBT > 1) {
+          cst[bt * 256 + threadIdx.x] = c;
+          hst[bt * 256 + threadIdx.x] = hp;
+        } else {
+          c1 = c;
+          h1 = hp;
+        }
+      }
+      // the owners read slot 0 before the next tile's partials overwrite it
+      if (bt + 1 < NBT && (bt + 1) * 32 < B) __syncthreads();
     }
     if (s + 1 < L && !dir_barrier(&a.sync[dir], (unsigned)(s + 1) * G, &a.sync[2], &smem[PW * 1024])) break;
   }
-  if (owner) {
-    const long si = ((long)dir * B + ob) * H + uj;
-    if (a.h_n) a.h_n[si] = hp;
-    if (a.c_n) a.c_n[si] = c;
+#pragma unroll
+  for (int bt = 0; bt < NBT; ++bt) {
+    const int ob = bt * 32 + oi;
+    if (own && ob < B) {
+      const long si = ((long)dir * B + ob) * H + uj;
+      if (a.h_n) a.h_n[si] = NBT > 1 ? hst[bt * 256 + threadIdx.x] : h1;
+      if (a.c_n) a.c_n[si] = NBT > 1 ? cst[bt * 256 + threadIdx.x] : c1;
+    }
   }
 }
 
@@ -309,16 +340,32 @@ bool bilstm_persist_ok(int B, int H) {
   return B >= 1 && B <= 32 && H % 256 == 0 && H >= 256 && H <= 1024;
 }
 
+// Forward: up to 6 batch tiles of 32 rows at the DicEncoder's H = 1024 (the teacher rollout encodes 4-8
+// steps x B = 20 sequences per launch; more tiles would spill); other H keep one tile.
+bool bilstm_persist_fwd_ok(int B, int H) {
+  return bilstm_persist_ok(B, H) || (H == 1024 && B >= 1 && B <= 192);
+}
+
 int bilstm_persist_fwd(const float* xproj, const float* whh_fwd, const float* whh_bwd, const int32_t* lengths,
                        float* out, float* h_n, float* c_n, float* save_act, float* save_c, int B, int L, int H,
                        float* hbuf, unsigned* sync, hipStream_t st) {
   PFwd a{xproj, whh_fwd, whh_bwd, lengths, out, save_act, save_c, h_n, c_n, hbuf, sync, B, L, H};
   const int grid = 2 * H / PU;
+  if (B > 32) {
+    if (H != 1024 || B > 192) return (int)hipErrorInvalidValue;
+    switch ((B + 31) / 32) {
+      case 2: return launch_persistent(bilstm_persist_fwd_kernel<8, 2>, grid, a, st);
+      case 3: return launch_persistent(bilstm_persist_fwd_kernel<8, 3>, grid, a, st);
+      case 4: return launch_persistent(bilstm_persist_fwd_kernel<8, 4>, grid, a, st);
+      case 5: return launch_persistent(bilstm_persist_fwd_kernel<8, 5>, grid, a, st);
+      default: return launch_persistent(bilstm_persist_fwd_kernel<8, 6>, grid, a, st);
+    }
+  }
   switch (H / 128) {
-    case 2: return launch_persistent(bilstm_persist_fwd_kernel<2>, grid, a, st);
-    case 4: return launch_persistent(bilstm_persist_fwd_kernel<4>, grid, a, st);
-    case 6: return launch_persistent(bilstm_persist_fwd_kernel<6>, grid, a, st);
-    case 8: return launch_persistent(bilstm_persist_fwd_kernel<8>, grid, a, st);
+    case 2: return launch_persistent(bilstm_persist_fwd_kernel<2, 1>, grid, a, st);
+    case 4: return launch_persistent(bilstm_persist_fwd_kernel<4, 1>, grid, a, st);
+    case 6: return launch_persistent(bilstm_persist_fwd_kernel<6, 1>, grid, a, st);
+    case 8: return launch_persistent(bilstm_persist_fwd_kernel<8, 1>, grid, a, st);
     default: return (int)hipErrorInvalidValue;
   }
 }

@@ -6,13 +6,17 @@ import sys
 from collections import defaultdict
 
 FAMILY_PREFIX = [
-    ("gemm", ("gemm_f32_kernel",)),           # the GEMM launch (its split-K reduce listed separately)
+    ("gemm", ("gemm_f32_kernel", "gemm_nt_k64_kernel", "gemm_nt_glds_kernel")),   # (split-K reduce apart)
     ("gemm_splitk_reduce", ("splitk_reduce_kernel",)),
     ("bilstm", ("bilstm_persist_fwd_kernel", "bilstm_step_fused_kernel", "bilstm_step_cell_kernel")),
     ("bilstm_bptt", ("bilstm_persist_bwd_kernel", "bilstm_bptt_step_kernel", "bilstm_bptt_cell_kernel")),
     ("mha", ("mha_fwd_kernel", "mha_bwd_kernel")),
     ("layernorm", ("ln_fwd_kernel", "ln_bwd_kernel")),
-    ("softdot/shift", ("scores_kernel", "apply_fwd_kernel", "apply_bwd_kernel")),
+    ("softdot/shift/cand", ("scores_kernel", "apply_fwd_kernel", "apply_bwd_kernel", "attn_fwd_kernel",
+                            "attn_bwd_apply_kernel", "attn_bwd_scores_kernel")),
+    ("ada_gate", ("AdaFwdOp", "AdaBwdOp")),
+    ("adain_musigma", ("adain_musigma",)),
+    ("policy_head", ("policy_head_fwd_kernel", "policy_head_bwd_kernel")),
 ]
 
 

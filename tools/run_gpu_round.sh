@@ -33,5 +33,7 @@ if [ "${PROF:-1}" = "1" ]; then
   # keep only the summaries (the full kernel trace is far larger than gpurun's copy-back limit)
   find gpurun_out/prof_$TAG \( -name "*kernel_trace*" -o -name "*.db" \) -delete 2>/dev/null
   find gpurun_out/prof_$TAG -type f
-  python tools/prof_compare.py gpurun_out/prof_$TAG/run_kernel_stats.csv gpurun_out/profrun_$TAG.log | head -20
+  python tools/prof_compare.py gpurun_out/prof_$TAG/run_kernel_stats.csv gpurun_out/profrun_$TAG.log \
+    > gpurun_out/prof_compare_$TAG.txt
+  head -20 gpurun_out/prof_compare_$TAG.txt
 fi
