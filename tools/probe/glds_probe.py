@@ -44,10 +44,14 @@ def bench(fn, it=20):
     return e0.elapsed_time(e1) / it
 
 def timing():
-    for M, N, K in ((12800, 3072, 768), (12800, 768, 3072), (12800, 2304, 768), (12800, 768, 768),
-                    (1600, 768, 768), (1600, 3072, 768), (1600, 768, 3072), (1600, 2304, 768), (1600, 4096, 768),
-                    (720, 768, 768), (720, 3072, 768), (720, 768, 3072), (720, 2304, 768), (1040, 2048, 2048),
-                    (5760, 768, 768), (4096, 4096, 4096)):
+    shapes = ((12800, 3072, 768), (12800, 768, 3072), (12800, 2304, 768), (12800, 768, 768),
+              (1600, 768, 768), (1600, 3072, 768), (1600, 768, 3072), (1600, 2304, 768), (1600, 4096, 768),
+              (720, 768, 768), (720, 3072, 768), (720, 768, 3072), (720, 2304, 768), (1040, 2048, 2048),
+              (5760, 768, 768), (4096, 4096, 4096))
+    if os.environ.get("PROBE_SKINNY"):
+        shapes = ((20, 4096, 2240), (20, 2176, 1024), (20, 1024, 3072), (20, 1024, 2048), (20, 2048, 1024),
+                  (20, 1024, 2176), (20, 5, 1024), (20, 1024, 1024), (1400, 1024, 1024), (700, 1024, 1024))
+    for M, N, K in shapes:
         A = torch.rand(M, K, device=dev) * 2 - 1; W = torch.rand(N, K, device=dev) * 2 - 1
         fl = 2.0 * M * N * K
         f = lambda: ops.linear(A, W)
@@ -65,5 +69,5 @@ def timing():
         print(f"M{M} N{N} K{K}: auto {auto:.1f} torch {tor:.1f} glds " +
               " ".join(f"c{c}s{s}:{t:.0f}" for t, c, s in res[:6]), flush=True)
 
-if check() == 0:
+if os.environ.get("PROBE_SKINNY") or check() == 0:
     timing()
