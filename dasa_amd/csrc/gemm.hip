@@ -26,6 +26,7 @@ struct GemmP {
   const float* colscale;
   float alpha, beta;
   float* ws;
+  int group_m;   // > 1: L2-grouped tile order (64-deep K kernels, non-stream-K)
 };
 
 __device__ __forceinline__ float apply_act(float v, int act) {
@@ -546,9 +547,9 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
 }
 
-template <int BM, int BN, int WAVES_M, int WAVES_N, int MF, int NSTAGE, bool SK>
+template <int BM, int BN, int WAVES_M, int WAVES_N, int MF, int NSTAGE, bool SK, int BK = 64>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_nt_k64_kernel(GemmP p, SkP sk) {
-  constexpr int BK = 64;
+  static_assert(BK == 64 || (BK == 32 && MF == 16), "BK 32 tiles use the 16x16x4 fragment map");
   constexpr int NT = 64 * WAVES_M * WAVES_N;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   constexpr int TM = WM / MF, TN = WN / MF;
@@ -579,12 +580,12 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_nt_k64_kernel(Gem
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int row = wm + i * MF + fr;
-        af[i] = *reinterpret_cast<const float4*>(As + row * BK + 4 * (q ^ (row & 15)));
+        af[i] = *reinterpret_cast<const float4*>(As + row * BK + 4 * (q ^ qswz<BK>(row)));
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int row = wn + j * MF + fr;
-        bf[j] = *reinterpret_cast<const float4*>(Bs + row * BK + 4 * (q ^ (row & 15)));
+        bf[j] = *reinterpret_cast<const float4*>(Bs + row * BK + 4 * (q ^ qswz<BK>(row)));
       }
 #pragma unroll
       for (int e = 0; e < 4; ++e)
@@ -641,7 +642,18 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_nt_k64_kernel(Gem
 
   if constexpr (!SK) {
     const int wgid = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
-    const int n0 = (wgid % gridDim.x) * BN, m0 = (wgid / gridDim.x) * BM;
+    int n0, m0;
+    if (p.group_m > 1) {
+      // L2-grouped order: consecutive tiles of one XCD walk group_m row panels column by column, so
+      // the workgroups resident on an XCD share a few A row panels and B column panels in its L2
+      const int gm = p.group_m, per = gm * gridDim.x, grp = wgid / per;
+      const int rows = min(gm, (int)gridDim.y - grp * gm), r = wgid - grp * per;
+      m0 = (grp * gm + r % rows) * BM;
+      n0 = (r / rows) * BN;
+    } else {
+      n0 = (wgid % gridDim.x) * BN;
+      m0 = (wgid / gridDim.x) * BM;
+    }
     const int b = blockIdx.z / p.splitk, split = blockIdx.z % p.splitk;
     const int kbeg = split * p.kchunk;
     const int kend = min(p.K, kbeg + p.kchunk);
@@ -734,14 +746,14 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_nt_k64_kernel(Gem
   }
 }
 
-template <int BM, int BN, int WAVES_M, int WAVES_N, int MF, int NSTAGE>
+template <int BM, int BN, int WAVES_M, int WAVES_N, int MF, int NSTAGE, int BK = 64>
 int launch_k64(const GemmP& p, const SkP* sk, hipStream_t st) {
   if (sk) {
-    hipLaunchKernelGGL((gemm_nt_k64_kernel<BM, BN, WAVES_M, WAVES_N, MF, NSTAGE, true>), dim3(sk->grid),
+    hipLaunchKernelGGL((gemm_nt_k64_kernel<BM, BN, WAVES_M, WAVES_N, MF, NSTAGE, true, BK>), dim3(sk->grid),
                        dim3(64 * WAVES_M * WAVES_N), 0, st, p, *sk);
   } else {
     dim3 grid((p.N + BN - 1) / BN, (p.M + BM - 1) / BM, p.batch * p.splitk);
-    hipLaunchKernelGGL((gemm_nt_k64_kernel<BM, BN, WAVES_M, WAVES_N, MF, NSTAGE, false>), grid,
+    hipLaunchKernelGGL((gemm_nt_k64_kernel<BM, BN, WAVES_M, WAVES_N, MF, NSTAGE, false, BK>), grid,
                        dim3(64 * WAVES_M * WAVES_N), 0, st, p, SkP{});
   }
   DASA_CHECK_LAUNCH();
@@ -811,6 +823,10 @@ constexpr TileCfg kCfgs[] = {
     {64, 128, 32, 64, 16 | 1 << 8, true, true},    // 33
     {64, 64, 32, 32, 16 | 1 << 8, true, true},     // 34
     {128, 128, 32, 64, 16 | 1 << 8, true, true},   // 35: 8 waves
+    // 32-deep K, double-buffered LDS (one barrier per K tile), 8 waves
+    {128, 128, 32, 64, 16 | 2 << 8, true},   // 36: 64 KB LDS -> two workgroups per CU
+    {256, 128, 64, 64, 16 | 2 << 8, true},   // 37: 96 KB LDS
+    {128, 128, 64, 32, 16 | 2 << 8, true},   // 38: 4x2 waves of 32x64 -> 2x4 of 64x32
 };
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
@@ -823,7 +839,7 @@ int glds_fallback(int cfg) {
     case 18: return 2;
     case 19: return 0;
     case 20: return 1;
-    case 21: case 22: case 23: case 27: case 28: return 0;
+    case 21: case 22: case 23: case 27: case 28: case 36: case 37: case 38: return 0;
     case 24: case 30: return 6;
     case 25: case 33: return 1;
     case 31: case 35: return 0;
@@ -856,6 +872,9 @@ int launch_cfg(int cfg, bool vec, bool glds_ok, const GemmP& p, const SkP* sk, i
       case 32: return launch_k64<128, 64, 2, 2, 16, 1>(p, sk, st);
       case 33: return launch_k64<64, 128, 2, 2, 16, 1>(p, sk, st);
       case 34: return launch_k64<64, 64, 2, 2, 16, 1>(p, sk, st);
+      case 36: return launch_k64<128, 128, 4, 2, 16, 2, 32>(p, nullptr, st);
+      case 37: return launch_k64<256, 128, 4, 2, 16, 2, 32>(p, nullptr, st);
+      case 38: return launch_k64<128, 128, 2, 4, 16, 2, 32>(p, nullptr, st);
       default: return launch_k64<128, 128, 4, 2, 16, 1>(p, sk, st);
     }
   }
@@ -886,7 +905,7 @@ inline long cdiv(long a, long b) { return (a + b - 1) / b; }
 
 }  // namespace
 
-struct Plan { int cfg, splitk, kchunk; int64_t ws; int sk_grid, sk_dp, sk_tiles, sk_ipt; };
+struct Plan { int cfg, splitk, kchunk; int64_t ws; int sk_grid, sk_dp, sk_tiles, sk_ipt; int group_m; };
 
 // Leading words of every GEMM workspace: stream-K arrival counters (zero on allocation, re-armed
 // to zero by each call). Split-K partials and stream-K slabs follow.
@@ -918,6 +937,7 @@ static int sk_twin(int cfg) {
 }
 
 static int g_force_cfg = -2;   // DASA_GEMM_CFG=<index> pins a tile config (tuning sweeps)
+static int g_force_group = -2; // DASA_GEMM_GROUP=<n> pins the L2 group height (tuning sweeps)
 
 static Plan make_plan(const dasa_gemm_desc* d) {
   const int M = d->M, N = d->N, K = d->K, batch = d->batch < 1 ? 1 : d->batch;
@@ -946,7 +966,9 @@ static Plan make_plan(const dasa_gemm_desc* d) {
   else if (t64 >= 400) pl.cfg = (t64 >= 500 && K < 1536) ? 5 : 4;
   else if (t64 >= 250 && (K < 1536 || t64 >= 320)) pl.cfg = 5;
   else pl.cfg = 4;
-  const int fcfg = g_force_cfg >= 0 ? g_force_cfg % 64 : -1, fsplit = g_force_cfg >= 0 ? g_force_cfg / 64 : 0;
+  // forced value = cfg + 64 * split + 4096 * group (tuning sweeps)
+  const int fcfg = g_force_cfg >= 0 ? g_force_cfg % 64 : -1, fsplit = g_force_cfg >= 0 ? (g_force_cfg / 64) % 64 : 0;
+  const int fgroup = g_force_cfg >= 0 ? g_force_cfg / 4096 : 0;
   if (fcfg >= 0 && fcfg < kNumCfgs) pl.cfg = fcfg;
   const int bm = kCfgs[pl.cfg].bm, bn = kCfgs[pl.cfg].bn;
   const long blocks = tiles(bm, bn);
@@ -971,6 +993,9 @@ static Plan make_plan(const dasa_gemm_desc* d) {
   pl.kchunk = kchunk;
   pl.ws = splitk > 1 ? (int64_t)splitk * batch * M * N * (int64_t)sizeof(float) : 0;
   pl.sk_grid = pl.sk_dp = pl.sk_tiles = pl.sk_ipt = 0;
+  // 64-deep K tiles over many row panels walk 4-panel groups (profiles/r01e/gemm_k32_group.txt: +1-5%
+  // on the 12800-row language GEMMs, never slower)
+  pl.group_m = fgroup > 0 ? fgroup : ((pl.cfg == 25 || pl.cfg == 27) && cdiv(M, bm) >= 8 ? 4 : 1);
   if (kCfgs[pl.cfg].sk) {
     const int ipt = K / 64;
     const long nt = blocks;
@@ -996,6 +1021,7 @@ static Plan make_plan(const dasa_gemm_desc* d) {
 
 extern "C" int dasa_gemm_force_config(int cfg) {
   g_force_cfg = cfg;
+  if (cfg < 0) g_force_group = -1;
   return kNumCfgs;
 }
 
@@ -1036,6 +1062,11 @@ extern "C" int dasa_gemm_f32(const dasa_gemm_desc* d, void* ws, int64_t ws_bytes
   p.aux = d->aux; p.ld_aux = d->ld_aux; p.sAux = d->strideAux;
   p.colscale = d->colscale; p.alpha = d->alpha; p.beta = d->beta;
   p.ws = ws ? (float*)((char*)ws + kCntBytes) : nullptr;
+  if (g_force_group == -2) {
+    const char* e = getenv("DASA_GEMM_GROUP");
+    g_force_group = e ? atoi(e) : -1;
+  }
+  p.group_m = g_force_group > 0 ? g_force_group : pl.group_m;
   SkP sk{};
   if (pl.sk_grid > 0) {
     sk.grid = pl.sk_grid;

@@ -1,7 +1,8 @@
 """Generate tests/golden/*.npz by running the REFERENCE r2r_src code (imported here behind offline
 shims, CPU fp32) on seeded weights/inputs. Container-only test infrastructure: needs /root/reference.
 
-    python oracle/golden/make_golden.py
+    python oracle/golden/make_golden.py            # every fixture
+    python oracle/golden/make_golden.py finetune   # tests/golden/cfg4_finetune.npz only
 
 Fixtures hold outputs only (plus gradient norms and seeded random "sketches" <grad, r_name> for
 large tensors); tests regenerate weights (dasa_amd.synth.init_params) and inputs
@@ -232,15 +233,76 @@ def rollouts(R):
     return out
 
 
+def finetune(R):
+    """cfg4: the finetune path (--d_update_add_layer True, agent_dg.py:152; vilmodel.py:1408-1410 no
+    longer detaches), so the LXRT layers and the VisionEncoder receive gradients. Records the LXRT
+    layer backward on its own and one accumulate_gradient('sample') + backward with dropout 0."""
+    A = R.args
+    out = {}
+    # LXRT layer backward (eval): parameter and input gradients ------------------------------
+    from pytorch_transformers import BertConfig
+    lx = init_params(R.vilmodel.LXRTXLayer(BertConfig.from_pretrained("bert-base-uncased")), 40).eval()
+    lang, lmask, visn, vmask = GI.lxrt_inputs()
+    lang.requires_grad_(True)
+    visn.requires_grad_(True)
+    lo, vo = lx(lang, lmask[:, None, None, :], visn, vmask[:, None, None, :])
+    rng = np.random.default_rng(141)
+    w = [torch.from_numpy(rng.standard_normal(t.shape).astype(np.float32)) for t in (lo, vo)]
+    ((lo * w[0]).sum() + (vo * w[1]).sum()).backward()
+    grad_record(out, "lxrt/", lx.named_parameters())
+    grad_record(out, "lxrt_in/", [("lang", lang), ("visn", visn)])
+    # train iteration on the finetune path ------------------------------------------------------
+    cfg = GI.CFG4
+    A.d_vl_layers = cfg["vl_layers"]
+    A.batchSize = cfg["batch"]
+    A.maxAction = cfg["max_action"]
+    A.views = 36
+    A.d_update_add_layer = True
+    world = SynthWorld(n_viewpoints=16, feat_seed=0, graph_seed=3)
+    env = SynthR2RBatch(world, cfg["batch"], seed=9, mode="goal", instr_len=cfg["instr_len"], variable_len=True)
+    agent = make_agent(R, env, cfg["max_action"])
+    assert agent.encoder.bert.update_add_layer
+    for mod in (agent.encoder, agent.decoder, agent.critic, agent.adaIn):
+        for sub in mod.modules():
+            if isinstance(sub, torch.nn.Dropout):
+                sub.p = 0.0
+    A.ml_weight = A.ml_weight_org
+    orig_sample = torch.distributions.Categorical.sample
+    torch.distributions.Categorical.sample = lambda self, *a, **k: self.probs.argmax(-1)
+    try:
+        agent.zero_grad()
+        agent.accumulate_gradient("sample")
+    finally:
+        torch.distributions.Categorical.sample = orig_sample
+        A.d_update_add_layer = False
+    out["ft/loss"] = np.array(agent.loss.item())
+    out["ft/ml_loss_teacher"] = np.array(agent.logs["ml_loss"][0])
+    out["ft/ml_loss_sample"] = np.array(agent.logs["ml_loss"][1])
+    out["ft/rl_loss"] = np.array(agent.logs["normalized_rl_loss"][-1])
+    agent.loss.backward()
+    for name, mod in (("encoder", agent.encoder), ("decoder", agent.decoder), ("critic", agent.critic),
+                      ("adaIn", agent.adaIn)):
+        grad_record(out, f"ft/{name}.", mod.named_parameters())
+    return out
+
+
 def main():
     R = import_reference()
     os.makedirs(OUT_DIR, exist_ok=True)
+    if sys.argv[1:] == ["finetune"]:
+        ft = finetune(R)
+        np.savez_compressed(os.path.join(OUT_DIR, "cfg4_finetune.npz"), **ft)
+        print("cfg4_finetune.npz:", len(ft), "arrays")
+        return
     ops = per_op(R)
     np.savez_compressed(os.path.join(OUT_DIR, "ops.npz"), **ops)
     print("ops.npz:", len(ops), "arrays")
     ro = rollouts(R)
     np.savez_compressed(os.path.join(OUT_DIR, "cfg1_rollout.npz"), **ro)
     print("cfg1_rollout.npz:", len(ro), "arrays")
+    ft = finetune(R)
+    np.savez_compressed(os.path.join(OUT_DIR, "cfg4_finetune.npz"), **ft)
+    print("cfg4_finetune.npz:", len(ft), "arrays")
 
 
 if __name__ == "__main__":

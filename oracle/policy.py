@@ -200,7 +200,8 @@ def lxrt_layer(P, pre, lang, lang_mask, visn, visn_mask, train=False):
     return l_out, v_out
 
 
-def dic_model(P, input_ids, attention_mask, img_feats, la_layers, vl_layers, train=False, lang_cache=None):
+def dic_model(P, input_ids, attention_mask, img_feats, la_layers, vl_layers, train=False, lang_cache=None,
+              update_lang_bert=False):
     """DicModel.forward (vilmodel.py:1327-1423) with keys prefixed 'bert.'. attention_mask: 1 = token.
 
     lang_cache: optional precomputed language-stack output (it does not depend on img_feats).
@@ -217,6 +218,8 @@ def dic_model(P, input_ids, attention_mask, img_feats, la_layers, vl_layers, tra
             x = bert_layer(P, "bert.lalayer.%d" % i, x, ext, train)
     else:
         x = lang_cache
+    if not update_lang_bert:                  # vilmodel.py:1377-1378 (README default: BERT not trained)
+        x = x.detach()
     text = x
     v = linear(img_feats, P["bert.vision_encoder.visn_fc.weight"], P["bert.vision_encoder.visn_fc.bias"])
     v = _drop(layer_norm(v, P, "bert.vision_encoder.visn_layer_norm"), DROP["bert"], train)
@@ -375,7 +378,8 @@ class Weights:
 
 
 def vl_rollout(W, env, feedback, *, la_layers=9, vl_layers=3, episode_len=35, kernel_size=5, train_ml=None,
-               train_rl=False, train=False, gamma=0.9, obs=None, sample_fn=None, hoist_lang=False, record=None):
+               train_rl=False, train=False, gamma=0.9, obs=None, sample_fn=None, hoist_lang=False, record=None,
+               update_add_layer=False):
     """Seq2SeqAgent.vl_rollout (agent_dg.py:633-1033) for the README config without speaker
     (consistent_drop off, so the decoder's own drop_env applies in train mode).
 
@@ -408,7 +412,8 @@ def vl_rollout(W, env, feedback, *, la_layers=9, vl_layers=3, episode_len=35, ke
             L = seq_mask.shape[1]
             _, _, _, lang_cache = dic_model(W.enc, seq[:, :L], ~seq_mask, f_t, la_layers, 0, train)
         ctx, en_ht, en_ct, _, _ = dic_encoder(W.enc, seq, seq_mask, seq_lengths, f_t.clone(), la_layers, vl_layers,
-                                              train=train, lang_cache=lang_cache if hoist_lang else None)
+                                              train=train, lang_cache=lang_cache if hoist_lang else None,
+                                              update_add_layer=update_add_layer)
         if t == 0:
             h_t, c_t, logit, h1 = decoder_step(W.dec, a_in, df_t, cf, en_ht, en_ct, ctx, seq_mask, kernel_size, train)
         else:

@@ -7,6 +7,9 @@ import torch
 # weight seeds per reference module (agent_dg.py:161-200)
 SEED_ENC, SEED_DEC, SEED_CRITIC, SEED_ADA = 1, 2, 3, 4
 CFG1 = dict(batch=2, vl_layers=1, la_layers=9, max_action=5, instr_len=80, kernel=5)
+# cfg4 (finetune, --d_update_add_layer True): the LXRT stack and VisionEncoder are trained; per-rank B=2.
+# Two cross layers so the backward crosses a layer boundary; fewer steps keep the CPU reference short.
+CFG4 = dict(batch=2, vl_layers=2, la_layers=9, max_action=4, instr_len=80, kernel=5)
 
 
 def _u(rng, *shape):

@@ -172,3 +172,50 @@ def test_rollout_train_grads():
     for name, d in (("encoder", W.enc), ("decoder", W.dec), ("critic", W.critic), ("adaIn", W.ada)):
         n += check_grads(G, f"train/{name}.", [(k, v.grad) for k, v in d.items()], rtol=1e-3)
     assert n == 30
+
+
+def test_lxrt_layer_backward():
+    """LXRTXLayer backward (vilmodel.py:1014-1064): parameter and input gradients (cfg4's extra path)."""
+    G = golden("cfg4_finetune")
+    sch = {k[len("bert.addlayer.0."):]: v for k, v in S.encoder_schema(1, 0).items() if k.startswith("bert.addlayer.0.")}
+    P = {"x." + k: v.requires_grad_(True) for k, v in init_param_dict(sch, 40).items()}
+    lang, lmask, visn, vmask = GI.lxrt_inputs()
+    lang.requires_grad_(True)
+    visn.requires_grad_(True)
+    lo, vo = O.lxrt_layer(P, "x", lang, lmask, visn, vmask)
+    rng = np.random.default_rng(141)
+    w = [torch.from_numpy(rng.standard_normal(t.shape).astype(np.float32)) for t in (lo, vo)]
+    ((lo * w[0]).sum() + (vo * w[1]).sum()).backward()
+    n = check_grads(G, "lxrt/", [(k[2:], v.grad) for k, v in P.items()], rtol=1e-3)
+    assert n == sum(1 for k in G if k.startswith("gnorm/lxrt/"))
+    assert check_grads(G, "lxrt_in/", [("lang", lang.grad), ("visn", visn.grad)], rtol=1e-3) == 2
+
+
+def test_finetune_train_grads():
+    """cfg4 finetune path (--d_update_add_layer True): accumulate_gradient('sample') with dropout 0 and
+    argmax 'sampling'; the LXRT layers and VisionEncoder now receive gradients (vilmodel.py:1408-1410)."""
+    G = golden("cfg4_finetune")
+    cfg = GI.CFG4
+    saved = dict(O.DROP)
+    O.DROP.update(dec=0.0, feat=0.0, enc=0.0, bert=0.0)
+    try:
+        W = oracle_weights(cfg["vl_layers"], requires_grad=True)
+        env = SynthR2RBatch(SynthWorld(16, 0, 3), cfg["batch"], seed=9, mode="goal", instr_len=cfg["instr_len"],
+                            variable_len=True)
+        kw = dict(la_layers=9, vl_layers=cfg["vl_layers"], episode_len=cfg["max_action"], train=True,
+                  update_add_layer=True)
+        r1 = O.vl_rollout(W, env, "teacher", train_ml=0.4, **kw)
+        r2 = O.vl_rollout(W, env, "sample", train_ml=None, train_rl=True, sample_fn=lambda p: p.argmax(-1), **kw)
+    finally:
+        O.DROP.update(saved)
+    loss = r1["loss"] + r2["loss"]
+    assert abs(loss.item() - float(G["ft/loss"])) < 2e-5 * max(1, abs(float(G["ft/loss"])))
+    assert abs(r2["rl_loss"].item() - float(G["ft/rl_loss"])) < 1e-5
+    loss.backward()
+    n = 0
+    for name, d in (("encoder", W.enc), ("decoder", W.dec), ("critic", W.critic), ("adaIn", W.ada)):
+        n += check_grads(G, f"ft/{name}.", [(k, v.grad) for k, v in d.items()], rtol=1e-3)
+    assert n == sum(1 for k in G if k.startswith("gnorm/ft/"))
+    # nothing the reference leaves without a gradient gets one here
+    for k, v in W.enc.items():
+        assert (v.grad is not None) == (f"gnorm/ft/encoder.{k}" in G), k

@@ -114,6 +114,22 @@ def test_lxrt_layer(R, dev):
     close(vo.cpu(), G["lxrt/visn"], TOL, "visn")
 
 
+def test_lxrt_layer_backward(R, dev):
+    """LXRTXLayer backward (the finetune path, cfg4): parameter and input gradients vs the reference."""
+    vilmodel = R[4]
+    G = golden("cfg4_finetune")
+    lx = init_params(vilmodel.LXRTXLayer(vilmodel.BertConfig()), 40).to(dev).eval()
+    lang, lmask, visn, vmask = GI.lxrt_inputs()
+    lang, visn = _req(lang, dev), _req(visn, dev)
+    lo, vo = lx(lang, lmask[:, None, None, :].to(dev), visn, vmask[:, None, None, :].to(dev))
+    rng = np.random.default_rng(141)
+    w = [torch.from_numpy(rng.standard_normal(t.shape).astype(np.float32)).to(dev) for t in (lo, vo)]
+    ((lo * w[0]).sum() + (vo * w[1]).sum()).backward()
+    n = check_grads(G, "lxrt/", [(k, p.grad) for k, p in lx.named_parameters()], rtol=1e-3)
+    assert n == sum(1 for k in G if k.startswith("gnorm/lxrt/"))
+    assert check_grads(G, "lxrt_in/", [("lang", lang.grad), ("visn", visn.grad)], rtol=1e-3) == 2
+
+
 def test_dic_encoder(R, dev):
     param, r2rmodel = R[0], R[3]
     A = param.args
@@ -232,6 +248,48 @@ def test_train_iteration_grads(R, dev, deferred):
     for name, mod in (("encoder", ag.encoder), ("decoder", ag.decoder), ("critic", ag.critic), ("adaIn", ag.adaIn)):
         n += check_grads(G, f"train/{name}.", [(k, p.grad) for k, p in mod.named_parameters()], rtol=2e-3)
     assert n == 30
+
+
+@pytest.mark.parametrize("deferred", [False, True])
+def test_finetune_train_iteration_grads(R, dev, monkeypatch, deferred):
+    """cfg4 finetune path (--d_update_add_layer True): the LXRT stack and VisionEncoder are trained.
+    accumulate_gradient('sample') + backward with dropout 0 and argmax 'sampling' vs the reference."""
+    from dasa_amd import functional as DF
+    param = R[0]
+    G = golden("cfg4_finetune")
+    cfg = GI.CFG4
+    monkeypatch.setattr(param.args, "d_vl_layers", cfg["vl_layers"])
+    monkeypatch.setattr(param.args, "maxAction", cfg["max_action"])
+    monkeypatch.setattr(param.args, "d_update_add_layer", True)
+    env = SynthR2RBatch(SynthWorld(16, 0, 3), cfg["batch"], seed=9, mode="goal", instr_len=cfg["instr_len"],
+                        variable_len=True)
+    ag = _agent(R, env, cfg["max_action"])
+    assert ag.encoder.bert.update_add_layer
+    for m in ag.models:
+        for sub in m.modules():
+            if isinstance(sub, torch.nn.Dropout):
+                sub.p = 0.0
+    monkeypatch.setattr(param.args, "ml_weight", param.args.ml_weight_org)
+    ag.sample_fn = lambda p: p.argmax(-1)
+    ag.zero_grad()
+    ag.accumulate_gradient("sample")
+    assert abs(ag.loss.item() - float(G["ft/loss"])) < TOL * max(1.0, abs(float(G["ft/loss"])))
+    assert abs(ag.logs["ml_loss"][0] - float(G["ft/ml_loss_teacher"])) < 1e-3
+    assert abs(ag.logs["ml_loss"][1] - float(G["ft/ml_loss_sample"])) < 1e-3
+    assert abs(ag.logs["normalized_rl_loss"][-1] - float(G["ft/rl_loss"])) < TOL
+    if deferred:
+        with DF.defer_bilstm_backward(), DF.defer_weight_grads():
+            ag.loss.backward()
+        DF.flush_bilstm_backward()
+        DF.flush_weight_grads()
+    else:
+        ag.loss.backward()
+    n = 0
+    for name, mod in (("encoder", ag.encoder), ("decoder", ag.decoder), ("critic", ag.critic), ("adaIn", ag.adaIn)):
+        n += check_grads(G, f"ft/{name}.", [(k, p.grad) for k, p in mod.named_parameters()], rtol=2e-3)
+    assert n == sum(1 for k in G if k.startswith("gnorm/ft/"))
+    for k, p in ag.encoder.named_parameters():     # the same parameter set receives gradients
+        assert (p.grad is not None) == (f"gnorm/ft/encoder.{k}" in G), k
 
 
 @pytest.mark.parametrize("batched", ["1", "0"])
