@@ -50,6 +50,9 @@ def parse():
     p.add_argument("--shapes", type=int, default=0, help="add the top-N GEMM shapes by device time")
     p.add_argument("--fast-exit", action="store_true",
                    help="os._exit after the JSON line (skips interpreter teardown; used under rocprofv3)")
+    p.add_argument("--no-cfg5", action="store_true", help="skip the BASELINE configs[4] (B=256, vl=6, bf16) leg")
+    p.add_argument("--cfg5-only", action="store_true", help="run only the configs[4] leg (tuning)")
+    p.add_argument("--cfg5-steps", type=int, default=6, help="decision steps per configs[4] rollout")
     p.add_argument("--backend", default="nccl", help="nccl (= RCCL on ROCm) | gloo (rehearsal only)")
     p.add_argument("--same-device", action="store_true",
                    help="map every rank to cuda:0 (rehearsing the DP path on a one-GPU box with gloo)")
@@ -170,12 +173,53 @@ def cpu_baseline(a):
                       f"{platform.processor() or platform.machine()})"}
 
 
+def cfg5_leg(a):
+    """BASELINE configs[4]: B=256, d_vl_layers=6, 36x2048 synthetic feats, forward (eval/argmax rollout)
+    with bf16 GEMM operands and fp32 accumulation (ops.bf16_matmul); the same rollout in fp32 beside it.
+    A decision step here is one batched step of 256 agents; the roofline is the bf16 GEMM family's."""
+    from types import SimpleNamespace
+    from dasa_amd import ops, prof
+    c = SimpleNamespace(**vars(a))
+    c.batch, c.vl, c.max_action = 256, 6, a.cfg5_steps
+    agent, _ = build_agent(c, 0, 1)
+    res = {"workload": f"configs[4]: eval/argmax rollout, B=256, vl=6, la=9, L=80, {c.max_action} steps, "
+                       "36x2048 synthetic feats", "unit": "agent-decisions/s"}
+    for mode in ("bf16", "fp32"):
+        def run():
+            if mode == "bf16":
+                with torch.no_grad(), ops.bf16_matmul():
+                    return fwd_rollout(agent)
+            return fwd_rollout(agent)
+        run()
+        u, dt = timed(run, 2, 0, 1)
+        ent = {"value": round(u / dt, 2), "ms_per_step": round(1000 * dt * c.batch / u, 2)}
+        with prof.collect() as rec:
+            run()
+        summ = rec.summary()
+        ent["kernels"] = {k: v for k, v in summ["kernels"].items() if k in ("gemm", "gemm_bf16", "mha", "bilstm",
+                                                                              "layernorm", "elementwise")}
+        fam = "gemm_bf16" if mode == "bf16" else "gemm"
+        if fam in summ["kernels"]:
+            k = summ["kernels"][fam]
+            ent["roofline"] = {"kernel": fam, "bound": "mfma", "achieved": k["achieved"], "peak": k["peak"],
+                               "unit": "TFLOP/s", "frac": k["frac"]}
+        res[mode] = ent
+    res["dtype_note"] = ("bf16: nn.Linear operands rounded to bf16 (weights once, activations on load), fp32 "
+                         "accumulation and epilogue; attention cores, LayerNorm, softmax, LSTM recurrences fp32")
+    del agent
+    torch.cuda.empty_cache()
+    return res
+
+
 def main():
     a = parse()
     rank, world = setup_dist(a)
     torch.manual_seed(1 + rank)
     from dasa_amd import functional as DF
     DF.reseed(1234 + rank)
+    if a.cfg5_only:
+        print(json.dumps({"cfg5": cfg5_leg(a)}), flush=True)
+        return
     agent, env = build_agent(a, rank, world)
     for _ in range(a.warmup):
         train_step(agent)
@@ -205,6 +249,8 @@ def main():
         out["hbm_kernels"] = kbench.hbm_kernels((a.batch, 256))
         out["hbm_kernels_note"] = ("AdaIN gate / mu-sigma and attention kernels in isolation, graph-replayed back to back "
                                    "(no host gaps); B=256 is BASELINE configs[4]'s batch; algorithmic bytes / time vs 8 TB/s")
+    if rank == 0 and world == 1 and not a.no_cfg5:
+        out["cfg5"] = cfg5_leg(a)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a)
     if rank == 0:

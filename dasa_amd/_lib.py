@@ -42,6 +42,8 @@ SIGNATURES = {
     "dasa_error_string": (C.c_char_p, [i32]),
     "dasa_gemm_f32_workspace": (i64, [C.POINTER(GemmDesc)]),
     "dasa_gemm_f32": (i32, [C.POINTER(GemmDesc), vp, i64, vp]),
+    "dasa_gemm_bf16": (i32, [C.POINTER(GemmDesc), vp]),
+    "dasa_f32_to_bf16": (i32, [vp, vp, i64, vp]),
     "dasa_gemm_force_config": (i32, [i32]),
     "dasa_layernorm_fwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, f32, f32, u64, vp]),
     "dasa_layernorm_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp]),

@@ -10,6 +10,7 @@
 // (bias, activation, gate-multiply for DGAdaChannel, column scale for env-drop, beta accumulate).
 // Split-K over gridDim.z with a deterministic fixed-order reduce for skinny (M<=64) decoder GEMMs.
 #include "common.h"
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 #include "../../include/dasa_hip.h"
@@ -903,6 +904,138 @@ int launch_cfg(int cfg, bool vec, bool glds_ok, const GemmP& p, const SkP* sk, i
 
 inline long cdiv(long a, long b) { return (a + b - 1) / b; }
 
+// ---- bf16-operand NT GEMM (BASELINE configs[4]: B = 256, bf16 with fp32 accumulation) --------------
+// C = epilogue(A . W^T): A fp32 [M][lda] converted to bf16 on its way into LDS (v_cvt_pk_bf16_f32,
+// round-to-nearest-even), W bf16 [N][ldb] (a weight copy converted once), v_mfma_f32_16x16x32_bf16,
+// fp32 accumulators and the fp32 fused epilogue of the f32 kernels. K tiles of 64 bf16 = 128-B LDS
+// rows of eight 16-B quads, quad q of row r at slot q ^ ((r >> 1) & 7) (two rows per 256-B bank row:
+// each 16-lane ds_read_b128 group hits 16 distinct slots); two LDS stages, one barrier per K tile,
+// next tile prefetched into registers across the MFMAs.
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef short bf16x8_t __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
+  const f32x2_t w = {a, b};
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(w, bf16x2_t));
+}
+
+__device__ __forceinline__ int bswz(int row) { return (row >> 1) & 7; }
+
+template <int BM, int BN, int WAVES_M, int WAVES_N>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_nt_kernel(GemmP p) {
+  constexpr int NT = 64 * WAVES_M * WAVES_N;
+  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N, TM = WM / 16, TN = WN / 16;
+  constexpr int NA = BM * 8 / NT, NB = BN * 8 / NT;   // 16-B bf16 quads per thread per tile
+  static_assert((BM * 8) % NT == 0 && (BN * 8) % NT == 0, "tile quads must split evenly");
+  constexpr int STAGE = (BM + BN) * 8;                // uint4 per LDS stage
+  __shared__ uint4 smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave / WAVES_N) * WM, wn = (wave % WAVES_N) * WN;
+  const int wgid = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+  int m0, n0;
+  if (p.group_m > 1) {
+    const int gm = p.group_m, per = gm * gridDim.x, grp = wgid / per;
+    const int rows = min(gm, (int)gridDim.y - grp * gm), r = wgid - grp * per;
+    m0 = (grp * gm + r % rows) * BM;
+    n0 = (r / rows) * BN;
+  } else {
+    n0 = (wgid % gridDim.x) * BN;
+    m0 = (wgid / gridDim.x) * BM;
+  }
+  const int b = blockIdx.z;
+  const float* A = p.A + (long)b * p.sA;
+  const unsigned short* W = reinterpret_cast<const unsigned short*>(p.B) + (long)b * p.sB;
+
+  floatx4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // staging registers of the next K tile (a struct with member functions like TileLoader: hipcc keeps
+  // it in VGPRs, where lambda-captured local arrays were promoted to LDS)
+  struct Stage {
+    float4 a[NA][2];
+    uint4 b[NB];
+    __device__ __forceinline__ void load(const GemmP& p, const float* A, const unsigned short* W, int m0, int n0,
+                                         int k0, int tid) {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int q = tid + NT * i, row = q >> 3, kq = q & 7;
+        const float* src = A + (long)min(m0 + row, p.M - 1) * p.lda + k0 + 8 * kq;
+        a[i][0] = *reinterpret_cast<const float4*>(src);
+        a[i][1] = *reinterpret_cast<const float4*>(src + 4);
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const int q = tid + NT * i, row = q >> 3, kq = q & 7;
+        b[i] = *reinterpret_cast<const uint4*>(W + (long)min(n0 + row, p.N - 1) * p.ldb + k0 + 8 * kq);
+      }
+    }
+    __device__ __forceinline__ void store(uint4* S, int tid) const {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int q = tid + NT * i, row = q >> 3, kq = q & 7;
+        const float4 x = a[i][0], y = a[i][1];
+        S[row * 8 + (kq ^ bswz(row))] = uint4{pack_bf16x2(x.x, x.y), pack_bf16x2(x.z, x.w),
+                                              pack_bf16x2(y.x, y.y), pack_bf16x2(y.z, y.w)};
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const int q = tid + NT * i, row = q >> 3, kq = q & 7;
+        S[BM * 8 + row * 8 + (kq ^ bswz(row))] = b[i];
+      }
+    }
+  } stg;
+  // clamped rows: rows past M / N re-read the last valid row; the epilogue never stores them
+  // lane l of a 16x16x32 MFMA holds A[row l & 15][k = 8 (l >> 4) + j]: K step s reads quad 4s + (l >> 4)
+  auto compute = [&](const uint4* S) {
+    const uint4* As = S;
+    const uint4* Bs = S + BM * 8;
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const int q = 4 * st + (lane >> 4);
+      bf16x8_t af[TM], bf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm + 16 * i + (lane & 15);
+        af[i] = __builtin_bit_cast(bf16x8_t, As[row * 8 + (q ^ bswz(row))]);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn + 16 * j + (lane & 15);
+        bf[j] = __builtin_bit_cast(bf16x8_t, Bs[row * 8 + (q ^ bswz(row))]);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  const int nk = p.K / 64;
+  stg.load(p, A, W, m0, n0, 0, tid);
+  stg.store(smem, tid);
+  __syncthreads();
+  for (int t = 0; t < nk; ++t) {
+    stg.load(p, A, W, m0, n0, 64 * min(t + 1, nk - 1), tid);   // unconditional (see gemm_nt_k64_kernel)
+    compute(smem + (t & 1) * STAGE);
+    stg.store(smem + ((t + 1) & 1) * STAGE, tid);
+    __syncthreads();
+  }
+  store_tile_mf<16, TM, TN, BM, BN>(p, acc, b, 0, m0, n0, wm, wn, lane);
+}
+
+__global__ void f32_to_bf16_kernel(const float* __restrict__ x, unsigned* __restrict__ y, long npairs) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < npairs; i += (long)gridDim.x * blockDim.x) {
+    const float2 v = reinterpret_cast<const float2*>(x)[i];
+    y[i] = pack_bf16x2(v.x, v.y);
+  }
+}
+
 }  // namespace
 
 struct Plan { int cfg, splitk, kchunk; int64_t ws; int sk_grid, sk_dp, sk_tiles, sk_ipt; int group_m; };
@@ -967,8 +1100,9 @@ static Plan make_plan(const dasa_gemm_desc* d) {
   else if (t64 >= 250 && (K < 1536 || t64 >= 320)) pl.cfg = 5;
   else pl.cfg = 4;
   // forced value = cfg + 64 * split + 4096 * group (tuning sweeps)
-  const int fcfg = g_force_cfg >= 0 ? g_force_cfg % 64 : -1, fsplit = g_force_cfg >= 0 ? (g_force_cfg / 64) % 64 : 0;
-  const int fgroup = g_force_cfg >= 0 ? g_force_cfg / 4096 : 0;
+  const int fval = g_force_cfg < (1 << 20) ? g_force_cfg : -1;   // >= 1 << 20: a bf16 configuration
+  const int fcfg = fval >= 0 ? fval % 64 : -1, fsplit = fval >= 0 ? (fval / 64) % 64 : 0;
+  const int fgroup = fval >= 0 ? fval / 4096 : 0;
   if (fcfg >= 0 && fcfg < kNumCfgs) pl.cfg = fcfg;
   const int bm = kCfgs[pl.cfg].bm, bn = kCfgs[pl.cfg].bn;
   const long blocks = tiles(bm, bn);
@@ -1091,5 +1225,51 @@ extern "C" int dasa_gemm_f32(const dasa_gemm_desc* d, void* ws, int64_t ws_bytes
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid), dim3(256), 0, st, p);
     DASA_CHECK_LAUNCH();
   }
+  return 0;
+}
+
+// bf16 plan: 128x128 tiles (4 waves, two workgroups per CU); the 256x128 (8-wave) form measured slower
+// on every configs[4] shape (profiles/r01e/gemm_bf16.txt) and is kept for sweeps:
+// dasa_gemm_force_config(kBf16Force + 0 | 1).
+constexpr int kBf16Force = 1 << 20;
+
+extern "C" int dasa_gemm_bf16(const dasa_gemm_desc* d, void* stream) {
+  if (!d) return (int)hipErrorInvalidValue;
+  const int M = d->M, N = d->N, K = d->K, batch = d->batch < 1 ? 1 : d->batch;
+  if (M < 0 || N < 0 || K < 0 || d->opA != 0 || d->opB != 1) return (int)hipErrorInvalidValue;
+  if (K % 64 != 0 || (d->lda & 3) || (d->ldb & 7) || d->lda < K || d->ldb < K || d->ldc < N)
+    return (int)hipErrorInvalidValue;
+  if (((uintptr_t)d->A & 15) || ((uintptr_t)d->B & 15) || (batch > 1 && ((d->strideA & 3) || (d->strideB & 7))))
+    return (int)hipErrorInvalidValue;
+  if (M == 0 || N == 0) return 0;
+  GemmP p{};
+  p.M = M; p.N = N; p.K = K; p.batch = batch; p.splitk = 1; p.kchunk = K;
+  p.A = d->A; p.lda = d->lda; p.sA = d->strideA;
+  p.B = d->B; p.ldb = d->ldb; p.sB = d->strideB;
+  p.C = d->C; p.ldc = d->ldc; p.sC = d->strideC;
+  p.bias = d->bias; p.act = d->act;
+  p.aux = d->aux; p.ld_aux = d->ld_aux; p.sAux = d->strideAux;
+  p.colscale = d->colscale; p.alpha = d->alpha; p.beta = d->beta;
+  p.ws = nullptr;
+  int cfg = 0;
+  if (g_force_cfg >= kBf16Force) cfg = (g_force_cfg - kBf16Force) & 1;
+  const int bm = cfg ? 256 : 128;
+  p.group_m = cdiv(M, bm) >= 8 ? 4 : 1;
+  dim3 grid((unsigned)cdiv(N, 128), (unsigned)cdiv(M, bm), batch);
+  hipStream_t st = (hipStream_t)stream;
+  if (cfg) hipLaunchKernelGGL((gemm_bf16_nt_kernel<256, 128, 4, 2>), grid, dim3(512), 0, st, p);
+  else hipLaunchKernelGGL((gemm_bf16_nt_kernel<128, 128, 2, 2>), grid, dim3(256), 0, st, p);
+  DASA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dasa_f32_to_bf16(const float* x, uint16_t* y, int64_t n, void* stream) {
+  if (n < 0 || (n & 1) || ((uintptr_t)x & 7) || ((uintptr_t)y & 3)) return (int)hipErrorInvalidValue;
+  if (n == 0) return 0;
+  const long np = n / 2;
+  const int grid = (int)std::min<long>(cdiv(np, 256), 4096);
+  hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, x,
+                     reinterpret_cast<unsigned*>(y), np);
+  DASA_CHECK_LAUNCH();
   return 0;
 }

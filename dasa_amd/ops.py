@@ -127,6 +127,70 @@ def gemm(A, B, C, *, M, N, K, opA=0, opB=1, lda, ldb, ldc, bias=None, act=None, 
           detail=(int(M), int(N), int(K), b, int(opA), int(opB)))
 
 
+# bf16 matmul mode (BASELINE configs[4]: B = 256, bf16 weights/operands with fp32 accumulation).
+# Forward-only: nn.Linear forwards whose K % 64 == 0 run dasa_gemm_bf16 on a bf16 copy of the weight
+# (converted once per weight version); LayerNorm, softmax, attention cores, the LSTM recurrences and
+# every elementwise op stay fp32.
+_BF16 = {"on": False}
+_bf16_w = {}
+
+
+class bf16_matmul:
+    """Context manager: the policy's linear layers compute with bf16 operands (no autograd)."""
+
+    def __enter__(self):
+        if torch.is_grad_enabled():
+            raise _lib.DasaError("bf16 matmul mode is forward-only: enter it under torch.no_grad()")
+        self._prev = _BF16["on"]
+        _BF16["on"] = True
+        return self
+
+    def __exit__(self, *exc):
+        _BF16["on"] = self._prev
+        if not self._prev:
+            _bf16_w.clear()
+        return False
+
+
+def to_bf16(x, out=None):
+    """Round an fp32 tensor to bf16 (RNE) on the device: dasa_f32_to_bf16."""
+    _f32(x, "to_bf16.x")
+    x = x.contiguous()
+    if out is None:
+        out = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+    _call("dasa_f32_to_bf16", "elementwise", _lib.lib().dasa_f32_to_bf16, _p(x), _p(out), x.numel(), _stream(),
+          nbytes=6.0 * x.numel())
+    return out
+
+
+def _bf16_weight(W):
+    key = (W.data_ptr(), W._version, tuple(W.shape), W.stride(0))
+    t = _bf16_w.get(key)
+    if t is None:
+        if len(_bf16_w) > 1024:
+            _bf16_w.clear()
+        t = to_bf16(W)
+        _bf16_w[key] = t
+    return t
+
+
+def gemm_bf16(x, Wb, out, *, M, N, K, lda, ldc, bias=None, act=None, aux=None, ld_aux=0, colscale=None,
+              alpha=1.0, beta=0.0):
+    d = GemmDesc()
+    d.M, d.N, d.K, d.batch = int(M), int(N), int(K), 1
+    d.opA, d.opB = 0, 1
+    d.A, d.lda, d.strideA = _p(x), int(lda), 0
+    d.B, d.ldb, d.strideB = _p(Wb), int(Wb.stride(0)), 0
+    d.C, d.ldc, d.strideC = _p(out), int(ldc), 0
+    d.bias = _p(bias)
+    d.act = _ACT_IDS[act] if not isinstance(act, int) else act
+    d.aux, d.ld_aux, d.strideAux = _p(aux), int(ld_aux), 0
+    d.colscale = _p(colscale)
+    d.alpha, d.beta = float(alpha), float(beta)
+    _call("dasa_gemm_bf16", "gemm_bf16", _lib.lib().dasa_gemm_bf16, ctypes.byref(d), _stream(),
+          flops=2.0 * M * N * K, nbytes=4.0 * M * K + 2.0 * K * N + 4.0 * M * N, detail=(int(M), int(N), int(K)))
+
+
 def linear(x, W, b=None, act=None, out=None, aux=None, colscale=None, beta=0.0, alpha=1.0):
     """y = act(x @ W^T + b) [* aux] [* colscale] (+ beta*out). x [..., K] (row-strided ok), W [N, K]."""
     _f32(x, "linear.x")
@@ -142,6 +206,10 @@ def linear(x, W, b=None, act=None, out=None, aux=None, colscale=None, beta=0.0, 
     if aux is not None:
         Ma, ld_aux = _rows(aux)
         assert Ma == M
+    if _BF16["on"] and K % 64 == 0 and lda % 4 == 0 and x.data_ptr() % 16 == 0:
+        gemm_bf16(x, _bf16_weight(W), out, M=M, N=N, K=K, lda=lda, ldc=ldc, bias=b, act=act, aux=aux,
+                  ld_aux=ld_aux, colscale=colscale, alpha=alpha, beta=beta)
+        return out
     gemm(x, W, out, M=M, N=N, K=K, opA=0, opB=1, lda=lda, ldb=W.stride(0), ldc=ldc, bias=b, act=act,
          aux=aux, ld_aux=ld_aux, colscale=colscale, alpha=alpha, beta=beta)
     return out

@@ -8,9 +8,13 @@ import torch
 
 _REC = None
 
+# dense MFMA peaks other than fp32's 157.3 TFLOP/s (MI355X_MICROARCH.md: bf16 ~2.5 PF dense)
+PEAK_TF = {"gemm_bf16": 2500.0}
+
 # family -> (roofline bound, kernel name prefix in rocprof)
 FAMILIES = {
     "gemm": ("mfma", "gemm_f32_kernel"),
+    "gemm_bf16": ("mfma", "gemm_bf16_nt_kernel"),
     "bilstm": ("mfma", "bilstm_step_fused_kernel"),
     "bilstm_bptt": ("mfma", "bilstm_bptt_step_kernel"),
     "shift_attn": ("hbm", "attn_fwd_kernel<12>"),
@@ -57,8 +61,9 @@ class _Recorder:
             ent = {"launches": f["launches"], "device_ms": round(f["ms"], 3), "share": round(f["ms"] / total, 4),
                    "avg_launch_us": round(1e3 * f["ms"] / f["launches"], 2), "bound": bound}
             if bound == "mfma":
+                pk = PEAK_TF.get(name, peak_tf)
                 ach = f["flops"] / s / 1e12 if s > 0 else 0.0
-                ent.update(achieved=round(ach, 2), peak=peak_tf, unit="TFLOP/s", frac=round(ach / peak_tf, 4))
+                ent.update(achieved=round(ach, 2), peak=pk, unit="TFLOP/s", frac=round(ach / pk, 4))
             else:
                 ach = f["bytes"] / s / 1e9 if s > 0 else 0.0
                 ent.update(achieved=round(ach, 1), peak=peak_gbs, unit="GB/s", frac=round(ach / peak_gbs, 4))
@@ -115,3 +120,6 @@ def collect(shapes=0):
         yield rec
     finally:
         _REC = None
+
+# dense MFMA peaks other than fp32's 157.3 TFLOP/s (MI355X_MICROARCH.md: bf16 ~2.5 PF dense)
+PEAK_TF = {"gemm_bf16": 2500.0}

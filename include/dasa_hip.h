@@ -60,6 +60,14 @@ int64_t dasa_gemm_f32_workspace(const dasa_gemm_desc* d);
  * Returns the number of configurations. Host-only; not thread-safe with concurrent GEMM planning. */
 int dasa_gemm_force_config(int cfg);
 int dasa_gemm_f32(const dasa_gemm_desc* d, void* ws, int64_t ws_bytes, void* stream);
+/* bf16-operand nn.Linear forward for BASELINE configs[4] (B = 256, bf16 with fp32 accumulation):
+ * C = epilogue(A . B^T) with A fp32 [M][lda] rounded to bf16 (RNE) on load and B a bf16 weight copy
+ * [N][ldb] (pass its address as d->B), fp32 accumulation, the same fused epilogue as dasa_gemm_f32.
+ * Only opA = 0, opB = 1; K % 64 == 0, lda % 4 == 0, ldb % 8 == 0, 16-B aligned A and B.
+ * Replaces the nn.Linear forwards of model.py / vilmodel.py / agent_dg.py:1519 in that config. */
+int dasa_gemm_bf16(const dasa_gemm_desc* d, void* stream);
+/* y[i] = bf16(x[i]) (round to nearest even), n even; weight copies for dasa_gemm_bf16. */
+int dasa_f32_to_bf16(const float* x, uint16_t* y, int64_t n, void* stream);
 
 /* ---- elementwise / reductions ---------------------------------------------------------------- */
 /* y = LayerNorm(dropout_p(x) + res) over N columns (eps), optionally saving mean/rstd [M] and the

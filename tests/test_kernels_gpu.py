@@ -391,3 +391,64 @@ def test_policy_head(dev):
     freq = torch.bincount(acts, minlength=11).double() / N
     assert (freq - p).abs().max() < 0.03
     assert (lps.cpu().double() - torch.log(p)[acts]).abs().max() < 1e-5
+
+
+def test_f32_to_bf16_matches_torch_rounding(dev):
+    from dasa_amd import ops
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(4096 + 6, generator=g) * 3.0
+    x[:6] = torch.tensor([0.0, -0.0, 1e-40, 65504.0, 1.0 + 2.0 ** -8, 1.0 + 3 * 2.0 ** -9])   # ties, subnormal
+    y = ops.to_bf16(x.to(dev)).cpu()
+    assert torch.equal(y.view(torch.int16), x.to(torch.bfloat16).view(torch.int16))   # RNE, bit-exact
+
+
+@pytest.mark.parametrize("M,N,K", [(20480, 3072, 768), (1040, 2048, 2048), (300, 130, 64), (1, 1024, 2240),
+                                   (517, 768, 3072), (9216, 768, 2176)])
+def test_gemm_bf16(dev, M, N, K):
+    """bf16-operand GEMM (configs[4]) against fp64 host math on the SAME bf16-rounded operands: bf16
+    products are exact in fp32, so the only error is fp32 accumulation (~1e-6 of sum|a*b|)."""
+    from dasa_amd import ops, _lib
+    g = torch.Generator().manual_seed(M + N + K)
+    x = _rand(M, K, g=g)
+    W = _rand(N, K, g=g, scale=0.05)
+    b = _rand(N, g=g)
+    xb, Wb = x.to(torch.bfloat16).double(), W.to(torch.bfloat16).double()
+    L = _lib.lib()
+    for cfg in ((1 << 20), (1 << 20) + 1, -1):
+        L.dasa_gemm_force_config(cfg)
+        try:
+            with torch.no_grad(), ops.bf16_matmul():
+                y = ops.linear(x.to(dev), W.to(dev), b.to(dev), act="gelu").cpu().double()
+        finally:
+            L.dasa_gemm_force_config(-1)
+        z = xb @ Wb.t() + b.double()
+        ref = 0.5 * z * (1.0 + torch.erf(z / math.sqrt(2.0)))
+        scale = (xb.abs() @ Wb.abs().t()).max().item()
+        assert (y - ref).abs().max().item() < 2e-6 * scale + 1e-6, cfg
+
+
+def test_gemm_bf16_epilogue_and_strides(dev):
+    """aux gate, column scale, beta accumulate and a row-strided A (the AdaIN feature layout, ld 2176)."""
+    from dasa_amd import ops
+    g = torch.Generator().manual_seed(5)
+    M, N, K = 333, 2048, 2048
+    buf = _rand(M, 2176, g=g)
+    W = _rand(N, K, g=g, scale=0.05)
+    b = _rand(N, g=g)
+    aux = _rand(M, N, g=g)
+    cs = _rand(N, g=g)
+    c0 = _rand(M, N, g=g)
+    xb, Wb = buf[:, :K].to(torch.bfloat16).double(), W.to(torch.bfloat16).double()
+    out = c0.to(dev)
+    with torch.no_grad(), ops.bf16_matmul():
+        ops.linear(buf.to(dev)[:, :K], W.to(dev), b.to(dev), act="sigmoid", aux=aux.to(dev), colscale=cs.to(dev),
+                   out=out, beta=0.5)
+    ref = torch.sigmoid(xb @ Wb.t() + b.double()) * aux.double() * cs.double() + 0.5 * c0.double()
+    assert (out.cpu().double() - ref).abs().max().item() < 2e-5
+
+
+def test_bf16_mode_is_forward_only(dev):
+    from dasa_amd import ops, _lib
+    with pytest.raises(_lib.DasaError):
+        with ops.bf16_matmul():
+            pass

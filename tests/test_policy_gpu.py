@@ -211,6 +211,39 @@ def test_rollout_eval_argmax(R, dev, host_path):
     assert ["|".join(p[0] for p in tr["path"]) for tr in traj] == list(G["eval/paths"])
 
 
+def test_rollout_bf16_matmul_first_step(R, dev):
+    """configs[4] numerics: the eval rollout under ops.bf16_matmul (bf16 GEMM operands, fp32 accumulation)
+    against the reference's fp32 golden. Only step 0 is compared (argmax paths may legitimately part
+    once logits differ at bf16 precision); tolerance 3e-2 of the logit range, 2e-2 on the states."""
+    from dasa_amd import ops
+    G = golden("cfg1_rollout")
+    cfg = GI.CFG1
+    env = SynthR2RBatch(SynthWorld(16, 0, 3), cfg["batch"], seed=7, mode="goal", instr_len=cfg["instr_len"],
+                        variable_len=True)
+    ag = _agent(R, env, cfg["max_action"])
+    rec = []
+    fwd = ag.decoder.forward
+
+    def wrap(*a, **k):
+        r = fwd(*a, **k)
+        rec.append((r[2].detach().cpu(), r[0].detach().cpu()))
+        return r
+    ag.decoder.forward = wrap
+    ag.loss = 0
+    ag.feedback = "argmax"
+    for m in (ag.encoder, ag.decoder, ag.critic):
+        m.eval()
+    with torch.no_grad(), ops.bf16_matmul():
+        ag.vl_rollout(train_ml=None, train_rl=False, reset=True)
+    logit, h1 = rec[0]
+    ref = torch.from_numpy(G["eval/logit/0"])
+    fin = torch.isfinite(ref)
+    span = (ref[fin].max() - ref[fin].min()).item()
+    close(logit[fin], ref[fin], 3e-2 * span, "bf16 logit0")
+    close(h1, G["eval/h1/0"], 2e-2, "bf16 h1")
+    assert (logit[fin] - ref[fin]).abs().max().item() > 0.0     # the bf16 GEMM actually ran
+
+
 @pytest.mark.parametrize("deferred", [False, True])
 def test_train_iteration_grads(R, dev, deferred):
     """accumulate_gradient('sample') + backward with every dropout p = 0 and argmax 'sampling'.
