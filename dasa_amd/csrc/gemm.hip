@@ -1228,9 +1228,9 @@ extern "C" int dasa_gemm_f32(const dasa_gemm_desc* d, void* ws, int64_t ws_bytes
   return 0;
 }
 
-// bf16 plan: 128x128 tiles (4 waves, two workgroups per CU); the 256x128 (8-wave) form measured slower
-// on every configs[4] shape (profiles/r01e/gemm_bf16.txt) and is kept for sweeps:
-// dasa_gemm_force_config(kBf16Force + 0 | 1).
+// bf16 plan: 128x128 tiles of 8 waves (4x2 of 32x64; 64 KB LDS, two workgroups per CU) won or tied on
+// every configs[4] shape of the sweep (profiles/r01e/gemm_bf16.txt); the other tile/wave forms stay for
+// sweeps: dasa_gemm_force_config(kBf16Force + cfg), cfg 0..6.
 constexpr int kBf16Force = 1 << 20;
 
 extern "C" int dasa_gemm_bf16(const dasa_gemm_desc* d, void* stream) {
@@ -1251,14 +1251,21 @@ extern "C" int dasa_gemm_bf16(const dasa_gemm_desc* d, void* stream) {
   p.aux = d->aux; p.ld_aux = d->ld_aux; p.sAux = d->strideAux;
   p.colscale = d->colscale; p.alpha = d->alpha; p.beta = d->beta;
   p.ws = nullptr;
-  int cfg = 0;
-  if (g_force_cfg >= kBf16Force) cfg = (g_force_cfg - kBf16Force) & 1;
-  const int bm = cfg ? 256 : 128;
+  int cfg = 2;
+  if (g_force_cfg >= kBf16Force) cfg = (g_force_cfg - kBf16Force) % 8;
+  const int bm = (cfg == 1 || cfg == 5) ? 256 : 128, bn = cfg == 3 ? 64 : cfg == 6 ? 256 : 128;
   p.group_m = cdiv(M, bm) >= 8 ? 4 : 1;
-  dim3 grid((unsigned)cdiv(N, 128), (unsigned)cdiv(M, bm), batch);
+  dim3 grid((unsigned)cdiv(N, bn), (unsigned)cdiv(M, bm), batch);
   hipStream_t st = (hipStream_t)stream;
-  if (cfg) hipLaunchKernelGGL((gemm_bf16_nt_kernel<256, 128, 4, 2>), grid, dim3(512), 0, st, p);
-  else hipLaunchKernelGGL((gemm_bf16_nt_kernel<128, 128, 2, 2>), grid, dim3(256), 0, st, p);
+  switch (cfg) {
+    case 1: hipLaunchKernelGGL((gemm_bf16_nt_kernel<256, 128, 4, 2>), grid, dim3(512), 0, st, p); break;
+    case 2: hipLaunchKernelGGL((gemm_bf16_nt_kernel<128, 128, 4, 2>), grid, dim3(512), 0, st, p); break;
+    case 3: hipLaunchKernelGGL((gemm_bf16_nt_kernel<128, 64, 2, 2>), grid, dim3(256), 0, st, p); break;
+    case 4: hipLaunchKernelGGL((gemm_bf16_nt_kernel<128, 128, 4, 4>), grid, dim3(1024), 0, st, p); break;
+    case 5: hipLaunchKernelGGL((gemm_bf16_nt_kernel<256, 128, 8, 2>), grid, dim3(1024), 0, st, p); break;
+    case 6: hipLaunchKernelGGL((gemm_bf16_nt_kernel<128, 256, 2, 4>), grid, dim3(512), 0, st, p); break;
+    default: hipLaunchKernelGGL((gemm_bf16_nt_kernel<128, 128, 2, 2>), grid, dim3(256), 0, st, p); break;
+  }
   DASA_CHECK_LAUNCH();
   return 0;
 }
