@@ -233,7 +233,8 @@ def main():
         "config": {"workload": "cfg2 auglistener training iteration (teacher + sample rollout, backward, "
                                "grad all-reduce, RMSprop), README flags",
                    "global_batch": a.batch * world, "per_rank_batch": a.batch, "max_action": a.max_action,
-                   "instr_len": 80, "vl_layers": a.vl, "la_layers": 9, "parallelism": f"dp{world}"},
+                   "instr_len": 80, "vl_layers": a.vl, "la_layers": 9, "parallelism": f"dp{world}",
+                   "world_size": world, "backend": (dist.get_backend() if world > 1 else None)},
     }
     if not a.no_fwd:
         fwd_rollout(agent)

@@ -63,8 +63,11 @@ SIGNATURES = {
     "dasa_bilstm_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp]),
     "dasa_bilstm_hprev": (i32, [vp, vp, i32, i32, i32, vp]),
     "dasa_bilstm_set_mode": (i32, [i32]),
+    "dasa_set_error_word": (i32, [vp]),
+    "dasa_persist_force_timeout": (i32, [i32]),
     "dasa_bilstm_bwd_workspace": (i64, [i32, i32]),
     "dasa_adain_musigma_fwd": (i32, [vp, i64, vp, i64, vp, i64, vp, i32, i32, f32, vp]),
+    "dasa_adain_musigma_bwd": (i32, [vp, i64, vp, i64, vp, i64, vp, i64, vp, i64, i32, i32, f32, vp]),
     "dasa_reverse_valid": (i32, [vp, vp, vp, i32, i32, i32, vp]),
     "dasa_dropout_fwd": (i32, [vp, i64, vp, i64, i32, i32, f32, u64, vp]),
     "dasa_set_seed_source": (i32, [vp]),

@@ -498,6 +498,52 @@ __global__ __launch_bounds__(256) void adain_musigma_reg_kernel(const float* __r
   }
 }
 
+// AdaIN mu/sigma backward (autograd of model.py:1822-1840), one wave per row, statistics recomputed.
+// With xh = (c - mc)/sc, g = dout:  dc = (ss/sc) * (g - mean(g) - xh * sum(g xh)/(N-1));
+// ds = sum(g)/N + sum(g xh) * (s - ms) / ((N-1) ss). dc / ds may be NULL.
+__global__ __launch_bounds__(256) void adain_musigma_bwd_kernel(const float* __restrict__ cnt, long ldc,
+                                                                const float* __restrict__ sty, long lds,
+                                                                const float* __restrict__ dout, long ldg,
+                                                                float* __restrict__ dc, long lddc,
+                                                                float* __restrict__ ds, long ldds, int M, int N,
+                                                                float eps) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const float* c = cnt + (long)row * ldc;
+  const float* s = sty + (long)row * lds;
+  const float* g = dout + (long)row * ldg;
+  float sc = 0.f, ss = 0.f;
+  for (int i = lane; i < N; i += 64) { sc += c[i]; ss += s[i]; }
+  const float mc = wave_sum(sc) / N, ms = wave_sum(ss) / N;
+  float vc = 0.f, vs = 0.f;
+  for (int i = lane; i < N; i += 64) {
+    const float a = c[i] - mc, b = s[i] - ms;
+    vc += a * a;
+    vs += b * b;
+  }
+  const float sdc = sqrtf(wave_sum(vc) / (N - 1) + eps), sds = sqrtf(wave_sum(vs) / (N - 1) + eps);
+  const float rc = 1.f / sdc;
+  float sg = 0.f, sgx = 0.f;
+  for (int i = lane; i < N; i += 64) {
+    const float gi = g[i];
+    sg += gi;
+    sgx += gi * (c[i] - mc) * rc;
+  }
+  sg = wave_sum(sg);
+  sgx = wave_sum(sgx);
+  const float mg = sg / N, kx = sgx / (N - 1);
+  if (dc) {
+    float* o = dc + (long)row * lddc;
+    const float f = sds * rc;
+    for (int i = lane; i < N; i += 64) o[i] = f * (g[i] - mg - (c[i] - mc) * rc * kx);
+  }
+  if (ds) {
+    float* o = ds + (long)row * ldds;
+    const float ks = sgx / ((N - 1) * sds);
+    for (int i = lane; i < N; i += 64) o[i] = mg + (s[i] - ms) * ks;
+  }
+}
+
 }  // namespace
 
 extern "C" int dasa_version(void) { return 2; }
@@ -631,6 +677,18 @@ extern "C" int dasa_adain_musigma_fwd(const float* content, int64_t ldc_, const 
   }
   hipLaunchKernelGGL(adain_musigma_kernel, dim3(cdivi(M, 4)), dim3(256), 0, (hipStream_t)stream, content,
                      (long)ldc_, style, (long)lds, out, (long)ldo, stats, M, N, eps);
+  DASA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dasa_adain_musigma_bwd(const float* content, int64_t ldc_, const float* style, int64_t lds,
+                                      const float* dout, int64_t ldg, float* dcontent, int64_t lddc, float* dstyle,
+                                      int64_t ldds, int32_t M, int32_t N, float eps, void* stream) {
+  if (M <= 0 || (!dcontent && !dstyle)) return 0;
+  if (N < 2) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(adain_musigma_bwd_kernel, dim3(cdivi(M, 4)), dim3(256), 0, (hipStream_t)stream, content,
+                     (long)ldc_, style, (long)lds, dout, (long)ldg, dcontent, (long)lddc, dstyle, (long)ldds, M, N,
+                     eps);
   DASA_CHECK_LAUNCH();
   return 0;
 }

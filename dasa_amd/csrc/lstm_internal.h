@@ -5,7 +5,7 @@
 #include <cstdint>
 
 bool bilstm_persist_ok(int B, int H);       // backward: B <= 32
-bool bilstm_persist_fwd_ok(int B, int H);   // forward: B <= 32, or B <= 256 at H = 1024 (batch tiles)
+bool bilstm_persist_fwd_ok(int B, int H);   // forward: B <= 32, or B <= 192 at H = 1024 (6 batch tiles)
 int bilstm_persist_fwd(const float* xproj, const float* whh_fwd, const float* whh_bwd, const int32_t* lengths,
                        float* out, float* h_n, float* c_n, float* save_act, float* save_c, int B, int L, int H,
                        float* hbuf, unsigned* sync, hipStream_t st);

@@ -15,6 +15,10 @@
 // Residency: one 1024-thread workgroup per CU, 2*H/8 <= 256 workgroups; the grid is checked against
 // the occupancy query once (the caller uses the step kernels if it would not be co-resident). The
 // callers run nothing concurrently with it (the encoder's side stream is joined before the LSTM).
+// A barrier that times out (a workgroup was not co-resident, e.g. another process or stream held
+// CUs) never returns silently: every workgroup that sees the timeout word fills its outputs with NaN
+// and ORs a bit into the library's error word (dasa_set_error_word), which the host reads at its next
+// sync point and raises on (dasa_amd.ops.check_device_errors).
 #include "common.h"
 #include "lstm_internal.h"
 
@@ -39,14 +43,19 @@ __device__ __forceinline__ void st_sc1(float* p, float v) {
 
 // Arrive + wait on the direction's monotonic counter. Returns false (after setting *tmo) if the
 // other workgroups did not arrive within kSpinTicks; every thread of the workgroup gets the answer.
-__device__ bool dir_barrier(unsigned* cnt, unsigned target, unsigned* tmo, float* flag_lds) {
+// `force` (test hook dasa_persist_force_timeout) takes the timeout path without waiting.
+__device__ bool dir_barrier(unsigned* cnt, unsigned target, unsigned* tmo, float* flag_lds, int force) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave drains its sc1 stores
   __syncthreads();
   if (threadIdx.x == 0) {
     __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const long long t0 = wall_clock64();
     float ok = 1.f;
-    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    if (force) {
+      __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ok = 0.f;
+    }
+    while (ok != 0.f && __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       __builtin_amdgcn_s_sleep(1);
       if (wall_clock64() - t0 > kSpinTicks) {
         __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -55,6 +64,18 @@ __device__ bool dir_barrier(unsigned* cnt, unsigned target, unsigned* tmo, float
       }
     }
     *flag_lds = ok;
+  }
+  __syncthreads();
+  return *flag_lds != 0.f;
+}
+
+// After the recurrence: did any workgroup of this launch time out? (every thread gets the answer)
+__device__ bool launch_failed(unsigned* tmo, unsigned* err, unsigned bit, float* flag_lds) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned t = __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t && err) __hip_atomic_fetch_or(err, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag_lds = t ? 1.f : 0.f;
   }
   __syncthreads();
   return *flag_lds != 0.f;
@@ -73,6 +94,8 @@ struct PFwd {
   float* c_n;
   float* hbuf;            // [2 parity][2 dir][B][H] hand-off
   unsigned* sync;         // [0], [1] arrivals per direction; [2] timeout word (zeroed by the caller)
+  unsigned* err;          // library error word (dasa_set_error_word) or NULL
+  int force_tmo;          // test hook: every barrier times out
   int B, L, H;
 };
 
@@ -174,13 +197,22 @@ __global__ __launch_bounds__(1024) void bilstm_persist_fwd_kernel(PFwd a) {
       // the owners read slot 0 before the next tile's partials overwrite it
       if (bt + 1 < NBT && (bt + 1) * 32 < B) __syncthreads();
     }
-    if (s + 1 < L && !dir_barrier(&a.sync[dir], (unsigned)(s + 1) * G, &a.sync[2], &smem[PW * 1024])) break;
+    if (s + 1 < L && !dir_barrier(&a.sync[dir], (unsigned)(s + 1) * G, &a.sync[2], &smem[PW * 1024], a.force_tmo))
+      break;
   }
+  const bool failed = launch_failed(&a.sync[2], a.err, 1u, &smem[PW * 1024]);
+  const float qnan = __builtin_nanf("");
 #pragma unroll
   for (int bt = 0; bt < NBT; ++bt) {
     const int ob = bt * 32 + oi;
     if (own && ob < B) {
       const long si = ((long)dir * B + ob) * H + uj;
+      if (failed) {   // poison everything this workgroup owns: no partial result passes for a good one
+        for (int t = 0; t < L; ++t) a.out[((long)ob * L + t) * 2 * H + dir * H + uj] = qnan;
+        if (a.h_n) a.h_n[si] = qnan;
+        if (a.c_n) a.c_n[si] = qnan;
+        continue;
+      }
       if (a.h_n) a.h_n[si] = NBT > 1 ? hst[bt * 256 + threadIdx.x] : h1;
       if (a.c_n) a.c_n[si] = NBT > 1 ? cst[bt * 256 + threadIdx.x] : c1;
     }
@@ -199,6 +231,8 @@ struct PBwd {
   const float* dc_n;
   float* dgates;          // [B][L][2][4H]: output and the step-to-step hand-off (stored sc1)
   unsigned* sync;
+  unsigned* err;
+  int force_tmo;
   int B, L, H;
 };
 
@@ -305,11 +339,32 @@ __global__ __launch_bounds__(1024) void bilstm_persist_bwd_kernel(PBwd a) {
         dh = rec + dh;
       }
     }
-    if (s + 1 < L && !dir_barrier(&a.sync[dir], (unsigned)(s + 1) * G, &a.sync[2], &smem[PW * 512])) break;
+    if (s + 1 < L && !dir_barrier(&a.sync[dir], (unsigned)(s + 1) * G, &a.sync[2], &smem[PW * 512], a.force_tmo))
+      break;
+  }
+  if (launch_failed(&a.sync[2], a.err, 2u, &smem[PW * 512]) && owner) {
+    const float qnan = __builtin_nanf("");
+    for (int t = 0; t < L; ++t) {
+      float* dg = a.dgates + (((long)ob * L + t) * 2 + dir) * G4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dg[q * H + j] = qnan;
+    }
   }
 }
 
 }  // namespace
+
+// Library error word (device pointer, dasa_set_error_word) and the forced-timeout test hook.
+static unsigned* g_err_word = nullptr;
+static int g_force_tmo = 0;
+extern "C" int dasa_set_error_word(uint32_t* dev_word) {
+  g_err_word = reinterpret_cast<unsigned*>(dev_word);
+  return 0;
+}
+extern "C" int dasa_persist_force_timeout(int32_t on) {
+  g_force_tmo = on ? 1 : 0;
+  return 0;
+}
 
 // Residency check done once per kernel: the grid (one 1024-thread workgroup per CU) must fit the
 // device in one wave of workgroups. Launched as plain kernels: a cooperative launch adds only this
@@ -349,7 +404,8 @@ bool bilstm_persist_fwd_ok(int B, int H) {
 int bilstm_persist_fwd(const float* xproj, const float* whh_fwd, const float* whh_bwd, const int32_t* lengths,
                        float* out, float* h_n, float* c_n, float* save_act, float* save_c, int B, int L, int H,
                        float* hbuf, unsigned* sync, hipStream_t st) {
-  PFwd a{xproj, whh_fwd, whh_bwd, lengths, out, save_act, save_c, h_n, c_n, hbuf, sync, B, L, H};
+  PFwd a{xproj, whh_fwd, whh_bwd, lengths, out, save_act, save_c, h_n, c_n, hbuf, sync, g_err_word, g_force_tmo,
+         B, L, H};
   const int grid = 2 * H / PU;
   if (B > 32) {
     if (H != 1024 || B > 192) return (int)hipErrorInvalidValue;
@@ -373,7 +429,8 @@ int bilstm_persist_fwd(const float* xproj, const float* whh_fwd, const float* wh
 int bilstm_persist_bwd(const float* whh_fwd, const float* whh_bwd, const int32_t* lengths, const float* save_act,
                        const float* save_c, const float* dout, const float* dh_n, const float* dc_n, float* dgates,
                        int B, int L, int H, unsigned* sync, hipStream_t st) {
-  PBwd a{whh_fwd, whh_bwd, lengths, save_act, save_c, dout, dh_n, dc_n, dgates, sync, B, L, H};
+  PBwd a{whh_fwd, whh_bwd, lengths, save_act, save_c, dout, dh_n, dc_n, dgates, sync, g_err_word, g_force_tmo,
+         B, L, H};
   const int grid = 2 * H / PU;
   switch (H / 64) {   // NGB = 4H / 256
     case 4: return launch_persistent(bilstm_persist_bwd_kernel<4>, grid, a, st);

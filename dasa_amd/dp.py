@@ -77,9 +77,19 @@ def _trainable(agent):
 
 
 def attach(agent):
-    """Broadcast rank 0's weights and install the gradient all-reduce in agent.optim_step()."""
+    """Broadcast rank 0's weights and install the gradient all-reduce in agent.optim_step().
+
+    Every rank of an unchanged train.py seeds torch identically (train.py:521), so the random streams
+    are made rank-specific here: torch's generator (nn.Dropout, the env-drop noise) is re-seeded with
+    seed + 7919 * rank, and the counter-RNG seed stream of the HIP kernels (dropout masks, Categorical
+    draws) gets the rank as salt. Rank 0 keeps the single-GPU streams."""
     if not dist.is_initialized() or dist.get_world_size() == 1:
         return None
+    from . import functional as DF
+    rank = dist.get_rank()
+    if rank:
+        torch.manual_seed((torch.initial_seed() + 7919 * rank) % (2**63))
+    DF.set_rank_salt(rank)
     broadcast_params(agent.models)
     sync = GradSync(_trainable(agent))
     agent.grad_sync = sync

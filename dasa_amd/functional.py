@@ -10,17 +10,47 @@ import torch
 
 from . import ops
 
-_seed_rng = np.random.default_rng(int(torch.initial_seed()) & 0xFFFFFFFF)
+class _SeedStream:
+    """Host stream of 63-bit seeds for the counter-RNG kernels (dropout, feature dropout, Categorical
+    draws). It follows torch's seed: derived lazily from torch.initial_seed() at first use and again
+    whenever torch.manual_seed() changed it (train.py:521 seeds after this module is imported), mixed
+    with a per-rank salt (dp.attach) so data-parallel ranks draw different masks and actions."""
+
+    def __init__(self):
+        self.rng = None
+        self.torch_seed = None
+        self.salt = 0
+        self.explicit = False
+
+    def get(self):
+        s = torch.initial_seed()
+        if self.rng is None or (not self.explicit and s != self.torch_seed):
+            self.torch_seed = s
+            self.rng = np.random.default_rng([s & 0xFFFFFFFFFFFFFFFF, self.salt])
+            self.explicit = False
+        return self.rng
+
+
+_SEEDS = _SeedStream()
 
 
 def new_seed():
     """A fresh 63-bit seed for the counter-RNG dropout kernels."""
-    return int(_seed_rng.integers(1, 2**63 - 1))
+    return int(_SEEDS.get().integers(1, 2**63 - 1))
 
 
 def reseed(seed):
-    global _seed_rng
-    _seed_rng = np.random.default_rng(seed)
+    """Pin the seed stream to `seed` (mixed with the rank salt) until torch's seed changes."""
+    _SEEDS.rng = np.random.default_rng([int(seed) & 0xFFFFFFFFFFFFFFFF, _SEEDS.salt])
+    _SEEDS.torch_seed = torch.initial_seed()
+    _SEEDS.explicit = True
+
+
+def set_rank_salt(rank):
+    """Data-parallel ranks: make the seed stream rank-specific (restarts it from torch's seed)."""
+    _SEEDS.salt = int(rank) + 1 if rank else 0
+    _SEEDS.rng = None
+    _SEEDS.explicit = False
 
 
 def _flat(t):
@@ -227,6 +257,35 @@ class AdaFeatFn(torch.autograd.Function):
 
 def ada_feature(f, d, W, b, noise=None, n_angle=128):
     return AdaFeatFn.apply(f, d, W, b, noise, n_angle)
+
+
+class AdaINMuSigmaFn(torch.autograd.Function):
+    """adaptive_instance_normalization (model.py:1832-1840): per-row mu/sigma of content and style
+    (unbiased variance + eps), forward dasa_adain_musigma_fwd, backward dasa_adain_musigma_bwd."""
+
+    @staticmethod
+    def forward(ctx, content, style, eps):
+        ctx.eps = eps
+        if any(ctx.needs_input_grad):
+            ctx.save_for_backward(content, style)
+        return ops.adain_musigma(content, style, eps=eps)
+
+    @staticmethod
+    def backward(ctx, dout):
+        content, style = ctx.saved_tensors
+        dc, ds = ops.adain_musigma_bwd(content, style, dout.contiguous(), ctx.needs_input_grad[0],
+                                       ctx.needs_input_grad[1], ctx.eps)
+        return dc, ds, None
+
+
+def adain_musigma(content, style, eps=1e-5, out=None):
+    if torch.is_grad_enabled() and (content.requires_grad or style.requires_grad):
+        y = AdaINMuSigmaFn.apply(content, style, eps)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+    return ops.adain_musigma(content, style, out=out, eps=eps)
 
 
 # -------------------------------------------------------------------- attention heads

@@ -41,6 +41,7 @@ class StepGraphs:
         self._params = None
         self.entries = {}
         self.counter = None         # device seed counter (uint64), bumped by every replay
+        self.stream = None          # warm-up + capture stream (its workspaces are the graphs' own)
         self.captures = 0
         self.replays = 0
 
@@ -56,24 +57,26 @@ class StepGraphs:
         dev = inputs[0].device
         if self.counter is None:
             self.counter = torch.zeros(1, dtype=torch.int64, device=dev)
+        if self.stream is None:
+            self.stream = torch.cuda.Stream(device=dev)
         static_in = tuple(torch.empty_strided(x.shape, x.stride(), dtype=x.dtype, device=dev) for x in inputs)
         for s, x in zip(static_in, inputs):
             s.copy_(x)
-        # warm-up on a side stream: builds every lazily cached tensor (fused QKV weights, workspaces)
-        # outside the capture, as torch.cuda.graphs requires
-        side = torch.cuda.Stream(device=dev)
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side), torch.no_grad():
+        # warm-up on the capture stream itself: builds every lazily cached tensor (fused QKV weights,
+        # and the GEMM / attention workspaces, which ops.py keys by stream) outside the capture, as
+        # torch.cuda.graphs requires; the capture then reuses them (one workspace per StepGraphs)
+        self.stream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.stream), torch.no_grad():
             fn(*static_in)
-        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.current_stream().wait_stream(self.stream)
         torch.cuda.synchronize(dev)
         g = torch.cuda.CUDAGraph()
         L = _lib.lib()
         ctr = ctypes.c_void_p(self.counter.data_ptr())
         L.dasa_set_seed_source(ctr)
         try:
-            with torch.cuda.graph(g), torch.no_grad():
-                _lib.check(L.dasa_seed_bump(ctr, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
+            with torch.cuda.graph(g, stream=self.stream), torch.no_grad():
+                _lib.check(L.dasa_seed_bump(ctr, ctypes.c_void_p(self.stream.cuda_stream)),
                            "dasa_seed_bump")
                 out = fn(*static_in)
         finally:

@@ -537,6 +537,40 @@ def lstm_cell_bwd(act, c_prev, c, dh, dc):
     return dgates, dc_prev
 
 
+_ERR = {}
+
+
+def _error_word(dev):
+    """The device error word of `dev` (include/dasa_hip.h dasa_set_error_word): persistent kernels
+    OR a bit into it when their inter-workgroup barrier times out (and poison their outputs)."""
+    w = _ERR.get(dev.index)
+    if w is None:
+        w = torch.zeros(1, dtype=torch.int32, device=dev)
+        _ERR[dev.index] = w
+        _lib.check(_lib.lib().dasa_set_error_word(w.data_ptr()), "dasa_set_error_word")
+    return w
+
+
+_ERR_BITS = {1: "persistent bi-LSTM forward: inter-workgroup barrier timed out (outputs poisoned with NaN)",
+             2: "persistent bi-LSTM BPTT: inter-workgroup barrier timed out (gate gradients poisoned with NaN)"}
+
+
+def check_device_errors():
+    """Raise DasaError if a kernel reported a device-side failure since the last check. Reads the
+    error word(s) from the device (a host sync: call it where the caller syncs anyway)."""
+    for idx, w in _ERR.items():
+        v = int(w.item())
+        if v:
+            w.zero_()
+            msgs = [m for bit, m in _ERR_BITS.items() if v & bit] or [f"error word 0x{v:x}"]
+            raise _lib.DasaError(f"device-side failure on cuda:{idx}: " + "; ".join(msgs))
+
+
+def force_persist_timeout(on):
+    """Test hook: every persistent-kernel barrier takes its timeout path."""
+    _lib.check(_lib.lib().dasa_persist_force_timeout(1 if on else 0), "dasa_persist_force_timeout")
+
+
 _CONCURRENT = []
 
 
@@ -568,6 +602,7 @@ def bilstm_fwd(xproj, whh_f, whh_b, lengths_i32, H, save=False):
         sc = torch.empty(L, 2, B, H, dtype=torch.float32, device=dev)
     L_ = _lib.lib()
     ws = torch.empty(L_.dasa_bilstm_workspace(B, H) // 4, dtype=torch.float32, device=dev)
+    _error_word(dev)
     _exclusive(dev)
     _call("dasa_bilstm_fwd", "bilstm", L_.dasa_bilstm_fwd, _p(xproj.contiguous()), _p(whh_f.contiguous()),
           _p(whh_b.contiguous()), _p(lengths_i32), _p(out), _p(h_n), _p(c_n), _p(sa), _p(sc), B, L, H, _p(ws), _stream(),
@@ -581,6 +616,7 @@ def bilstm_bwd(whh_f, whh_b, lengths_i32, saved, dout, dh_n, dc_n, H):
     dev = sa.device
     dgates = torch.empty(B, L, 2, 4 * H, dtype=torch.float32, device=dev)
     ws = torch.empty(_lib.lib().dasa_bilstm_bwd_workspace(B, H) // 4 + 4, dtype=torch.float32, device=dev)
+    _error_word(dev)
     _exclusive(dev)
     _call("dasa_bilstm_bwd", "bilstm_bptt", _lib.lib().dasa_bilstm_bwd, _p(whh_f.contiguous()), _p(whh_b.contiguous()),
           _p(lengths_i32), _p(sa), _p(sc), _p(dout.contiguous()),
@@ -615,6 +651,19 @@ def adain_musigma(content, style, out=None, eps=1e-5):
     _call("dasa_adain_musigma_fwd", "elementwise", _lib.lib().dasa_adain_musigma_fwd, _p(content), ldc, _p(style), lds, _p(out), ldo, None, M, N, float(eps),
                                             _stream())
     return out
+
+
+def adain_musigma_bwd(content, style, dout, want_dcontent=True, want_dstyle=True, eps=1e-5):
+    """Gradients of adain_musigma w.r.t. content and style (dasa_adain_musigma_bwd)."""
+    M, ldc = _rows(content)
+    _, lds = _rows(style)
+    _, ldg = _rows(dout)
+    N = content.shape[-1]
+    dc = torch.empty(content.shape, dtype=torch.float32, device=content.device) if want_dcontent else None
+    ds = torch.empty(style.shape, dtype=torch.float32, device=style.device) if want_dstyle else None
+    _call("dasa_adain_musigma_bwd", "elementwise", _lib.lib().dasa_adain_musigma_bwd, _p(content), ldc, _p(style),
+          lds, _p(dout), ldg, _p(dc), N, _p(ds), N, M, N, float(eps), _stream(), nbytes=4.0 * M * N * 5)
+    return dc, ds
 
 
 def gather_rows(ta, ia, tb, ib, out):

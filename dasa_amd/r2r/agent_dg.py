@@ -732,6 +732,7 @@ class Seq2SeqAgent(BaseAgent):
                 for _ in deferred[k]:
                     self.logs[k].append(vals[i])
                     i += 1
+        ops.check_device_errors()     # a persistent-kernel failure since the last check raises here
         if type(self.loss) is int:
             self.losses.append(0.0)
         else:

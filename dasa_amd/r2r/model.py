@@ -164,6 +164,7 @@ def calc_mean_std(feat, eps=1e-5, dim=-1):
 
 
 def adaptive_instance_normalization(content_feat, style_feat, out=None):
-    """model.py:1832-1840, one wave per row (two wave-shuffle reductions per operand) on gfx950."""
+    """model.py:1832-1840, one wave per row (two wave-shuffle reductions per operand) on gfx950;
+    differentiable in content and style (dasa_adain_musigma_bwd)."""
     assert content_feat.size() == style_feat.size()
-    return ops.adain_musigma(content_feat, style_feat, out=out)
+    return DF.adain_musigma(content_feat, style_feat, out=out)

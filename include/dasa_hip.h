@@ -162,6 +162,13 @@ int dasa_bilstm_bwd(const float* whh_fwd, const float* whh_bwd, const int32_t* l
  * per sequence when B <= 32 and H is a multiple of 256 up to 1024, else one launch per timestep),
  * 1 = per-timestep launches only, 2 = persistent only (error when not eligible). Host-only setting. */
 int dasa_bilstm_set_mode(int mode);
+/* Error word for failures that a kernel can only detect on the device (no host sync inside a call):
+ * a persistent bi-LSTM launch whose inter-workgroup barrier times out (a workgroup was not
+ * co-resident) ORs 1 (forward) / 2 (BPTT) into *dev_word and fills its outputs with NaN. The host
+ * reads the word at its own sync points. NULL disables the report (the NaN poisoning stays).
+ * Host-only setting. dasa_persist_force_timeout(1) is a test hook: every barrier times out. */
+int dasa_set_error_word(uint32_t* dev_word);
+int dasa_persist_force_timeout(int32_t on);
 int dasa_bilstm_hprev(const float* out, float* hprev, int32_t B, int32_t L, int32_t H, void* stream);
 
 /* ---- AdaIN mu/sigma (model.py:1822-1840, adaIn_type default) ---------------------------------
@@ -169,6 +176,11 @@ int dasa_bilstm_hprev(const float* out, float* hprev, int32_t B, int32_t L, int3
 int dasa_adain_musigma_fwd(const float* content, int64_t ldc_, const float* style, int64_t lds,
                            float* out, int64_t ldo, float* stats, int32_t M, int32_t N, float eps,
                            void* stream);
+/* Backward of the above (autograd of model.py:1822-1840): dout -> dcontent, dstyle (either may be
+ * NULL); the row statistics are recomputed from content / style. */
+int dasa_adain_musigma_bwd(const float* content, int64_t ldc_, const float* style, int64_t lds,
+                           const float* dout, int64_t ldg, float* dcontent, int64_t lddc, float* dstyle,
+                           int64_t ldds, int32_t M, int32_t N, float eps, void* stream);
 
 /* ---- training-path elementwise ------------------------------------------------------------------
  * DGAdaChannel with saved gate (agent_dg.py:1537-1547): out = s*f*noise[c]; backward gives the grad

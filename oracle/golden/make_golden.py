@@ -1,8 +1,8 @@
 """Generate tests/golden/*.npz by running the REFERENCE r2r_src code (imported here behind offline
 shims, CPU fp32) on seeded weights/inputs. Container-only test infrastructure: needs /root/reference.
 
-    python oracle/golden/make_golden.py            # every fixture
-    python oracle/golden/make_golden.py finetune   # tests/golden/cfg4_finetune.npz only
+    python oracle/golden/make_golden.py                 # every fixture
+    python oracle/golden/make_golden.py cfg2 cfg5       # the named fixtures only
 
 Fixtures hold outputs only (plus gradient norms and seeded random "sketches" <grad, r_name> for
 large tensors); tests regenerate weights (dasa_amd.synth.init_params) and inputs
@@ -10,7 +10,6 @@ large tensors); tests regenerate weights (dasa_amd.synth.init_params) and inputs
 """
 import os
 import sys
-import zlib
 
 import numpy as np
 import torch
@@ -21,24 +20,18 @@ sys.path.insert(0, ROOT)
 from dasa_amd.synth import SynthR2RBatch, SynthWorld, init_params  # noqa: E402
 from oracle.golden.refimport import import_reference  # noqa: E402
 from tests import golden_inputs as GI  # noqa: E402
+from tests import helpers as H  # noqa: E402
 
 OUT_DIR = os.path.join(ROOT, "tests", "golden")
 
 
-def sketch_vec(name, n):
-    return np.random.default_rng(zlib.crc32(name.encode())).standard_normal(n).astype(np.float64)
-
-
-def grad_record(out, prefix, named_params, full_max=4096):
+def grad_record(out, prefix, named_params):
+    """Norm, max, 8 Gaussian sketches and full values / a fixed row subset of every gradient
+    (tests/helpers.py grad_record / check_grads)."""
     for name, p in named_params:
         if p.grad is None:
             continue
-        g = p.grad.detach().double().flatten().numpy()
-        key = prefix + name
-        out["gnorm/" + key] = np.array(np.linalg.norm(g))
-        out["gsketch/" + key] = np.array(g @ sketch_vec(key, g.size))
-        if g.size <= full_max:
-            out["gfull/" + key] = p.grad.detach().numpy().astype(np.float32)
+        H.grad_record(out, prefix + name, p.grad)
 
 
 def f32(t):
@@ -58,7 +51,12 @@ def per_op(R):
     grad_record(out, "ada/", ada.named_parameters())
     # AdaIN mu/sigma ----------------------------------------------------------------
     c, s = GI.adain_inputs()
-    out["adain/out"] = f32(R.model.adaptive_instance_normalization(c, s))
+    c.requires_grad_(True)
+    s.requires_grad_(True)
+    y = R.model.adaptive_instance_normalization(c, s)
+    out["adain/out"] = f32(y)
+    (y * GI.adain_grad_weights()).sum().backward()
+    grad_record(out, "adain/", [("content", c), ("style", s)])
     # Shift attention ---------------------------------------------------------------
     for K in (5, 3):
         m = init_params(R.model.ShiftSoftDotAttention(1024, 2176, K), 20 + K)
@@ -233,6 +231,135 @@ def rollouts(R):
     return out
 
 
+def _zero_dropout(agent):
+    for mod in (agent.encoder, agent.decoder, agent.critic, agent.adaIn):
+        for sub in mod.modules():
+            if isinstance(sub, torch.nn.Dropout):
+                sub.p = 0.0
+
+
+def _train_iteration(R, agent, out, prefix):
+    """accumulate_gradient('sample') with argmax 'sampling', then backward; losses + gradients."""
+    A = R.args
+    A.ml_weight = A.ml_weight_org
+    orig_sample = torch.distributions.Categorical.sample
+    torch.distributions.Categorical.sample = lambda self, *a, **k: self.probs.argmax(-1)
+    try:
+        agent.zero_grad()
+        agent.accumulate_gradient("sample")
+    finally:
+        torch.distributions.Categorical.sample = orig_sample
+    out[prefix + "loss"] = np.array(agent.loss.item())
+    out[prefix + "ml_loss_teacher"] = np.array(agent.logs["ml_loss"][0])
+    out[prefix + "ml_loss_sample"] = np.array(agent.logs["ml_loss"][1])
+    out[prefix + "rl_loss"] = np.array(agent.logs["normalized_rl_loss"][-1])
+    out[prefix + "steps_teacher"] = np.array(agent.logs["viewsteps/teacher"][-1])
+    out[prefix + "steps_sample"] = np.array(agent.logs["viewsteps/sample"][-1])
+    agent.loss.backward()
+    for name, mod in (("encoder", agent.encoder), ("decoder", agent.decoder), ("critic", agent.critic),
+                      ("adaIn", agent.adaIn)):
+        grad_record(out, f"{prefix}{name}.", mod.named_parameters())
+
+
+def _eval_rollout(agent, feedback, out, prefix, keep_states=()):
+    """An eval rollout (no dropout) with per-step logits, critic values of the decoder state, and the
+    states of the steps in keep_states."""
+    rec = Recorder(agent)
+    for m in (agent.encoder, agent.decoder, agent.critic):
+        m.eval()
+    agent.feedback = feedback
+    agent.loss = 0
+    with torch.no_grad():
+        traj = agent.vl_rollout(train_ml=None, train_rl=False, reset=True)
+        steps = len(rec.rec["logit"])
+        for t in range(steps):
+            out[f"{prefix}logit/{t}"] = rec.rec["logit"][t]
+            # critic values of every step's decoder state (Critic(h_t), agent_dg.py:977)
+            out[f"{prefix}value/{t}"] = f32(agent.critic(torch.from_numpy(rec.rec["h1"][t])))
+            if t in keep_states or t == steps - 1:
+                out[f"{prefix}h_tilde/{t}"] = rec.rec["h_tilde"][t]
+                out[f"{prefix}c1/{t}"] = rec.rec["c1"][t]
+    out[prefix + "steps"] = np.array(steps)
+    out[prefix + "ml_loss"] = np.array(agent.logs["ml_loss"][-1])
+    out[prefix + "paths"] = np.array(["|".join(p[0] for p in tr["path"]) for tr in traj])
+
+
+def cfg2(R):
+    """The bench configuration (B=20, vl=3, L=80): an argmax eval rollout (it ends when every agent
+    stops), a 35-step teacher-forced eval rollout, and one training iteration at maxAction 5 (dropout
+    0, argmax 'sampling')."""
+    A = R.args
+    cfg = GI.CFG2
+    A.d_vl_layers, A.batchSize, A.views = cfg["vl_layers"], cfg["batch"], 36
+    world = SynthWorld(n_viewpoints=cfg["viewpoints"], feat_seed=0, graph_seed=cfg["graph_seed"])
+    out = {}
+    A.maxAction = cfg["max_action"]
+    env = SynthR2RBatch(world, cfg["batch"], seed=cfg["eval_seed"], mode="goal", instr_len=cfg["instr_len"],
+                        variable_len=True)
+    agent = make_agent(R, env, cfg["max_action"])
+    _eval_rollout(agent, "argmax", out, "eval/", keep_states=(0, 1))
+    # the full 35 steps: teacher forcing on 'wander' episodes (the teacher never stops; the bench's
+    # teacher rollout), so logits / critic values are pinned over a whole episode at B=20
+    env = SynthR2RBatch(world, cfg["batch"], seed=cfg["eval_seed"], mode="wander", instr_len=cfg["instr_len"],
+                        variable_len=True)
+    agent = make_agent(R, env, cfg["max_action"])
+    _eval_rollout(agent, "teacher", out, "teacher/", keep_states=(0, 17))
+    A.maxAction = cfg["train_max_action"]
+    env = SynthR2RBatch(world, cfg["batch"], seed=cfg["train_seed"], mode="goal", instr_len=cfg["instr_len"],
+                        variable_len=True)
+    agent = make_agent(R, env, cfg["train_max_action"])
+    _zero_dropout(agent)
+    _train_iteration(R, agent, out, "train/")
+    return out
+
+
+def cfg5(R):
+    """vl=6 (BASELINE configs[4]'s depth) at B=4: a teacher-forced eval rollout, fp32 reference."""
+    A = R.args
+    cfg = GI.CFG5
+    A.d_vl_layers, A.batchSize, A.views, A.maxAction = cfg["vl_layers"], cfg["batch"], 36, cfg["max_action"]
+    world = SynthWorld(n_viewpoints=cfg["viewpoints"], feat_seed=0, graph_seed=cfg["graph_seed"])
+    env = SynthR2RBatch(world, cfg["batch"], seed=cfg["seed"], mode="wander", instr_len=cfg["instr_len"],
+                        variable_len=True)
+    agent = make_agent(R, env, cfg["max_action"])
+    out = {}
+    _eval_rollout(agent, "teacher", out, "teacher/", keep_states=tuple(range(cfg["max_action"])))
+    return out
+
+
+def checkpoint_schema(R):
+    """The structure of a reference checkpoint (Seq2SeqAgent.save, agent_dg.py:1466-1487) after one
+    optimizer step: top-level names, per-module entry names, state_dict keys, optimizer state layout."""
+    import json
+    import tempfile
+    A = R.args
+    cfg = GI.CFG1
+    A.d_vl_layers, A.batchSize, A.maxAction, A.views = cfg["vl_layers"], cfg["batch"], cfg["max_action"], 36
+    world = SynthWorld(n_viewpoints=16, feat_seed=0, graph_seed=3)
+    env = SynthR2RBatch(world, cfg["batch"], seed=8, mode="goal", instr_len=cfg["instr_len"], variable_len=True)
+    agent = make_agent(R, env, cfg["max_action"])
+    _zero_dropout(agent)
+    A.ml_weight = A.ml_weight_org
+    agent.zero_grad()
+    agent.accumulate_gradient("teacher")
+    agent.optim_step()
+    path = os.path.join(tempfile.mkdtemp(prefix="dasa_ckpt_"), "ckpt")
+    agent.save(3, path)
+    st = torch.load(path, map_location="cpu", weights_only=True)
+    desc = {}
+    for name, ent in st.items():
+        opt = ent["optimizer"]
+        desc[name] = {"entries": sorted(ent.keys()), "epoch": ent["epoch"],
+                      "state_dict": sorted(ent["state_dict"].keys()),
+                      "optimizer": sorted(opt.keys()),
+                      "param_groups": [sorted(g.keys()) for g in opt["param_groups"]],
+                      "n_params": [len(g["params"]) for g in opt["param_groups"]],
+                      "state_keys": sorted({k for v in opt["state"].values() for k in v.keys()}),
+                      "n_state": len(opt["state"])}
+    os.remove(path)
+    return {"ckpt/schema": np.array(json.dumps(desc, sort_keys=True))}
+
+
 def finetune(R):
     """cfg4: the finetune path (--d_update_add_layer True, agent_dg.py:152; vilmodel.py:1408-1410 no
     longer detaches), so the LXRT layers and the VisionEncoder receive gradients. Records the LXRT
@@ -286,23 +413,25 @@ def finetune(R):
     return out
 
 
+FIXTURES = {
+    "ops": per_op,
+    "cfg1_rollout": lambda R: {**rollouts(R), **checkpoint_schema(R)},
+    "cfg4_finetune": finetune,
+    "cfg2": cfg2,
+    "cfg5": cfg5,
+}
+
+
 def main():
     R = import_reference()
     os.makedirs(OUT_DIR, exist_ok=True)
-    if sys.argv[1:] == ["finetune"]:
-        ft = finetune(R)
-        np.savez_compressed(os.path.join(OUT_DIR, "cfg4_finetune.npz"), **ft)
-        print("cfg4_finetune.npz:", len(ft), "arrays")
-        return
-    ops = per_op(R)
-    np.savez_compressed(os.path.join(OUT_DIR, "ops.npz"), **ops)
-    print("ops.npz:", len(ops), "arrays")
-    ro = rollouts(R)
-    np.savez_compressed(os.path.join(OUT_DIR, "cfg1_rollout.npz"), **ro)
-    print("cfg1_rollout.npz:", len(ro), "arrays")
-    ft = finetune(R)
-    np.savez_compressed(os.path.join(OUT_DIR, "cfg4_finetune.npz"), **ft)
-    print("cfg4_finetune.npz:", len(ft), "arrays")
+    names = sys.argv[1:] or list(FIXTURES)
+    names = ["cfg4_finetune" if n == "finetune" else n for n in names]
+    for name in names:
+        torch.manual_seed(0)
+        out = FIXTURES[name](R)
+        np.savez_compressed(os.path.join(OUT_DIR, name + ".npz"), **out)
+        print(f"{name}.npz:", len(out), "arrays", flush=True)
 
 
 if __name__ == "__main__":

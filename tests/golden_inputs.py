@@ -10,6 +10,14 @@ CFG1 = dict(batch=2, vl_layers=1, la_layers=9, max_action=5, instr_len=80, kerne
 # cfg4 (finetune, --d_update_add_layer True): the LXRT stack and VisionEncoder are trained; per-rank B=2.
 # Two cross layers so the backward crosses a layer boundary; fewer steps keep the CPU reference short.
 CFG4 = dict(batch=2, vl_layers=2, la_layers=9, max_action=4, instr_len=80, kernel=5)
+# cfg2 (the bench configuration: B=20, vl=3): a full 35-step argmax eval rollout, and one training
+# iteration (teacher + argmax-'sampled' rollout, backward) at maxAction 5 with dropout 0.
+CFG2 = dict(batch=20, vl_layers=3, la_layers=9, max_action=35, train_max_action=5, instr_len=80, kernel=5,
+            viewpoints=32, graph_seed=5, eval_seed=21, train_seed=22)
+# cfg5 numerics at a CPU-affordable batch: vl=6, B=4, a 6-step teacher-forced eval rollout (fp32
+# golden; the GPU compares its fp32 and its bf16-operand rollouts against it).
+CFG5 = dict(batch=4, vl_layers=6, la_layers=9, max_action=6, instr_len=80, kernel=5, viewpoints=16, graph_seed=3,
+            seed=23)
 
 
 def _u(rng, *shape):
@@ -28,6 +36,10 @@ def ada_inputs():
 def adain_inputs():
     rng = np.random.default_rng(101)
     return _u(rng, 2, 10, 2048), _u(rng, 2, 10, 2048)
+
+
+def adain_grad_weights():
+    return _n(np.random.default_rng(102), 2, 10, 2048)
 
 
 def shift_inputs(K):

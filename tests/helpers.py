@@ -23,23 +23,68 @@ def sketch_vec(name, n):
     return np.random.default_rng(zlib.crc32(name.encode())).standard_normal(n).astype(np.float64)
 
 
+N_SKETCH = 8          # independent Gaussian sketches <g, r_i> per recorded gradient
+SUBSET_ROWS = 32      # rows of every matrix gradient larger than FULL_MAX kept in full
+SUBSET_ELEMS = 512    # elements of every vector gradient larger than FULL_MAX kept in full
+FULL_MAX = 4096       # gradients up to this many elements are kept in full
+
+
+def grad_subset_index(key, shape):
+    """The fixed (seeded by the key) row subset of a matrix gradient, or element subset of a vector."""
+    rng = np.random.default_rng(zlib.crc32(("rows:" + key).encode()))
+    n = shape[0]
+    k = min(n, SUBSET_ROWS if len(shape) == 2 else SUBSET_ELEMS)
+    return np.sort(rng.choice(n, size=k, replace=False)).astype(np.int64)
+
+
+def grad_record(out, key, g):
+    """Fixture entries for one gradient (used by oracle/golden/make_golden.py): its norm, max |g|,
+    N_SKETCH sketches, and the full values (small tensors) or a fixed row / element subset."""
+    gd = g.detach().double().cpu()
+    gf = gd.flatten().numpy()
+    out["gnorm/" + key] = np.array(np.linalg.norm(gf))
+    out["gmax/" + key] = np.array(np.abs(gf).max() if gf.size else 0.0)
+    out["gsketch/" + key] = np.array([gf @ sketch_vec(f"{key}#{i}", gf.size) for i in range(N_SKETCH)])
+    if gf.size <= FULL_MAX:
+        out["gfull/" + key] = gd.numpy().astype(np.float32)
+    elif gd.dim() <= 2:
+        idx = grad_subset_index(key, tuple(gd.shape))
+        out["grows/" + key] = gd.numpy()[idx].astype(np.float32)
+
+
 def check_grads(G, prefix, named_grads, rtol=2e-4, atol=1e-6):
-    """Compare grads against fixture norms / sketches / full small tensors. Returns #checked."""
+    """Compare gradients with a fixture. For each recorded gradient g_ref (error e = g - g_ref):
+      * norm:      | ||g|| - ||g_ref|| | <= rtol ||g_ref|| + atol;
+      * sketches:  each <e, r_i> ~ N(0, ||e||^2) for the recorded Gaussian r_i, so requiring
+                   |<e, r_i>| <= 4 rtol ||g_ref|| over N_SKETCH independent sketches bounds ||e|| by
+                   about rtol ||g_ref|| (no sqrt(numel) slack);
+      * elements:  the full tensor (<= FULL_MAX elements) or the fixed row / element subset within
+                   rtol * max|g_ref| + atol (catches a wrong row block, sign or permutation).
+    Returns the number of gradients checked."""
     n = 0
     for name, g in named_grads:
         key = prefix + name
         if "gnorm/" + key not in G:
             continue
         assert g is not None, f"missing grad for {key}"
-        gd = g.detach().double().flatten().cpu().numpy()
+        gt = g.detach().double().cpu()
+        gd = gt.flatten().numpy()
         ref_norm = float(G["gnorm/" + key])
         assert abs(np.linalg.norm(gd) - ref_norm) <= rtol * ref_norm + atol, (key, np.linalg.norm(gd), ref_norm)
-        sk = float(gd @ sketch_vec(key, gd.size))
-        ref_sk = float(G["gsketch/" + key])
-        assert abs(sk - ref_sk) <= rtol * ref_norm * np.sqrt(gd.size) * 0.05 + atol * 10, (key, sk, ref_sk)
+        sks = np.atleast_1d(G["gsketch/" + key])
+        for i, ref_sk in enumerate(sks):
+            sk = float(gd @ sketch_vec(f"{key}#{i}", gd.size))
+            assert abs(sk - ref_sk) <= 4.0 * rtol * ref_norm + 10 * atol, (key, i, sk, float(ref_sk), ref_norm)
+        gmax = float(G["gmax/" + key]) if "gmax/" + key in G else float(np.abs(gd).max())
         if "gfull/" + key in G:
             ref = torch.from_numpy(G["gfull/" + key]).double()
-            assert (g.detach().double().cpu() - ref).abs().max().item() <= rtol * max(1.0, ref.abs().max().item()) + atol, key
+            err = (gt - ref).abs().max().item()
+            assert err <= rtol * max(1.0, ref.abs().max().item()) + atol, (key, err)
+        if "grows/" + key in G:
+            idx = grad_subset_index(key, tuple(gt.shape))
+            ref = torch.from_numpy(G["grows/" + key]).double()
+            err = (gt[torch.from_numpy(idx)] - ref).abs().max().item()
+            assert err <= rtol * gmax + atol, (key, "row subset", err, gmax)
         n += 1
     return n
 

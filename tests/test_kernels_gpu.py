@@ -303,6 +303,42 @@ def _check_bilstm(dev, B, L):
         assert (dWhh_r - lstm.weight_hh_l0_reverse.grad).abs().max() < 1e-3 * max(1, lstm.weight_hh_l0_reverse.grad.abs().max())
 
 
+def test_persistent_barrier_timeout_raises(dev):
+    """A persistent bi-LSTM launch whose inter-workgroup barrier times out must not pass for a good
+    result: its outputs come back NaN and the host raises DasaError at its next check
+    (dasa_set_error_word; test hook dasa_persist_force_timeout makes every barrier time out)."""
+    from dasa_amd import _lib, ops
+    lib = _lib.lib()
+    B, L, H = 4, 6, 1024
+    g = torch.Generator().manual_seed(3)
+    xproj = (torch.randn(B, L, 2, 4 * H, generator=g) * 0.1).to(dev)
+    whh_f = (torch.randn(4 * H, H, generator=g) * 0.02).to(dev)
+    whh_b = (torch.randn(4 * H, H, generator=g) * 0.02).to(dev)
+    li = torch.tensor([6, 5, 3, 1], dtype=torch.int32, device=dev)
+    assert lib.dasa_bilstm_set_mode(2) == 0        # persistent only
+    try:
+        ops.check_device_errors()                   # nothing pending
+        out, h_n, c_n, saved = ops.bilstm_fwd(xproj, whh_f, whh_b, li, H, save=True)
+        assert torch.isfinite(out).all()
+        ops.check_device_errors()
+        ops.force_persist_timeout(True)
+        try:
+            out2, h2, c2, _ = ops.bilstm_fwd(xproj, whh_f, whh_b, li, H, save=True)
+            dg = ops.bilstm_bwd(whh_f, whh_b, li, saved, torch.ones(B, L, 2 * H, device=dev), None, None, H)
+            torch.cuda.synchronize()
+        finally:
+            ops.force_persist_timeout(False)
+        assert torch.isnan(h2).all() and torch.isnan(c2).all() and torch.isnan(out2).all()
+        assert torch.isnan(dg).all()
+        with pytest.raises(_lib.DasaError, match="barrier timed out"):
+            ops.check_device_errors()
+        ops.check_device_errors()                   # reported once, then cleared
+        out3, _, _, _ = ops.bilstm_fwd(xproj, whh_f, whh_b, li, H)
+        assert torch.equal(out3, out)               # and the next launch is healthy again
+    finally:
+        lib.dasa_bilstm_set_mode(0)
+
+
 def test_adain_musigma_reverse_dropout(dev):
     from dasa_amd import ops
     g = torch.Generator().manual_seed(19)

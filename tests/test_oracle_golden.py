@@ -219,3 +219,87 @@ def test_finetune_train_grads():
     # nothing the reference leaves without a gradient gets one here
     for k, v in W.enc.items():
         assert (v.grad is not None) == (f"gnorm/ft/encoder.{k}" in G), k
+
+
+def test_adain_musigma_grads():
+    """adaptive_instance_normalization backward (model.py:1822-1840) w.r.t. content and style."""
+    G = golden("ops")
+    c, s = GI.adain_inputs()
+    c.requires_grad_(True)
+    s.requires_grad_(True)
+    y = O.adaptive_instance_normalization(c, s)
+    (y * GI.adain_grad_weights()).sum().backward()
+    assert check_grads(G, "adain/", [("content", c.grad), ("style", s.grad)], rtol=1e-4) == 2
+
+
+def _cfg2_env(mode, seed):
+    cfg = GI.CFG2
+    return SynthR2RBatch(SynthWorld(cfg["viewpoints"], 0, cfg["graph_seed"]), cfg["batch"], seed=seed, mode=mode,
+                         instr_len=cfg["instr_len"], variable_len=True)
+
+
+def _check_eval_rollout(G, prefix, r, W, tol=5e-5):
+    assert r["steps"] == int(G[prefix + "steps"])
+    for t in range(r["steps"]):
+        close(r["logits"][t], G[f"{prefix}logit/{t}"], tol, f"{prefix}logit{t}")
+        h, c, ht = r["states"][t]
+        close(O.critic(W.critic, h), G[f"{prefix}value/{t}"], tol, f"{prefix}value{t}")
+        if f"{prefix}h_tilde/{t}" in G:
+            close(ht, G[f"{prefix}h_tilde/{t}"], tol, f"{prefix}h_tilde{t}")
+            close(c, G[f"{prefix}c1/{t}"], tol, f"{prefix}c1{t}")
+    assert abs(float(r["ml_loss"]) - float(G[prefix + "ml_loss"])) < 1e-4 * max(1.0, abs(float(G[prefix + "ml_loss"])))
+    assert ["|".join(p) for p in r["traj"]] == list(G[prefix + "paths"])
+
+
+def test_cfg2_eval_rollouts():
+    """The bench configuration (B=20, vl=3, L<=80): the argmax eval rollout (until every agent stops)
+    and a full 35-step teacher-forced eval rollout — logits, critic values, states, paths."""
+    G = golden("cfg2")
+    cfg = GI.CFG2
+    W = oracle_weights(cfg["vl_layers"])
+    kw = dict(la_layers=9, vl_layers=cfg["vl_layers"], episode_len=cfg["max_action"], hoist_lang=True)
+    with torch.no_grad():
+        r = O.vl_rollout(W, _cfg2_env("goal", cfg["eval_seed"]), "argmax", **kw)
+        _check_eval_rollout(G, "eval/", r, W)
+        r = O.vl_rollout(W, _cfg2_env("wander", cfg["eval_seed"]), "teacher", **kw)
+        assert r["steps"] == cfg["max_action"]
+        _check_eval_rollout(G, "teacher/", r, W)
+
+
+def test_cfg2_train_grads():
+    """One training iteration at the bench shape (B=20, vl=3, maxAction 5; dropout 0, argmax 'sampling')."""
+    G = golden("cfg2")
+    cfg = GI.CFG2
+    saved = dict(O.DROP)
+    O.DROP.update(dec=0.0, feat=0.0, enc=0.0, bert=0.0)
+    try:
+        W = oracle_weights(cfg["vl_layers"], requires_grad=True)
+        env = _cfg2_env("goal", cfg["train_seed"])
+        kw = dict(la_layers=9, vl_layers=cfg["vl_layers"], episode_len=cfg["train_max_action"], train=True)
+        r1 = O.vl_rollout(W, env, "teacher", train_ml=0.4, **kw)
+        r2 = O.vl_rollout(W, env, "sample", train_ml=None, train_rl=True, sample_fn=lambda p: p.argmax(-1), **kw)
+    finally:
+        O.DROP.update(saved)
+    loss = r1["loss"] + r2["loss"]
+    assert abs(loss.item() - float(G["train/loss"])) < 2e-5 * max(1, abs(float(G["train/loss"])))
+    assert abs(r2["rl_loss"].item() - float(G["train/rl_loss"])) < 1e-5
+    assert r1["steps"] == int(G["train/steps_teacher"]) and r2["steps"] == int(G["train/steps_sample"])
+    loss.backward()
+    n = 0
+    for name, d in (("encoder", W.enc), ("decoder", W.dec), ("critic", W.critic), ("adaIn", W.ada)):
+        n += check_grads(G, f"train/{name}.", [(k, v.grad) for k, v in d.items()], rtol=2e-4)
+    assert n == sum(1 for k in G if k.startswith("gnorm/train/")) == 30
+
+
+def test_cfg5_vl6_teacher_rollout():
+    """d_vl_layers = 6 (BASELINE configs[4]) at B=4: a 6-step teacher-forced eval rollout."""
+    G = golden("cfg5")
+    cfg = GI.CFG5
+    W = oracle_weights(cfg["vl_layers"])
+    env = SynthR2RBatch(SynthWorld(cfg["viewpoints"], 0, cfg["graph_seed"]), cfg["batch"], seed=cfg["seed"],
+                        mode="wander", instr_len=cfg["instr_len"], variable_len=True)
+    with torch.no_grad():
+        r = O.vl_rollout(W, env, "teacher", la_layers=9, vl_layers=cfg["vl_layers"], episode_len=cfg["max_action"],
+                         hoist_lang=True)
+    assert r["steps"] == cfg["max_action"]
+    _check_eval_rollout(G, "teacher/", r, W)

@@ -437,3 +437,265 @@ def test_vl_stack_graph_replay(R, dev, monkeypatch):
     for x in (a, b):                                    # same distribution as the eager dropout draw
         assert abs(x.std().item() - c.std().item()) < 0.1 * c.std().item()
         assert (x - c).abs().mean().item() < 2.0 * (c - ref_v).abs().mean().item() + 1e-3
+
+
+def test_adain_musigma_vs_reference(R, dev):
+    """mu/sigma AdaIN (adaIn_type default, model.py:1822-1840): forward and content/style gradients
+    against the reference's golden."""
+    model = R[2]
+    G = golden("ops")
+    c, s = GI.adain_inputs()
+    c, s = _req(c, dev), _req(s, dev)
+    y = model.adaptive_instance_normalization(c, s)
+    close(y.detach().cpu(), G["adain/out"], 1e-5, "adain out")
+    (y * GI.adain_grad_weights().to(dev)).sum().backward()
+    assert check_grads(G, "adain/", [("content", c.grad), ("style", s.grad)], rtol=1e-4) == 2
+
+
+def _record_eval(ag, feedback, bf16=False):
+    """Eval rollout with per-step (logit, h1, c1, h_tilde) and the critic value of every step's state."""
+    from dasa_amd import ops
+    rec = []
+    fwd = ag.decoder.forward
+
+    def wrap(*a, **k):
+        r = fwd(*a, **k)
+        rec.append({"logit": r[2].detach().clone(), "h1": r[0].detach().clone(), "c1": r[1].detach().clone(),
+                    "h_tilde": r[3].detach().clone()})
+        return r
+    ag.decoder.forward = wrap
+    ag.loss = 0
+    ag.feedback = feedback
+    for m in (ag.encoder, ag.decoder, ag.critic):
+        m.eval()
+    with torch.no_grad(), (ops.bf16_matmul() if bf16 else _nullctx()):
+        traj = ag.vl_rollout(train_ml=None, train_rl=False, reset=True)
+        for r in rec:
+            r["value"] = ag.critic(r["h1"]).detach().cpu()
+            for k in ("logit", "h1", "c1", "h_tilde"):
+                r[k] = r[k].cpu()
+    ag.decoder.forward = fwd
+    return rec, traj
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def _check_eval(G, prefix, rec, traj, ag, tol=TOL):
+    assert len(rec) == int(G[prefix + "steps"])
+    for t, r in enumerate(rec):
+        close(r["logit"], G[f"{prefix}logit/{t}"], tol, f"{prefix}logit{t}")
+        close(r["value"], G[f"{prefix}value/{t}"], tol, f"{prefix}value{t}")
+        if f"{prefix}h_tilde/{t}" in G:
+            close(r["h_tilde"], G[f"{prefix}h_tilde/{t}"], tol, f"{prefix}h_tilde{t}")
+            close(r["c1"], G[f"{prefix}c1/{t}"], tol, f"{prefix}c1{t}")
+    ref_ml = float(G[prefix + "ml_loss"])
+    assert abs(ag.logs["ml_loss"][-1] - ref_ml) < 1e-4 * max(1.0, abs(ref_ml))
+    assert ["|".join(p[0] for p in tr["path"]) for tr in traj] == list(G[prefix + "paths"])
+
+
+def _cfg2_env(mode, seed):
+    cfg = GI.CFG2
+    return SynthR2RBatch(SynthWorld(cfg["viewpoints"], 0, cfg["graph_seed"]), cfg["batch"], seed=seed, mode=mode,
+                         instr_len=cfg["instr_len"], variable_len=True)
+
+
+@pytest.fixture
+def cfg2_args(R):
+    param = R[0]
+    cfg = GI.CFG2
+    param.readme_train(["--d_vl_layers", str(cfg["vl_layers"]), "--batchSize", str(cfg["batch"]),
+                        "--maxAction", str(cfg["max_action"])])
+    yield param
+    param.readme_train(["--d_vl_layers", "1", "--batchSize", "2", "--maxAction", "5"])
+
+
+def test_cfg2_argmax_rollout(R, dev, cfg2_args):
+    """Bench shape (B=20, vl=3, L<=80): the argmax eval rollout until every agent stops — logits and
+    critic values within 1e-4 of the reference, identical argmax paths."""
+    G = golden("cfg2")
+    cfg = GI.CFG2
+    ag = _agent(R, _cfg2_env("goal", cfg["eval_seed"]), cfg["max_action"])
+    rec, traj = _record_eval(ag, "argmax")
+    _check_eval(G, "eval/", rec, traj, ag)
+
+
+@pytest.mark.parametrize("batched", ["1", "0"])
+def test_cfg2_teacher_rollout_35(R, dev, cfg2_args, monkeypatch, batched):
+    """Bench shape: a full 35-step teacher-forced eval rollout (B=20, vl=3) — every step's logits and
+    critic values within 1e-4 of the reference. batched=1: the train path's chunked encoder."""
+    monkeypatch.setenv("DASA_TEACHER_BATCH", batched)
+    G = golden("cfg2")
+    cfg = GI.CFG2
+    ag = _agent(R, _cfg2_env("wander", cfg["eval_seed"]), cfg["max_action"])
+    rec, traj = _record_eval(ag, "teacher")
+    assert len(rec) == 35
+    _check_eval(G, "teacher/", rec, traj, ag)
+
+
+@pytest.mark.parametrize("deferred", [True, False])
+def test_cfg2_train_iteration_grads(R, dev, cfg2_args, deferred):
+    """Bench configuration's training iteration (B=20, vl=3, maxAction 5; dropout 0, argmax
+    'sampling'): losses within 1e-4 relative, all 30 parameter gradients by norm, 8 sketches and a
+    fixed row subset at rtol 1e-3 (tests/helpers.check_grads)."""
+    from dasa_amd import functional as DF
+    param = cfg2_args
+    G = golden("cfg2")
+    cfg = GI.CFG2
+    param.args.maxAction = cfg["train_max_action"]
+    ag = _agent(R, _cfg2_env("goal", cfg["train_seed"]), cfg["train_max_action"])
+    for m in ag.models:
+        for sub in m.modules():
+            if isinstance(sub, torch.nn.Dropout):
+                sub.p = 0.0
+    param.args.ml_weight = param.args.ml_weight_org
+    ag.sample_fn = lambda p: p.argmax(-1)
+    ag.zero_grad()
+    ag.accumulate_gradient("sample")
+    ref = float(G["train/loss"])
+    assert abs(ag.loss.item() - ref) < TOL * max(1.0, abs(ref))
+    assert abs(ag.logs["ml_loss"][0] - float(G["train/ml_loss_teacher"])) < TOL * max(1.0, float(G["train/ml_loss_teacher"]))
+    assert abs(ag.logs["ml_loss"][1] - float(G["train/ml_loss_sample"])) < TOL * max(1.0, float(G["train/ml_loss_sample"]))
+    assert abs(ag.logs["normalized_rl_loss"][-1] - float(G["train/rl_loss"])) < TOL
+    assert ag.logs["viewsteps/teacher"][-1] == int(G["train/steps_teacher"])
+    assert ag.logs["viewsteps/sample"][-1] == int(G["train/steps_sample"])
+    if deferred:
+        with DF.defer_bilstm_backward(), DF.defer_weight_grads():
+            ag.loss.backward()
+        DF.flush_bilstm_backward()
+        DF.flush_weight_grads()
+    else:
+        ag.loss.backward()
+    n = 0
+    for name, mod in (("encoder", ag.encoder), ("decoder", ag.decoder), ("critic", ag.critic), ("adaIn", ag.adaIn)):
+        n += check_grads(G, f"train/{name}.", [(k, p.grad) for k, p in mod.named_parameters()], rtol=1e-3)
+    assert n == 30
+
+
+# bf16-operand GEMMs (ops.bf16_matmul) against the fp32 reference: per-step logit tolerance as a
+# fraction of that step's logit range. Teacher forcing keeps the paths identical, so every step compares.
+BF16_LOGIT_FRAC = 5e-2
+
+
+def test_cfg5_vl6_teacher_rollout(R, dev, monkeypatch):
+    """d_vl_layers = 6 (BASELINE configs[4]) at B=4, 6 teacher-forced steps: the fp32 rollout within
+    1e-4 of the reference at every step; the bf16-operand rollout within BF16_LOGIT_FRAC of each step's
+    logit range (and 5e-2 on critic values)."""
+    param = R[0]
+    G = golden("cfg5")
+    cfg = GI.CFG5
+    param.readme_train(["--d_vl_layers", str(cfg["vl_layers"]), "--batchSize", str(cfg["batch"]),
+                        "--maxAction", str(cfg["max_action"])])
+    try:
+        def env():
+            return SynthR2RBatch(SynthWorld(cfg["viewpoints"], 0, cfg["graph_seed"]), cfg["batch"], seed=cfg["seed"],
+                                 mode="wander", instr_len=cfg["instr_len"], variable_len=True)
+        ag = _agent(R, env(), cfg["max_action"])
+        rec, traj = _record_eval(ag, "teacher")
+        _check_eval(G, "teacher/", rec, traj, ag)
+        ag = _agent(R, env(), cfg["max_action"])
+        rec, traj = _record_eval(ag, "teacher", bf16=True)
+        assert len(rec) == cfg["max_action"]
+        worst = 0.0
+        for t, r in enumerate(rec):
+            ref = torch.from_numpy(G[f"teacher/logit/{t}"])
+            fin = torch.isfinite(ref)
+            span = (ref[fin].max() - ref[fin].min()).item()
+            err = (r["logit"][fin] - ref[fin]).abs().max().item()
+            worst = max(worst, err / span)
+            assert err <= BF16_LOGIT_FRAC * span, (t, err, span)
+            close(r["value"], G[f"teacher/value/{t}"], 5e-2, f"bf16 value{t}")
+        assert worst > 0.0      # the bf16 GEMM actually ran
+    finally:
+        param.readme_train(["--d_vl_layers", "1", "--batchSize", "2", "--maxAction", "5"])
+
+
+def test_cfg5_full_batch_bf16_vs_fp32(R, dev):
+    """configs[4] at its own size (B=256, vl=6, L=80), 2 teacher-forced eval steps: finite, and the
+    bf16-operand logits within BF16_LOGIT_FRAC of the fp32 rollout's logit range at every step."""
+    param = R[0]
+    param.readme_train(["--d_vl_layers", "6", "--batchSize", "256", "--maxAction", "2"])
+    try:
+        def env():
+            return SynthR2RBatch(SynthWorld(64, 0, 3), 256, seed=31, mode="wander", instr_len=80)
+        ag = _agent(R, env(), 2)
+        r32, _ = _record_eval(ag, "teacher")
+        ag2 = _agent(R, env(), 2)
+        r16, _ = _record_eval(ag2, "teacher", bf16=True)
+        assert len(r32) == len(r16) == 2
+        for a, b in zip(r32, r16):
+            fin = torch.isfinite(a["logit"])
+            assert torch.equal(fin, torch.isfinite(b["logit"]))
+            assert torch.isfinite(b["h1"]).all() and torch.isfinite(b["value"]).all()
+            span = (a["logit"][fin].max() - a["logit"][fin].min()).item()
+            assert (a["logit"][fin] - b["logit"][fin]).abs().max().item() <= BF16_LOGIT_FRAC * span
+    finally:
+        param.readme_train(["--d_vl_layers", "1", "--batchSize", "2", "--maxAction", "5"])
+
+
+def test_checkpoint_roundtrip(R, dev, tmp_path):
+    """Seq2SeqAgent.save / load (agent_dg.py:1466-1510): (1) after one optimizer step the checkpoint
+    has the reference's structure — top-level modules, per-module entries, state_dict keys, optimizer
+    layout and state (tests/golden ckpt/schema, written by the reference's own save); (2) a checkpoint
+    in the reference schema built from the golden weights loads into a fresh agent and reproduces the
+    reference's eval rollout; (3) save -> load into a differently initialised agent gives bitwise the
+    same rollout."""
+    import json
+    param = R[0]
+    G = golden("cfg1_rollout")
+    cfg = GI.CFG1
+
+    def env(seed):
+        return SynthR2RBatch(SynthWorld(16, 0, 3), cfg["batch"], seed=seed, mode="goal", instr_len=cfg["instr_len"],
+                             variable_len=True)
+    ag = _agent(R, env(8), cfg["max_action"])
+    for m in ag.models:
+        for sub in m.modules():
+            if isinstance(sub, torch.nn.Dropout):
+                sub.p = 0.0
+    param.args.ml_weight = param.args.ml_weight_org
+    ag.zero_grad()
+    ag.accumulate_gradient("teacher")
+    ag.optim_step()
+    path = str(tmp_path / "ckpt")
+    ag.save(3, path)
+    st = torch.load(path, map_location="cpu", weights_only=True)
+    want = json.loads(str(G["ckpt/schema"]))
+    assert sorted(st.keys()) == sorted(want.keys())
+    for name, ent in st.items():
+        w, opt = want[name], ent["optimizer"]
+        assert sorted(ent.keys()) == w["entries"] and ent["epoch"] == w["epoch"], name
+        assert sorted(ent["state_dict"].keys()) == w["state_dict"], name
+        assert sorted(opt.keys()) == w["optimizer"], name
+        assert [sorted(g.keys()) for g in opt["param_groups"]] == w["param_groups"], name
+        assert [len(g["params"]) for g in opt["param_groups"]] == w["n_params"], name
+        assert sorted({k for v in opt["state"].values() for k in v.keys()}) == w["state_keys"], name
+        assert len(opt["state"]) == w["n_state"], name
+    # (2) a reference-schema checkpoint of the golden weights (what the reference would have written)
+    from tests.helpers import oracle_weights
+    W = oracle_weights(cfg["vl_layers"])
+    ref_ckpt = {name: {"epoch": 7, "state_dict": sd, "optimizer": st[name]["optimizer"]}
+                for name, sd in (("encoder", W.enc), ("decoder", W.dec), ("critic", W.critic), ("adaIn", W.ada))}
+    ref_path = str(tmp_path / "ref_ckpt")
+    torch.save(ref_ckpt, ref_path)
+    fresh = _agent(R, env(7), cfg["max_action"], seed_weights=False)
+    assert fresh.load(ref_path) == 6
+    rec, traj = _record_eval(fresh, "argmax")
+    assert len(rec) == int(G["eval/steps"])
+    for t, r in enumerate(rec):
+        close(r["logit"], G[f"eval/logit/{t}"], TOL, f"ckpt logit{t}")
+    assert ["|".join(p[0] for p in tr["path"]) for tr in traj] == list(G["eval/paths"])
+    # (3) save -> load round trip of the trained agent
+    other = _agent(R, env(7), cfg["max_action"], seed_weights=False)
+    assert other.load(path) == 3
+    ag.env = env(7)
+    a, _ = _record_eval(ag, "argmax")
+    b, _ = _record_eval(other, "argmax")
+    assert len(a) == len(b)
+    for x, y in zip(a, b):
+        assert torch.equal(x["logit"], y["logit"]) and torch.equal(x["value"], y["value"])

@@ -3,7 +3,7 @@
 # Any step that faults, aborts or times out ends the session (nothing else touches the GPU after it).
 set -o pipefail
 mkdir -p gpurun_out
-TAG=${TAG:-r01}
+TAG=${TAG:-r02}
 
 step() {   # step <name> <timeout> <log> cmd...
   local name=$1 t=$2 log=$3; shift 3
@@ -19,8 +19,8 @@ step() {   # step <name> <timeout> <log> cmd...
 [ "${TESTS:-1}" = "1" ] && step tests 400 gpurun_out/tests_$TAG.log python -u -m pytest tests -q -m gpu -x --timeout 120 --timeout-method thread
 grep -E "passed|failed" gpurun_out/tests_$TAG.log | tail -3
 [ "${TESTS:-1}" = "1" ] && step smoke 200 gpurun_out/smoke_$TAG.log python -c "import __graft_entry__ as g; g.smoke()"
-if [ "${DP:-1}" = "1" ]; then
-  step dp 400 gpurun_out/dp2_$TAG.log python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+if [ "${DP:-0}" = "1" ]; then
+  DASA_LSTM_MODE=1 step dp 400 gpurun_out/dp2_$TAG.log python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
     --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 1 --warmup 0 --backend gloo \
     --same-device --no-fwd --no-profile --max-action 4
 fi
