@@ -17,7 +17,6 @@ import contextlib
 import io
 import json
 import os
-import platform
 import sys
 import time
 
@@ -43,7 +42,7 @@ def parse():
     p.add_argument("--viewpoints", type=int, default=64)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-fwd", action="store_true")
-    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--cpu-threads", type=int, default=0, help="0: the CPUs this process may use (OMP_NUM_THREADS share)")
     p.add_argument("--no-profile", action="store_true")
     p.add_argument("--no-kbench", action="store_true",
                    help="skip the isolated HBM-kernel table (dasa_amd.kbench at B=20 and B=256)")
@@ -146,31 +145,19 @@ def kernel_profile(agent, fn, shapes=0):
 
 
 def cpu_baseline(a):
-    """The CPU oracle (oracle/policy.py, the reference math restated in PyTorch-CPU fp32) on a bounded
-    sample of the same workload: one training iteration (teacher + sampled rollout, backward) at
-    B=20, vl=3, L=80 with maxAction=2, on the host's cores."""
-    from oracle import policy as O
-    from tests.helpers import oracle_weights
-    from dasa_amd.synth import SynthR2RBatch, SynthWorld
-    threads = max(1, min(a.cpu_threads, os.cpu_count() or 1))
-    torch.set_num_threads(threads)
-    W = oracle_weights(a.vl, requires_grad=True)
-    for d in (W.enc,):   # BERT stack is detached in the train config: no grads there
-        for k, v in d.items():
-            if k.startswith("bert."):
-                v.requires_grad_(False)
-    env = SynthR2RBatch(SynthWorld(a.viewpoints, 0, 3), a.batch, seed=1000, mode="wander", instr_len=80)
-    T = 2
-    t0 = time.perf_counter()
-    r1 = O.vl_rollout(W, env, "teacher", la_layers=9, vl_layers=a.vl, episode_len=T, train=True, train_ml=0.4)
-    r2 = O.vl_rollout(W, env, "sample", la_layers=9, vl_layers=a.vl, episode_len=T, train=True, train_rl=True)
-    (r1["loss"] + r2["loss"]).backward()
-    dt = time.perf_counter() - t0
-    dec = (r1["steps"] + r2["steps"]) * a.batch
-    return {"value": dec / dt, "unit": "agent-decisions/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/policy.py train iteration (teacher+sample rollouts, backward), B={a.batch}, "
-                      f"vl={a.vl}, L=80, maxAction={T} ({dec} decisions in {dt:.1f}s, {threads} threads, "
-                      f"{platform.processor() or platform.machine()})"}
+    """BASELINE.md's CPU baseline (tools/cpu_baseline.py): the oracle's CPU restatement (oracle/policy.py)
+    on bounded samples of the workloads — cfg2 train (the headline metric's iteration, maxAction 2),
+    cfg2 fwd and cfg1 fwd — 1 warm-up + median of 3 on this host's CPU share."""
+    from tools import cpu_baseline as CB
+    r = CB.run(a.cpu_threads or None)
+    w = r["workloads"]
+    return {"value": w["cfg2_train"]["value"], "unit": "agent-decisions/s", "cores": r["cores"], "kind": "port",
+            "cpu_model": r["cpu_model"],
+            "sample": (f"oracle/policy.py {w['cfg2_train']['sample']} ({r['method']}, {r['cores']} threads, "
+                       f"{r['cpu_model']})"),
+            "fwd_cfg2": w["cfg2_fwd"]["value"], "fwd_cfg1": w["cfg1_fwd"]["value"], "workloads": w,
+            "validation": "profiles/r02/cpu_restatement_vs_reference.json (restatement / reference in the survey "
+                          "container, 8 threads: cfg2 train 0.97, cfg2 fwd 0.86, cfg1 fwd 0.70)"}
 
 
 def cfg5_leg(a):

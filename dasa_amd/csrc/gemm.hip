@@ -1029,6 +1029,184 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_nt_kernel(Ge
   store_tile_mf<16, TM, TN, BM, BN>(p, acc, b, 0, m0, n0, wm, wn, lane);
 }
 
+// ---- fp32 GEMM emulated on bf16 matrix cores ("bf16x6") ------------------------------------------
+// Every fp32 operand x is split exactly into three bf16 planes, x = hi + mid + lo (hi = bf16(x),
+// mid = bf16(x - hi), lo = bf16(x - hi - mid): 3 x 8 significand bits cover fp32's 24). A product
+// x * y then expands to nine bf16 products, each EXACT in fp32 (8 + 8 bits); the six kept here
+// (hh, hm, mh, hl, lh, mm) leave out terms below 2^-25 |x y|, i.e. under fp32's own rounding of the
+// product, and v_mfma_f32_16x16x32_bf16 accumulates them in fp32 — so the result carries fp32
+// accuracy (tests/test_kernels_gpu.py compares its error against the native fp32 MFMA kernel's, both
+// against fp64) at six bf16 MFMAs per tile step = 6/16 of the fp32 MFMA cost.
+// hh goes to its own accumulator, the five small terms to a second one, summed in the epilogue.
+// W (the nn.Linear weight) arrives pre-split (dasa_f32_split3_bf16, once per weight version); A is
+// split on its way into LDS. LDS holds per stage, per plane, the tile quad-major: 16-B unit (q, row)
+// at [q][row] (q = 8-bf16 K group of the 32-deep K tile) — the 16x16x32 fragment read (lane l: row
+// l & 15, quad l >> 4) and the 8-lane ds_write_b128 groups (8 consecutive rows of one quad) are both
+// bank-conflict-free without a swizzle.
+__device__ __forceinline__ void split3_pair(float a, float b, unsigned& h, unsigned& m, unsigned& l) {
+  h = pack_bf16x2(a, b);
+  const float ra = a - __uint_as_float(h << 16), rb = b - __uint_as_float(h & 0xffff0000u);
+  m = pack_bf16x2(ra, rb);
+  l = pack_bf16x2(ra - __uint_as_float(m << 16), rb - __uint_as_float(m & 0xffff0000u));
+}
+
+__device__ __forceinline__ void split3_quad(const float4& x, const float4& y, uint4& h, uint4& m, uint4& l) {
+  split3_pair(x.x, x.y, h.x, m.x, l.x);
+  split3_pair(x.z, x.w, h.y, m.y, l.y);
+  split3_pair(y.x, y.y, h.z, m.z, l.z);
+  split3_pair(y.z, y.w, h.w, m.w, l.w);
+}
+
+template <int BM, int BN, int WAVES_M, int WAVES_N, bool SEP>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_f32x6_nt_kernel(GemmP p, long plane) {
+  constexpr int NT = 64 * WAVES_M * WAVES_N;
+  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N, TM = WM / 16, TN = WN / 16;
+  constexpr int NA = BM * 4 / NT, NB = BN * 4 / NT;    // 16-B (8 x bf16) K quads per thread per plane
+  static_assert((BM * 4) % NT == 0 && (BN * 4) % NT == 0, "tile quads must split evenly");
+  constexpr int PA = BM * 4, PB = BN * 4;               // uint4 per plane image
+  constexpr int STAGE = 3 * (PA + PB);
+  __shared__ uint4 smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave / WAVES_N) * WM, wn = (wave % WAVES_N) * WN;
+  const int wgid = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+  int m0, n0;
+  if (p.group_m > 1) {
+    const int gm = p.group_m, per = gm * gridDim.x, grp = wgid / per;
+    const int rows = min(gm, (int)gridDim.y - grp * gm), r = wgid - grp * per;
+    m0 = (grp * gm + r % rows) * BM;
+    n0 = (r / rows) * BN;
+  } else {
+    n0 = (wgid % gridDim.x) * BN;
+    m0 = (wgid / gridDim.x) * BM;
+  }
+  const int b = blockIdx.z;
+  const float* A = p.A + (long)b * p.sA;
+  const unsigned short* W = reinterpret_cast<const unsigned short*>(p.B) + (long)b * p.sB;
+
+  floatx4 big[TM][TN], small[SEP ? TM : 1][SEP ? TN : 1];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) big[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  if (SEP) {
+#pragma unroll
+    for (int i = 0; i < (SEP ? TM : 1); ++i)
+#pragma unroll
+      for (int j = 0; j < (SEP ? TN : 1); ++j) small[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  // unit u -> (row, quad): 8 consecutive lanes take 8 consecutive rows of one quad (coalesced 128-B
+  // row segments per 4 x 8 lanes on the global side, conflict-free ds_write_b128 groups on the LDS side)
+  struct Stage {
+    float4 a[NA][2];
+    uint4 w[3][NB];
+    __device__ __forceinline__ static void unit(int u, int& row, int& q) {
+      q = (u >> 3) & 3;
+      row = (u & 7) + 8 * (u >> 5);
+    }
+    __device__ __forceinline__ void load(const GemmP& p, const float* A, const unsigned short* W, long plane, int m0,
+                                         int n0, int k0, int tid) {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        int row, q;
+        unit(tid + NT * i, row, q);
+        const float* src = A + (long)min(m0 + row, p.M - 1) * p.lda + k0 + 8 * q;
+        a[i][0] = *reinterpret_cast<const float4*>(src);
+        a[i][1] = *reinterpret_cast<const float4*>(src + 4);
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        int row, q;
+        unit(tid + NT * i, row, q);
+        const unsigned short* src = W + (long)min(n0 + row, p.N - 1) * p.ldb + k0 + 8 * q;
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) w[pl][i] = *reinterpret_cast<const uint4*>(src + pl * plane);
+      }
+    }
+    __device__ __forceinline__ void store(uint4* S, int tid) const {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        int row, q;
+        unit(tid + NT * i, row, q);
+        uint4 h, m, l;
+        split3_quad(a[i][0], a[i][1], h, m, l);
+        S[0 * PA + q * BM + row] = h;
+        S[1 * PA + q * BM + row] = m;
+        S[2 * PA + q * BM + row] = l;
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        int row, q;
+        unit(tid + NT * i, row, q);
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) S[3 * PA + pl * PB + q * BN + row] = w[pl][i];
+      }
+    }
+  } stg;
+
+  auto compute = [&](const uint4* S) {
+    const int q = lane >> 4;
+    bf16x8_t bf[3][TN];
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bf[pl][j] = __builtin_bit_cast(bf16x8_t, S[3 * PA + pl * PB + q * BN + wn + 16 * j + (lane & 15)]);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      bf16x8_t af[3];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        af[pl] = __builtin_bit_cast(bf16x8_t, S[pl * PA + q * BM + wm + 16 * i + (lane & 15)]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        floatx4& sm = SEP ? small[SEP ? i : 0][SEP ? j : 0] : big[i][j];
+        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bf[1][j], sm, 0, 0, 0);
+        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[2][j], sm, 0, 0, 0);
+        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2], bf[0][j], sm, 0, 0, 0);
+        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[1][j], sm, 0, 0, 0);
+        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bf[0][j], sm, 0, 0, 0);
+        big[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[0][j], big[i][j], 0, 0, 0);
+      }
+    }
+  };
+
+  const int nk = p.K / 32;
+  stg.load(p, A, W, plane, m0, n0, 0, tid);
+  stg.store(smem, tid);
+  __syncthreads();
+  for (int t = 0; t < nk; ++t) {
+    stg.load(p, A, W, plane, m0, n0, 32 * min(t + 1, nk - 1), tid);   // unconditional (clamped re-read)
+    compute(smem + (t & 1) * STAGE);
+    stg.store(smem + ((t + 1) & 1) * STAGE, tid);
+    __syncthreads();
+  }
+  if (SEP) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) big[i][j] += small[SEP ? i : 0][SEP ? j : 0];
+  }
+  store_tile_mf<16, TM, TN, BM, BN>(p, big, b, 0, m0, n0, wm, wn, lane);
+}
+
+// x [rows][ldx] fp32 -> y planes [3][rows][cols] bf16 (plane stride rows * cols), x = hi + mid + lo.
+__global__ void split3_bf16_kernel(const float* __restrict__ x, long ldx, uint4* __restrict__ y, int rows, int cols) {
+  const int cq = cols / 8;
+  const long n = (long)rows * cq, plane = n;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / cq;
+    const int c = (int)(i - r * cq) * 8;
+    const float* src = x + r * ldx + c;
+    uint4 h, m, l;
+    split3_quad(*reinterpret_cast<const float4*>(src), *reinterpret_cast<const float4*>(src + 4), h, m, l);
+    y[i] = h;
+    y[i + plane] = m;
+    y[i + 2 * plane] = l;
+  }
+}
+
 __global__ void f32_to_bf16_kernel(const float* __restrict__ x, unsigned* __restrict__ y, long npairs) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < npairs; i += (long)gridDim.x * blockDim.x) {
     const float2 v = reinterpret_cast<const float2*>(x)[i];
@@ -1232,6 +1410,7 @@ extern "C" int dasa_gemm_f32(const dasa_gemm_desc* d, void* ws, int64_t ws_bytes
 // every configs[4] shape of the sweep (profiles/r01e/gemm_bf16.txt); the other tile/wave forms stay for
 // sweeps: dasa_gemm_force_config(kBf16Force + cfg), cfg 0..6.
 constexpr int kBf16Force = 1 << 20;
+constexpr int kX6Force = 1 << 21;   // dasa_gemm_force_config(kX6Force + cfg): bf16x6 tile forms 0..5
 
 extern "C" int dasa_gemm_bf16(const dasa_gemm_desc* d, void* stream) {
   if (!d) return (int)hipErrorInvalidValue;
@@ -1252,7 +1431,7 @@ extern "C" int dasa_gemm_bf16(const dasa_gemm_desc* d, void* stream) {
   p.colscale = d->colscale; p.alpha = d->alpha; p.beta = d->beta;
   p.ws = nullptr;
   int cfg = 2;
-  if (g_force_cfg >= kBf16Force) cfg = (g_force_cfg - kBf16Force) % 8;
+  if (g_force_cfg >= kBf16Force && g_force_cfg < kX6Force) cfg = (g_force_cfg - kBf16Force) % 8;
   const int bm = (cfg == 1 || cfg == 5) ? 256 : 128, bn = cfg == 3 ? 64 : cfg == 6 ? 256 : 128;
   p.group_m = cdiv(M, bm) >= 8 ? 4 : 1;
   dim3 grid((unsigned)cdiv(N, bn), (unsigned)cdiv(M, bm), batch);
@@ -1266,6 +1445,60 @@ extern "C" int dasa_gemm_bf16(const dasa_gemm_desc* d, void* stream) {
     case 6: hipLaunchKernelGGL((gemm_bf16_nt_kernel<128, 256, 2, 4>), grid, dim3(512), 0, st, p); break;
     default: hipLaunchKernelGGL((gemm_bf16_nt_kernel<128, 128, 2, 2>), grid, dim3(256), 0, st, p); break;
   }
+  DASA_CHECK_LAUNCH();
+  return 0;
+}
+
+// fp32-accurate GEMM on bf16 MFMA (bf16x6 split; see gemm_f32x6_nt_kernel). d->B = the hi plane of
+// the pre-split weight, planes `plane` bf16 elements apart.
+extern "C" int dasa_gemm_f32x6(const dasa_gemm_desc* d, int64_t plane, void* stream) {
+  if (!d) return (int)hipErrorInvalidValue;
+  const int M = d->M, N = d->N, K = d->K, batch = d->batch < 1 ? 1 : d->batch;
+  if (M < 0 || N < 0 || K < 0 || d->opA != 0 || d->opB != 1) return (int)hipErrorInvalidValue;
+  if (K % 32 != 0 || (d->lda & 3) || (d->ldb & 7) || (plane & 7) || d->lda < K || d->ldb < K || d->ldc < N)
+    return (int)hipErrorInvalidValue;
+  if (((uintptr_t)d->A & 15) || ((uintptr_t)d->B & 15) || (batch > 1 && ((d->strideA & 3) || (d->strideB & 7))))
+    return (int)hipErrorInvalidValue;
+  if (M == 0 || N == 0) return 0;
+  GemmP p{};
+  p.M = M; p.N = N; p.K = K; p.batch = batch; p.splitk = 1; p.kchunk = K;
+  p.A = d->A; p.lda = d->lda; p.sA = d->strideA;
+  p.B = d->B; p.ldb = d->ldb; p.sB = d->strideB;
+  p.C = d->C; p.ldc = d->ldc; p.sC = d->strideC;
+  p.bias = d->bias; p.act = d->act;
+  p.aux = d->aux; p.ld_aux = d->ld_aux; p.sAux = d->strideAux;
+  p.colscale = d->colscale; p.alpha = d->alpha; p.beta = d->beta;
+  p.ws = nullptr;
+  // 256x128 tiles with the separate small-term accumulator: fastest form on every shape the plan
+  // routes here (profiles/r02/gemm_x6_sweep_a.txt); the others stay for sweeps
+  int cfg = 3;
+  if (g_force_cfg >= kX6Force) cfg = (g_force_cfg - kX6Force) % 16;
+  const int bm = (cfg == 1 || cfg == 3) ? 256 : (cfg == 4 || cfg == 5) ? 64 : 128;
+  const int bn = cfg == 5 ? 64 : 128;
+  p.group_m = cdiv(M, bm) >= 8 ? 4 : 1;
+  dim3 grid((unsigned)cdiv(N, bn), (unsigned)cdiv(M, bm), batch);
+  hipStream_t st = (hipStream_t)stream;
+  switch (cfg) {
+    case 1: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<256, 128, 4, 2, false>), grid, dim3(512), 0, st, p, (long)plane); break;
+    case 2: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, false>), grid, dim3(512), 0, st, p, (long)plane); break;
+    case 3: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<256, 128, 4, 2, true>), grid, dim3(512), 0, st, p, (long)plane); break;
+    case 4: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<64, 128, 2, 2, true>), grid, dim3(256), 0, st, p, (long)plane); break;
+    case 5: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<64, 64, 2, 2, true>), grid, dim3(256), 0, st, p, (long)plane); break;
+    default: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true>), grid, dim3(512), 0, st, p, (long)plane); break;
+  }
+  DASA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dasa_f32_split3_bf16(const float* x, int64_t ldx, uint16_t* y, int32_t rows, int32_t cols,
+                                    void* stream) {
+  if (rows < 0 || cols < 0 || (cols & 7) || (ldx & 3) || ldx < cols || ((uintptr_t)x & 15) || ((uintptr_t)y & 15))
+    return (int)hipErrorInvalidValue;
+  const long n = (long)rows * (cols / 8);
+  if (n == 0) return 0;
+  const int grid = (int)std::min<long>(cdiv(n, 256), 8192);
+  hipLaunchKernelGGL(split3_bf16_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, (long)ldx,
+                     reinterpret_cast<uint4*>(y), rows, cols);
   DASA_CHECK_LAUNCH();
   return 0;
 }

@@ -5,6 +5,8 @@ libdasa_hip.so on torch's current stream (so torch.cuda.graph capture records th
 CPU path: a CPU tensor is a usage error and raises.
 """
 import ctypes
+import os
+import weakref
 
 import torch
 
@@ -191,6 +193,78 @@ def gemm_bf16(x, Wb, out, *, M, N, K, lda, ldc, bias=None, act=None, aux=None, l
           flops=2.0 * M * N * K, nbytes=4.0 * M * K + 2.0 * K * N + 4.0 * M * N, detail=(int(M), int(N), int(K)))
 
 
+# fp32 GEMM emulated on bf16 matrix cores (include/dasa_hip.h dasa_gemm_f32x6): the nn.Linear weight
+# is split once per weight version into three bf16 planes (hi, mid, lo) and cached here; the input is
+# split inside the kernel. fp32-accurate (the six kept bf16 products are exact, dropped terms are below
+# fp32 rounding); DASA_GEMM_EMU=0 routes every nn.Linear back to the native fp32 MFMA kernels.
+_X6 = {}
+_EMU = {"on": os.environ.get("DASA_GEMM_EMU", "1") != "0", "min_rows": int(os.environ.get("DASA_GEMM_EMU_MIN_M", "512"))}
+
+
+def set_gemm_emulation(on=None, min_rows=None):
+    """Switch the bf16x6 fp32 path (returns the previous (on, min_rows))."""
+    prev = (_EMU["on"], _EMU["min_rows"])
+    if on is not None:
+        _EMU["on"] = bool(on)
+    if min_rows is not None:
+        _EMU["min_rows"] = int(min_rows)
+    return prev
+
+
+def split3_bf16(W):
+    """Three bf16 planes [3, N, K] with W = hi + mid + lo (dasa_f32_split3_bf16)."""
+    _f32(W, "split3.W")
+    N, K = W.shape
+    planes = torch.empty(3, N, K, dtype=torch.bfloat16, device=W.device)
+    _call("dasa_f32_split3_bf16", "elementwise", _lib.lib().dasa_f32_split3_bf16, _p(W), W.stride(0), _p(planes),
+          N, K, _stream(), nbytes=10.0 * N * K)
+    return planes
+
+
+def _x6_weight(W):
+    """The cached bf16 planes of W for this weight version (recomputed after in-place updates)."""
+    wid = id(W)
+    e = _X6.get(wid)
+    if e is not None and e[0]() is W and e[1] == W._version and e[2] == W.data_ptr():
+        return e[3]
+    planes = split3_bf16(W)
+
+    def _drop(ref, wid=wid):
+        ent = _X6.get(wid)
+        if ent is not None and ent[0] is ref:
+            del _X6[wid]
+    _X6[wid] = (weakref.ref(W, _drop), W._version, W.data_ptr(), planes)
+    return planes
+
+
+def _emu_ok(M, N, K, lda, x):
+    """Plan rule (profiles/r02/gemm_x6_sweep_a.txt): the 256x128-tile bf16x6 kernel beats the native fp32
+    MFMA kernels when its tiles fill the 256 CUs in whole rounds (>= 200 tiles, >= 85% of the last
+    round busy), e.g. the 12800-row language FFN / QKV and 1600 x 4096 shapes; elsewhere native fp32."""
+    if not (_EMU["on"] and M >= _EMU["min_rows"] and K % 32 == 0 and N % 8 == 0 and lda % 4 == 0
+            and x.data_ptr() % 16 == 0):
+        return False
+    tiles = -(-M // 256) * -(-N // 128)
+    return tiles >= 200 and tiles / (-(-tiles // 256) * 256) >= 0.85
+
+
+def gemm_f32x6(x, planes, out, *, M, N, K, lda, ldc, bias=None, act=None, aux=None, ld_aux=0, colscale=None,
+               alpha=1.0, beta=0.0):
+    d = GemmDesc()
+    d.M, d.N, d.K, d.batch = int(M), int(N), int(K), 1
+    d.opA, d.opB = 0, 1
+    d.A, d.lda, d.strideA = _p(x), int(lda), 0
+    d.B, d.ldb, d.strideB = _p(planes), int(K), 0
+    d.C, d.ldc, d.strideC = _p(out), int(ldc), 0
+    d.bias = _p(bias)
+    d.act = _ACT_IDS[act] if not isinstance(act, int) else act
+    d.aux, d.ld_aux, d.strideAux = _p(aux), int(ld_aux), 0
+    d.colscale = _p(colscale)
+    d.alpha, d.beta = float(alpha), float(beta)
+    _call("dasa_gemm_f32x6", "gemm_x6", _lib.lib().dasa_gemm_f32x6, ctypes.byref(d), int(N) * int(K), _stream(),
+          flops=2.0 * M * N * K, nbytes=4.0 * M * K + 6.0 * K * N + 4.0 * M * N, detail=(int(M), int(N), int(K)))
+
+
 def linear(x, W, b=None, act=None, out=None, aux=None, colscale=None, beta=0.0, alpha=1.0):
     """y = act(x @ W^T + b) [* aux] [* colscale] (+ beta*out). x [..., K] (row-strided ok), W [N, K]."""
     _f32(x, "linear.x")
@@ -209,6 +283,10 @@ def linear(x, W, b=None, act=None, out=None, aux=None, colscale=None, beta=0.0, 
     if _BF16["on"] and K % 64 == 0 and lda % 4 == 0 and x.data_ptr() % 16 == 0:
         gemm_bf16(x, _bf16_weight(W), out, M=M, N=N, K=K, lda=lda, ldc=ldc, bias=b, act=act, aux=aux,
                   ld_aux=ld_aux, colscale=colscale, alpha=alpha, beta=beta)
+        return out
+    if _emu_ok(M, N, K, lda, x):
+        gemm_f32x6(x, _x6_weight(W), out, M=M, N=N, K=K, lda=lda, ldc=ldc, bias=b, act=act, aux=aux,
+                   ld_aux=ld_aux, colscale=colscale, alpha=alpha, beta=beta)
         return out
     gemm(x, W, out, M=M, N=N, K=K, opA=0, opB=1, lda=lda, ldb=W.stride(0), ldc=ldc, bias=b, act=act,
          aux=aux, ld_aux=ld_aux, colscale=colscale, alpha=alpha, beta=beta)

@@ -8,13 +8,12 @@ import torch
 
 _REC = None
 
-# dense MFMA peaks other than fp32's 157.3 TFLOP/s (MI355X_MICROARCH.md: bf16 ~2.5 PF dense)
-PEAK_TF = {"gemm_bf16": 2500.0}
 
 # family -> (roofline bound, kernel name prefix in rocprof)
 FAMILIES = {
     "gemm": ("mfma", "gemm_f32_kernel"),
     "gemm_bf16": ("mfma", "gemm_bf16_nt_kernel"),
+    "gemm_x6": ("mfma", "gemm_f32x6_nt_kernel"),
     "bilstm": ("mfma", "bilstm_step_fused_kernel"),
     "bilstm_bptt": ("mfma", "bilstm_bptt_step_kernel"),
     "shift_attn": ("hbm", "attn_fwd_kernel<12>"),
@@ -121,5 +120,3 @@ def collect(shapes=0):
     finally:
         _REC = None
 
-# dense MFMA peaks other than fp32's 157.3 TFLOP/s (MI355X_MICROARCH.md: bf16 ~2.5 PF dense)
-PEAK_TF = {"gemm_bf16": 2500.0}

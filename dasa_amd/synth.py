@@ -449,96 +449,20 @@ class SynthR2RBatch:
         return obs
 
 
-class DeviceFeatureStore:
-    """Device-resident RGB/depth pools + the 36x36 angle table; assembles the agent's input tensors with
-    one libdasa_hip gather launch per block (dasa_gather_rows)."""
-
-    def __init__(self, world, device, angle_feat_size=ANGLE_FEAT_SIZE):
-        import torch
-        P = world.P
-        self.device = device
-        self.rgb = torch.from_numpy(world.rgb.reshape(P * NUM_VIEWS, FEATURE_SIZE)).to(device)
-        self.depth = torch.from_numpy(world.depth.reshape(P * NUM_VIEWS, FEATURE_SIZE)).to(device)
-        self.angles = torch.from_numpy(angle_table(angle_feat_size).reshape(NUM_VIEWS * NUM_VIEWS, -1)).to(device)
-        self.A = angle_feat_size
-
-    def input_feat(self, obs):
-        a_t, f_t, d_t, cf, cd, cinfo = self.input_feat_steps([obs])
-        _, C, leng = cinfo[0]
-        B = len(obs)
-        return a_t, f_t, d_t, cf.view(B, C, -1), cd.view(B, C, -1), leng
-
-    def input_feat_steps(self, obs_steps):
-        """The input blocks of several rollout steps stacked along the batch (step-major): a_t [T*B, A],
-        panoramas f_t / d_t [T*B, 36, F], and the candidates of every step as flat rows cf / cd [R, F]
-        with cinfo[t] = (first row, C_t, lengths_t) — step t's block is rows [off, off + B*C_t) viewed
-        as [B, C_t, F]. One gather launch per tensor for all steps."""
-        import torch
-        from . import ops
-        A = self.A
-        ia_v, ib_v, ia_c, ib_c, cangs, a_ts, cinfo = [], [], [], [], [], [], []
-        r36 = np.arange(NUM_VIEWS)
-        row = 0
-        for obs in obs_steps:
-            B = len(obs)
-            leng = [len(ob["candidate"]) + 1 for ob in obs]
-            C = max(leng)
-            vp = np.array([ob["_vp_index"] for ob in obs], np.int64)
-            view = np.array([ob["viewIndex"] for ob in obs], np.int64)
-            ia_v.append((vp[:, None] * NUM_VIEWS + r36[None]).astype(np.int32).reshape(-1))
-            ib_v.append((view[:, None] * NUM_VIEWS + r36[None]).astype(np.int32).reshape(-1))
-            iac = np.full((B, C), -1, np.int32)
-            ibc = np.full((B, C), -1, np.int32)
-            cang = np.zeros((B, C, A), np.float32)
-            a_t = np.zeros((B, A), np.float32)
-            base = sum(x.shape[0] for x in cangs)
-            for i, ob in enumerate(obs):
-                a_t[i] = angle_feature(ob["heading"], ob["elevation"], A)
-                for j, c in enumerate(ob["candidate"]):
-                    iac[i, j] = vp[i] * NUM_VIEWS + c["pointId"]
-                    ibc[i, j] = base + i * C + j
-                    cang[i, j] = c["angle"] if "angle" in c else c["feature"][-A:]
-            ia_c.append(iac.reshape(-1))
-            ib_c.append(ibc.reshape(-1))
-            cangs.append(cang.reshape(B * C, A))
-            a_ts.append(a_t)
-            cinfo.append((row, C, leng))
-            row += B * C
-        ia_v, ib_v = np.concatenate(ia_v), np.concatenate(ib_v)
-        ia_c, ib_c = np.concatenate(ia_c), np.concatenate(ib_c)
-        a_t, cang = np.concatenate(a_ts), np.concatenate(cangs)
-        ints = torch.from_numpy(np.concatenate([ia_v, ib_v, ia_c, ib_c])).pin_memory()
-        flts = torch.from_numpy(np.concatenate([a_t.reshape(-1), cang.reshape(-1)])).pin_memory()
-        ints = ints.to(self.device, non_blocking=True)
-        flts = flts.to(self.device, non_blocking=True)
-        N, R = a_t.shape[0], ia_c.shape[0]
-        n = N * NUM_VIEWS
-        ia_v_d, ib_v_d = ints[:n], ints[n:2 * n]
-        ia_c_d, ib_c_d = ints[2 * n:2 * n + R], ints[2 * n + R:]
-        a_t_d = flts[:N * A].view(N, A)
-        cang_d = flts[N * A:].view(R, A)
-        F = FEATURE_SIZE + A
-        f_t = torch.empty(N, NUM_VIEWS, F, dtype=torch.float32, device=self.device)
-        d_t = torch.empty_like(f_t)
-        cf = torch.empty(R, F, dtype=torch.float32, device=self.device)
-        cd = torch.empty_like(cf)
-        ops.gather_rows(self.rgb, ia_v_d, self.angles, ib_v_d, f_t)
-        ops.gather_rows(self.depth, ia_v_d, self.angles, ib_v_d, d_t)
-        ops.gather_rows(self.rgb, ia_c_d, cang_d, ib_c_d, cf)
-        ops.gather_rows(self.depth, ia_c_d, cang_d, ib_c_d, cd)
-        return a_t_d, f_t, d_t, cf, cd, cinfo
+def _store(self, device):
+    """The env's device-resident feature store (dasa_amd.features.DeviceFeatureStore)."""
+    from .features import DeviceFeatureStore
+    if self._store is None or self._store.device != device:
+        self._store = DeviceFeatureStore.from_world(self.world, device, self.angle_feat_size)
+    return self._store
 
 
 def _device_input_feat(self, obs, device):
-    if self._store is None or self._store.device != device:
-        self._store = DeviceFeatureStore(self.world, device, self.angle_feat_size)
-    return self._store.input_feat(obs)
+    return _store(self, device).input_feat(obs)
 
 
 def _device_input_feat_steps(self, obs_steps, device):
-    if self._store is None or self._store.device != device:
-        self._store = DeviceFeatureStore(self.world, device, self.angle_feat_size)
-    return self._store.input_feat_steps(obs_steps)
+    return _store(self, device).input_feat_steps(obs_steps)
 
 
 SynthR2RBatch.device_input_feat = _device_input_feat

@@ -68,6 +68,18 @@ int dasa_gemm_f32(const dasa_gemm_desc* d, void* ws, int64_t ws_bytes, void* str
 int dasa_gemm_bf16(const dasa_gemm_desc* d, void* stream);
 /* y[i] = bf16(x[i]) (round to nearest even), n even; weight copies for dasa_gemm_bf16. */
 int dasa_f32_to_bf16(const float* x, uint16_t* y, int64_t n, void* stream);
+/* fp32 nn.Linear forward at fp32 accuracy on the bf16 matrix cores ("bf16x6"): every fp32 operand is
+ * split exactly into bf16 planes hi + mid + lo, and C = epilogue(sum of the six products hh, hm, mh, hl,
+ * lh, mm) with fp32 accumulation — the dropped terms are below 2^-25 of each product, under fp32's own
+ * rounding. A fp32 [M][lda] is split on load; B = the weight pre-split by dasa_f32_split3_bf16: pass
+ * the hi plane as d->B with d->ldb its row stride, the mid / lo planes `plane` elements further on.
+ * Only opA = 0, opB = 1; K % 32 == 0, lda % 4 == 0, ldb % 8 == 0, plane % 8 == 0, 16-B aligned A / B.
+ * Same fused epilogue as dasa_gemm_f32. Replaces the nn.Linear forwards (vilmodel.py BERT / LXRT
+ * projections and FFN, model.py decoder linears, agent_dg.py:1519 DGAdaChannel.a_fc). */
+int dasa_gemm_f32x6(const dasa_gemm_desc* d, int64_t plane, void* stream);
+/* x [rows][ldx] fp32 -> y = three bf16 planes [3][rows][cols] (hi, mid, lo; plane stride rows*cols),
+ * x = hi + mid + lo exactly for normal fp32 values; cols % 8 == 0, 16-B aligned x and y. */
+int dasa_f32_split3_bf16(const float* x, int64_t ldx, uint16_t* y, int32_t rows, int32_t cols, void* stream);
 
 /* ---- elementwise / reductions ---------------------------------------------------------------- */
 /* y = LayerNorm(dropout_p(x) + res) over N columns (eps), optionally saving mean/rstd [M] and the

@@ -413,12 +413,50 @@ def finetune(R):
     return out
 
 
+def io_readers(R):
+    """The reference's feature readers on tiny real-format files: utils.read_img_features on a TSV and
+    env.Depth_Features on a (viewpointIds, values) .npy pair; records the keys and a SHA-256 of every
+    decoded array. (base64.decodestring, which utils.py:306 calls, is base64.decodebytes' pre-3.9
+    alias; it is re-exposed for this run.)"""
+    import base64
+    import hashlib
+    import importlib.util
+    import tempfile
+    from dasa_amd.features import write_img_features
+    A = R.args
+    d = tempfile.mkdtemp(prefix="dasa_io_")
+    img, keys, vals = GI.io_tables()
+    tsv = os.path.join(d, "feats.tsv")
+    write_img_features(tsv, img)
+    if not hasattr(base64, "decodestring"):
+        base64.decodestring = base64.decodebytes
+    np.save(os.path.join(d, "ids.npy"), keys)
+    np.save(os.path.join(d, "vals.npy"), vals)
+    A.depth_index_file, A.depth_value_file = os.path.join(d, "ids.npy"), os.path.join(d, "vals.npy")
+    # env.py raises the csv field limit at import (env.py:19) before the reader runs, as in train.py
+    spec = importlib.util.spec_from_file_location("ref_env_io", os.path.join("/root/reference/r2r_src", "env.py"))
+    env_mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(env_mod)
+    depth = env_mod.depth_features.depth_map
+    A.mini, A.features = False, "imagenet"
+    feats = R.utils.read_img_features(tsv)
+    out = {"img/keys": np.array(sorted(feats)), "depth/keys": np.array(sorted(depth))}
+    for tag, tab in (("img", feats), ("depth", depth)):
+        for k in sorted(tab):
+            a = np.ascontiguousarray(tab[k])
+            out[f"{tag}/sha256/{k}"] = np.array(hashlib.sha256(a.tobytes()).hexdigest())
+            out[f"{tag}/shape/{k}"] = np.array(a.shape)
+            out[f"{tag}/dtype/{k}"] = np.array(str(a.dtype))
+    return out
+
+
 FIXTURES = {
     "ops": per_op,
     "cfg1_rollout": lambda R: {**rollouts(R), **checkpoint_schema(R)},
     "cfg4_finetune": finetune,
     "cfg2": cfg2,
     "cfg5": cfg5,
+    "io": io_readers,
 }
 
 

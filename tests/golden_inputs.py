@@ -101,3 +101,12 @@ def encoder_inputs():
     mask = seq == 0
     f = _u(rng, B, 36, 2176)
     return seq, mask, lengths, f
+
+
+def io_tables():
+    """Tiny real-format feature tables (utils.py:272-312 TSV, env.py:22-29 depth .npy pair)."""
+    rng = np.random.default_rng(160)
+    img = {f"scan{s}_vp{v:02d}": rng.random((36, 2048), dtype=np.float32) for s, v in (("A", 0), ("A", 1), ("B", 7))}
+    keys = np.array([["scanA", "vp00"], ["scanB", "vp07"], ["scanC", "vp03"]])
+    vals = rng.random((3, 36, 2048), dtype=np.float32)
+    return img, keys, vals

@@ -488,3 +488,54 @@ def test_bf16_mode_is_forward_only(dev):
     with pytest.raises(_lib.DasaError):
         with ops.bf16_matmul():
             pass
+
+
+def test_split3_bf16_exact(dev):
+    """dasa_f32_split3_bf16: x = hi + mid + lo exactly (fp64 sum) for normal fp32 values, each plane a
+    bf16 (RNE of the running residual)."""
+    from dasa_amd import ops
+    g = torch.Generator().manual_seed(11)
+    x = torch.cat([torch.randn(64, 96, generator=g) * s for s in (1e-3, 1.0, 1e3)], 0)
+    x[0, :8] = torch.tensor([0.0, -0.0, 1.0, -1.0, 3.4e37, -2.5e-30, 1 / 3, 65504.0])
+    pl = ops.split3_bf16(x.to(dev)).cpu()
+    hi, mid, lo = (pl[i].double() for i in range(3))
+    assert torch.equal(hi + mid + lo, x.double())
+    assert torch.equal(pl[0], x.to(torch.bfloat16))                       # hi = RNE(x)
+    assert torch.equal(pl[1], (x.double() - hi).float().to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("M,N,K", [(517, 200, 96), (1030, 384, 768), (256, 128, 32), (3, 24, 64)])
+def test_gemm_f32x6(dev, M, N, K):
+    """The bf16x6 fp32-emulated GEMM (dasa_gemm_f32x6), every tile form, ragged edges, the fused
+    epilogue (bias, act, aux gate, column scale, beta) and a strided A: its error against fp64 is at
+    most that of the native fp32 MFMA GEMM (+10%)."""
+    from dasa_amd import _lib, ops
+    g = torch.Generator().manual_seed(M + N + K)
+    Abuf = torch.randn(M, K + 8, generator=g)
+    A = Abuf[:, 4:4 + K]                                     # lda = K + 8, 16-B aligned start
+    W = torch.randn(N, K, generator=g) * 0.05
+    bias = torch.randn(N, generator=g) * 0.1
+    aux = torch.rand(M, N, generator=g)
+    cs = torch.rand(N, generator=g)
+    c0 = torch.randn(M, N, generator=g)
+    ref = (A.double() @ W.double().t() + bias.double())
+    Ad, Wd = Abuf.to(dev)[:, 4:4 + K], W.to(dev)
+    planes = ops.split3_bf16(Wd)
+    lib = _lib.lib()
+    out_nat = torch.empty(M, N, device=dev)
+    ops.gemm(Ad, Wd, out_nat, M=M, N=N, K=K, lda=K + 8, ldb=K, ldc=N, bias=bias.to(dev))
+    err_nat = (out_nat.cpu().double() - ref).abs().max().item()
+    try:
+        for cfg in range(6):
+            lib.dasa_gemm_force_config((1 << 21) + cfg)
+            y = torch.empty(M, N, device=dev)
+            ops.gemm_f32x6(Ad, planes, y, M=M, N=N, K=K, lda=K + 8, ldc=N, bias=bias.to(dev))
+            err = (y.cpu().double() - ref).abs().max().item()
+            assert err <= 1.1 * err_nat + 1e-7, (cfg, err, err_nat)
+            y2 = c0.clone().to(dev)
+            ops.gemm_f32x6(Ad, planes, y2, M=M, N=N, K=K, lda=K + 8, ldc=N, bias=bias.to(dev), act="sigmoid",
+                           aux=aux.to(dev), ld_aux=N, colscale=cs.to(dev), beta=0.5)
+            want = torch.sigmoid(ref) * aux.double() * cs.double() + 0.5 * c0.double()
+            assert (y2.cpu().double() - want).abs().max().item() < 1e-5, cfg
+    finally:
+        lib.dasa_gemm_force_config(-1)

@@ -6,6 +6,8 @@ import sys
 from collections import defaultdict
 
 FAMILY_PREFIX = [
+    ("gemm_x6", ("gemm_f32x6_nt_kernel",)),
+    ("gemm_bf16", ("gemm_bf16_nt_kernel",)),
     ("gemm", ("gemm_f32_kernel", "gemm_nt_k64_kernel", "gemm_nt_glds_kernel")),   # (split-K reduce apart)
     ("gemm_splitk_reduce", ("splitk_reduce_kernel",)),
     ("bilstm", ("bilstm_persist_fwd_kernel", "bilstm_step_fused_kernel", "bilstm_step_cell_kernel")),
