@@ -73,6 +73,8 @@ class DeviceFeatureStore:
         self.depth = torch.from_numpy(np.ascontiguousarray(depth, np.float32).reshape(P * V, F)).to(device)
         self.angles = torch.from_numpy(angle_table(angle_feat_size).reshape(V * V, -1)).to(device)
         self.index = {k: i for i, k in enumerate(keys)} if keys is not None else None
+        self._angle_cache = {}
+        self._cand_cache = {}
 
     @classmethod
     def from_world(cls, world, device, angle_feat_size=128):
@@ -85,6 +87,35 @@ class DeviceFeatureStore:
         rgb = np.stack([np.asarray(img_features[k], np.float32) for k in keys])
         depth = np.stack([np.asarray(depth_features[k], np.float32) for k in keys])
         return cls(rgb, depth, device, keys, angle_feat_size)
+
+    def _angle(self, heading, elevation):
+        """utils.angle_feature of the agent's own heading / elevation (memoised: a few hundred distinct
+        discretized values)."""
+        key = (heading, elevation)
+        a = self._angle_cache.get(key)
+        if a is None:
+            from .synth import angle_feature
+            if len(self._angle_cache) > 65536:
+                self._angle_cache.clear()
+            a = self._angle_cache[key] = angle_feature(heading, elevation, self.A)
+        return a
+
+    def _cand_arrays(self, cands):
+        """(pointIds int32 [n], relative-angle block [n, A]) of a candidate list. Lists of lightweight
+        candidates (an "angle" entry instead of feature arrays: envs that memoise their candidate lists,
+        like the synthetic one) are memoised per list object; R2RBatch's per-step lists are not kept."""
+        e = self._cand_cache.get(id(cands))
+        if e is not None and e[0] is cands:
+            return e[1], e[2]
+        A = self.A
+        pts = np.array([c["pointId"] for c in cands], np.int32)
+        angs = (np.stack([c["angle"] if "angle" in c else c["feature"][-A:] for c in cands]).astype(np.float32)
+                if cands else np.zeros((0, A), np.float32))
+        if cands and "angle" in cands[0]:
+            if len(self._cand_cache) > 65536:
+                self._cand_cache.clear()
+            self._cand_cache[id(cands)] = (cands, pts, angs)
+        return pts, angs
 
     def _row(self, ob):
         if "_vp_index" in ob:
@@ -104,7 +135,6 @@ class DeviceFeatureStore:
         as [B, C_t, F+A]. The END candidate row is zero (agent_dg.py:305-306). One gather per tensor."""
         import torch
         from . import ops
-        from .synth import angle_feature
         A, V = self.A, 36
         ia_v, ib_v, ia_c, ib_c, cangs, a_ts, cinfo = [], [], [], [], [], [], []
         rv = np.arange(V)
@@ -123,11 +153,13 @@ class DeviceFeatureStore:
             cang = np.zeros((B, C, A), np.float32)
             a_t = np.zeros((B, A), np.float32)
             for i, ob in enumerate(obs):
-                a_t[i] = angle_feature(ob["heading"], ob["elevation"], A)
-                for j, c in enumerate(ob["candidate"]):
-                    iac[i, j] = vp[i] * V + c["pointId"]
-                    ibc[i, j] = base + i * C + j
-                    cang[i, j] = c["angle"] if "angle" in c else c["feature"][-A:]
+                a_t[i] = self._angle(ob["heading"], ob["elevation"])
+                pts, angs = self._cand_arrays(ob["candidate"])
+                n = len(pts)
+                if n:
+                    iac[i, :n] = vp[i] * V + pts
+                    ibc[i, :n] = base + i * C + np.arange(n, dtype=np.int32)
+                    cang[i, :n] = angs
             base += B * C
             ia_c.append(iac.reshape(-1))
             ib_c.append(ibc.reshape(-1))

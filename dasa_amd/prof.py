@@ -8,6 +8,11 @@ import torch
 
 _REC = None
 
+# dense MFMA peaks other than fp32's 157.3 TFLOP/s (MI355X_MICROARCH.md: bf16 ~2.5 PF dense).
+# gemm_x6 (the bf16x6 fp32 emulation: six bf16 MFMAs per fp32 product) is priced in fp32-equivalent
+# FLOP/s against 2.5 PF / 6 = 416.7 TF, i.e. frac = its bf16 MFMA work / the bf16 dense peak.
+PEAK_TF = {"gemm_bf16": 2500.0, "gemm_x6": 2500.0 / 6}
+
 
 # family -> (roofline bound, kernel name prefix in rocprof)
 FAMILIES = {

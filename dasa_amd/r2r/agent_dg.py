@@ -322,6 +322,11 @@ class Seq2SeqAgent(BaseAgent):
             if action != -1:
                 sim = sims[idx]
                 select_candidate = perm_obs[i]["candidate"][action]
+                if hasattr(sim, "equiv_action"):     # the same action sequence, one call per agent
+                    assert select_candidate["viewpointId"] == sim.navigable_id(select_candidate["idx"])
+                    sim.equiv_action(select_candidate["pointId"], select_candidate["idx"],
+                                     traj[i]["path"] if traj is not None else None)
+                    continue
                 src_point = perm_obs[i]["viewIndex"]
                 trg_point = select_candidate["pointId"]
                 src_level = src_point // 12

@@ -265,6 +265,37 @@ class SynthSim:
             elevation = -ELEVATION_INC
         self._set_heading_elevation(self.heading + heading, self.elevation + elevation)
 
+    def equiv_action(self, trg_point, nav_idx, path=None):
+        """agent_dg.py:372-391 for one agent in a single call: turn up/down to the target's elevation
+        level, then right until the view index is trg_point, then move to navigable location nav_idx —
+        the state sequence of that many makeAction calls (each turn is one discretized step of
+        MatterSim.cpp:339-367: elevation +-30 deg within [-30, 30], heading +30 deg mod 360), with the
+        same (viewpoint, heading, elevation) appended to `path` after every action."""
+        rec = path.append if path is not None else None
+        vid = self.world.ids[self.vp]
+        hstep, lvl = self.view_index % 12, self.view_index // 12
+        trg_level, trg_step = trg_point // 12, trg_point % 12
+        while lvl != trg_level:
+            lvl += 1 if lvl < trg_level else -1
+            self.elevation = (lvl - 1) * ELEVATION_INC
+            self.step += 1
+            if rec:
+                rec((vid, self.heading, self.elevation))
+        while hstep != trg_step:
+            hstep = (hstep + 1) % 12
+            self.heading = hstep * HEADING_INC
+            self.step += 1
+            if rec:
+                rec((vid, self.heading, self.elevation))
+        self.view_index = lvl * 12 + hstep
+        nav = self.navigable()
+        if nav_idx < 0 or nav_idx >= len(nav):
+            raise ValueError("MatterSim: Invalid action index: %d" % nav_idx)
+        self.vp = nav[nav_idx]
+        self.step += 1
+        if rec:
+            rec((self.world.ids[self.vp], self.heading, self.elevation))
+
     def quick_state(self):
         """(viewpointId, heading, elevation, viewIndex) without building a SimState: the agent's turn
         loop polls the view index after every makeAction (agent_dg.py:376-386)."""
@@ -322,6 +353,7 @@ class SynthR2RBatch:
         self._store = None
         self._cand_cache = {}
         self._dist_cache = {}
+        self._navloc_cache = {}
 
     # -- episodes
     def _new_batch(self):
@@ -415,26 +447,34 @@ class SynthR2RBatch:
             d = self._dist_cache[sim.vp] = float(np.linalg.norm(w.pos[sim.vp] - self.virtual_goal))
         return d
 
+    def _nav_locs(self, v):
+        """The (shared, read-only) navigableLocations list of viewpoint v."""
+        locs = self._navloc_cache.get(v)
+        if locs is None:
+            w = self.world
+            nav = [v] + [u for (u, _, _, _) in w.neighbors[v]]
+            locs = self._navloc_cache[v] = [w.loc(u) for u in nav]
+        return locs
+
     def _get_obs(self):
         obs = []
         w = self.world
+        lazy = self.lazy_features
         for sim, item in zip(self.env.sims, self.batch):
-            st = sim.getState()
             v = sim.vp
-            base = st.viewIndex
+            base = sim.view_index
             ang = self.angle_feature[base]
-            lazy = self.lazy_features
             obs.append({
                 "instr_id": item["instr_id"],
                 "scan": "synth",
                 "viewpoint": w.ids[v],
                 "viewIndex": base,
-                "heading": st.heading,
-                "elevation": st.elevation,
+                "heading": sim.heading,
+                "elevation": sim.elevation,
                 "feature": None if lazy else np.concatenate((w.rgb[v], ang), -1),
                 "dfeature": None if lazy else np.concatenate((w.depth[v], ang), -1),
                 "candidate": self._candidates(v, base),
-                "navigableLocations": st.navigableLocations,
+                "navigableLocations": self._nav_locs(v),
                 "instructions": item["instructions"],
                 "teacher": self._teacher(sim, item),
                 "back_teacher": item["path"][0],
