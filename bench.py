@@ -136,12 +136,14 @@ def timed(fn, n, rank, world):
 
 
 def kernel_profile(agent, fn, shapes=0):
-    """One extra (untimed) step with HIP events around every libdasa_hip launch on its stream:
-    per-kernel-family device time + algorithmic FLOPs/bytes for the roofline."""
+    """One extra (untimed) iteration with HIP events around every libdasa_hip launch on its stream:
+    per-kernel-family device time + algorithmic FLOPs/bytes for the roofline. It runs the timed path's
+    kernels at the timed path's shapes, except that the hipGraph-captured VL stack is launched eagerly
+    (graph.py: events need per-launch boundaries). Returns (summary, decisions of that iteration)."""
     from dasa_amd import prof
     with prof.collect(shapes) as rec:
-        fn()
-    return rec.summary()
+        units = fn()
+    return rec.summary(), units
 
 
 def cpu_baseline(a):
@@ -229,9 +231,17 @@ def main():
         out["fwd_value"] = round(fu / fdt, 2)
         out["fwd_note"] = "eval/argmax rollout decisions/s (language stack computed once per batch: exact in eval)"
     if not a.no_profile:
-        summ = kernel_profile(agent, lambda: train_step(agent), a.shapes)
+        summ, punits = kernel_profile(agent, lambda: train_step(agent), a.shapes)
         if rank == 0:
             out.update(summ)
+            # whole-iteration roofline: the algorithmic FLOPs of every launch of one iteration (GEMMs,
+            # attention, recurrences; fp32-equivalent) per decision x the timed decisions/s, vs fp32 peak
+            fpd = summ["profiled_alg_flops"] / max(1, punits)
+            ach = fpd * value / 1e12
+            out["whole_step"] = {"alg_gflop_per_decision": round(fpd / 1e9, 3), "achieved": round(ach, 2),
+                                 "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TF, 4),
+                                 "note": "sum of per-launch algorithmic FLOPs of the profiled iteration / its "
+                                         "decisions x timed decisions/s"}
     if rank == 0 and world == 1 and not a.no_kbench:
         from dasa_amd import kbench
         out["hbm_kernels"] = kbench.hbm_kernels((a.batch, 256))

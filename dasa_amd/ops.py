@@ -124,7 +124,10 @@ def gemm(A, B, C, *, M, N, K, opA=0, opB=1, lda, ldb, ldc, bias=None, act=None, 
     L = _lib.lib()
     ws, ws_bytes = _gemm_ws(C.device, d)
     b = max(1, int(batch))
-    _call("dasa_gemm_f32", "gemm", L.dasa_gemm_f32, ctypes.byref(d), ws, ws_bytes, _stream(),
+    # M <= 64 (the per-step decoder / critic linears at B = 20) is weight streaming: its own family,
+    # judged against HBM (bytes = weight + activations), not the MFMA roof
+    fam = "gemm_skinny" if M <= 64 else "gemm"
+    _call("dasa_gemm_f32", fam, L.dasa_gemm_f32, ctypes.byref(d), ws, ws_bytes, _stream(),
           flops=2.0 * M * N * K * b, nbytes=4.0 * b * (M * K + K * N + M * N),
           detail=(int(M), int(N), int(K), b, int(opA), int(opB)))
 

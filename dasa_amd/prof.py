@@ -17,6 +17,7 @@ PEAK_TF = {"gemm_bf16": 2500.0, "gemm_x6": 2500.0 / 6}
 # family -> (roofline bound, kernel name prefix in rocprof)
 FAMILIES = {
     "gemm": ("mfma", "gemm_f32_kernel"),
+    "gemm_skinny": ("hbm", "gemm_f32_kernel (M <= 64; rocprof cannot split it from gemm)"),
     "gemm_bf16": ("mfma", "gemm_bf16_nt_kernel"),
     "gemm_x6": ("mfma", "gemm_f32x6_nt_kernel"),
     "bilstm": ("mfma", "bilstm_step_fused_kernel"),
@@ -81,9 +82,20 @@ class _Recorder:
                                "alg_bytes": fam[dom_name]["bytes"] / nl}}
         pmc = _pmc_traffic()
         if pmc is not None and dom_name in pmc["families"]:
-            roof["traffic"] = pmc["families"][dom_name]["hbm_bytes_per_launch"]
+            pf = pmc["families"][dom_name]
+            roof["traffic"] = pf.get("hbm_bytes", pf.get("hbm_bytes_per_launch"))
+            if pf.get("mfma_busy") is not None:
+                roof["mfma_busy"] = round(pf["mfma_busy"], 4)
             roof["traffic_source"] = pmc["file"] + ": " + pmc["source"]
-        out = {"roofline": roof, "kernels": kernels, "profiled_device_ms": round(total, 2)}
+        for name, ent in kernels.items():          # PMC MFMA-busy / HBM bytes per family where measured
+            pf = (pmc or {}).get("families", {}).get(name)
+            if pf:
+                if pf.get("mfma_busy") is not None:
+                    ent["mfma_busy"] = round(pf["mfma_busy"], 4)
+                if pf.get("hbm_bytes") is not None:
+                    ent["pmc_hbm_bytes_per_launch"] = round(pf["hbm_bytes"])
+        out = {"roofline": roof, "kernels": kernels, "profiled_device_ms": round(total, 2),
+               "profiled_alg_flops": sum(f["flops"] for f in fam.values())}
         if self.want_shapes:
             top = sorted(shapes.items(), key=lambda kv: -kv[1][1])[:self.want_shapes]
             out["shapes"] = [{"kernel": k[0], "shape": list(k[1:]), "launches": v[0], "ms": round(v[1], 3),
@@ -97,13 +109,18 @@ def _pmc_traffic():
     (tools/pmc_traffic.py -> profiles/pmc_traffic.json), or None."""
     import json
     import os
-    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_traffic.json")
+    rel = PMC_FILE
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), rel)
     if not os.path.exists(path):
         return None
     with open(path) as f:
         d = json.load(f)
-    d["file"] = "profiles/pmc_traffic.json"
+    d["file"] = rel
     return d
+
+
+# the committed PMC summary the roofline's `traffic` / `mfma_busy` come from (tools/pmc_summary.py)
+PMC_FILE = "profiles/r02/pmc.json"
 
 
 def active():

@@ -541,3 +541,23 @@ def test_gemm_f32x6(dev, M, N, K):
             assert (y2.cpu().double() - want).abs().max().item() < 1e-5, cfg
     finally:
         lib.dasa_gemm_force_config(-1)
+
+
+@pytest.mark.parametrize("M,N,K", [(20, 2176, 1024), (20, 4096, 2240), (64, 1000, 512), (1, 1, 32), (7, 130, 96),
+                                   (32, 3072, 3072)])
+def test_gemm_skinny(dev, M, N, K):
+    """Skinny NT GEMMs (the per-step decoder / critic linears at B <= 64: split-K + reduce), the fused
+    epilogue and a strided A, against fp64."""
+    from dasa_amd import ops
+    g = torch.Generator().manual_seed(M * 31 + N + K)
+    Abuf = _rand(M, K + 4, g=g)
+    W, b = _rand(N, K, g=g, scale=0.05), _rand(N, g=g)
+    aux, cs, c0 = _rand(M, N, g=g), _rand(N, g=g), _rand(M, N, g=g)
+    z = Abuf[:, :K].double() @ W.double().t() + b.double()
+    y = ops.linear(Abuf.to(dev)[:, :K], W.to(dev), b.to(dev)).cpu()
+    assert (y.double() - z).abs().max().item() < 2e-6 * max(1.0, z.abs().max().item()) * math.sqrt(K / 256)
+    out = c0.clone().to(dev)
+    ops.linear(Abuf.to(dev)[:, :K], W.to(dev), b.to(dev), act="tanh", aux=aux.to(dev), colscale=cs.to(dev), out=out,
+               beta=0.25)
+    want = torch.tanh(z) * aux.double() * cs.double() + 0.25 * c0.double()
+    assert (out.cpu().double() - want).abs().max().item() < 1e-5

@@ -42,6 +42,10 @@ def main(stats_csv, bench_json=None):
     if bench_json:
         line = [ln for ln in open(bench_json).read().splitlines() if ln.startswith('{"metric"')][-1]
         bench = json.loads(line).get("kernels", {})
+        if "gemm_skinny" in bench and "gemm" in bench:   # rocprof cannot tell them apart: compare merged
+            g, k = bench["gemm"], bench["gemm_skinny"]
+            n = g["launches"] + k["launches"]
+            bench = dict(bench, gemm=dict(g, avg_launch_us=round(1e3 * (g["device_ms"] + k["device_ms"]) / n, 2)))
     print(f"{'family':<34}{'calls':>8}{'total ms':>11}{'share':>8}{'avg us':>10}{'bench avg us':>14}")
     for k, (n, ns) in sorted(fam.items(), key=lambda kv: -kv[1][1])[:25]:
         b = bench.get(k, {}).get("avg_launch_us", "")
