@@ -47,6 +47,8 @@ def parse():
     p.add_argument("--no-kbench", action="store_true",
                    help="skip the isolated HBM-kernel table (dasa_amd.kbench at B=20 and B=256)")
     p.add_argument("--shapes", type=int, default=0, help="add the top-N GEMM shapes by device time")
+    p.add_argument("--profile-only", action="store_true",
+                   help="warm-up + the HIP-event profile iteration only (for rocprofv3 runs of that iteration)")
     p.add_argument("--fast-exit", action="store_true",
                    help="os._exit after the JSON line (skips interpreter teardown; used under rocprofv3)")
     p.add_argument("--no-cfg5", action="store_true", help="skip the BASELINE configs[4] (B=256, vl=6, bf16) leg")
@@ -212,6 +214,10 @@ def main():
     agent, env = build_agent(a, rank, world)
     for _ in range(a.warmup):
         train_step(agent)
+    if a.profile_only:
+        summ, punits = kernel_profile(agent, lambda: train_step(agent), a.shapes)
+        print(json.dumps({"profile_only": True, "decisions": punits, **summ}), flush=True)
+        return
     units, dt = timed(lambda: train_step(agent), a.steps, rank, world)
     value = units / dt
     out = {

@@ -40,7 +40,7 @@ def main(stats_csv, bench_json=None):
         total += float(r["TotalDurationNs"])
     bench = {}
     if bench_json:
-        line = [ln for ln in open(bench_json).read().splitlines() if ln.startswith('{"metric"')][-1]
+        line = [ln for ln in open(bench_json).read().splitlines() if ln.startswith('{"metric"') or ln.startswith('{"profile_only"')][-1]
         bench = json.loads(line).get("kernels", {})
         if "gemm_skinny" in bench and "gemm" in bench:   # rocprof cannot tell them apart: compare merged
             g, k = bench["gemm"], bench["gemm_skinny"]
