@@ -450,6 +450,77 @@ def io_readers(R):
     return out
 
 
+EVAL_SCANS = ["17DRP5sb8fy", "8194nk5LbLH", "GdvgFV5R1Z5"]
+
+
+def eval_score(R):
+    """Evaluation.score (eval.py:74-108) of the reference on its own connectivity graphs (three scans,
+    tests/golden/connectivity holds copies) for synthetic R2R items and synthetic trajectories
+    (random walks on the graph, some along the shortest path); utils.load_datasets (which reads the
+    absent R2R json) is replaced by the item list. Inputs and outputs are both recorded."""
+    import importlib.util
+    import json
+    import random
+    import networkx as nx
+    R.args.depth_index_file, R.args.depth_value_file = _tiny_depth_files()
+    if "env" not in sys.modules or not hasattr(sys.modules["env"], "R2RBatch"):
+        spec = importlib.util.spec_from_file_location("env", "/root/reference/r2r_src/env.py")
+        m = importlib.util.module_from_spec(spec)
+        sys.modules["env"] = m
+        spec.loader.exec_module(m)
+    import eval as ref_eval
+    cwd = os.getcwd()
+    os.chdir("/root/reference")          # load_nav_graphs opens connectivity/<scan>_connectivity.json
+    try:
+        graphs = R.utils.load_nav_graphs(EVAL_SCANS)
+    finally:
+        os.chdir(cwd)
+    rng = random.Random(17)
+    items, results = [], []
+    pid = 1000
+    for scan in EVAL_SCANS:
+        G = graphs[scan]
+        nodes = sorted(G.nodes())
+        for _ in range(5):
+            a, b = rng.sample(nodes, 2)
+            path = nx.shortest_path(G, a, b, weight="weight")
+            items.append({"path_id": pid, "scan": scan, "path": path, "heading": 0.0,
+                          "instructions": ["go", "walk there", "stop"]})
+            for i in range(3):
+                traj = [(a, rng.uniform(0, 6.28), 0.0)]
+                if i == 0:
+                    traj += [(v, rng.uniform(0, 6.28), 0.0) for v in path[1:]]      # the exact path
+                else:
+                    cur = a
+                    for _ in range(rng.randint(0, 7)):
+                        cur = rng.choice(sorted(G.neighbors(cur)))
+                        for _ in range(rng.randint(0, 2)):                          # turns in place
+                            traj.append((cur, rng.uniform(0, 6.28), 0.0))
+                        traj.append((cur, rng.uniform(0, 6.28), 0.0))
+                results.append({"instr_id": "%d_%d" % (pid, i), "trajectory": traj})
+            pid += 1
+    ref_eval.load_datasets = lambda splits: items
+    cwd = os.getcwd()
+    os.chdir("/root/reference")
+    try:
+        ev = ref_eval.Evaluation(["val_seen"], EVAL_SCANS, None)
+    finally:
+        os.chdir(cwd)
+    summary, scores = ev.score(results)
+    return {"eval/items": np.array(json.dumps(items)), "eval/results": np.array(json.dumps(results)),
+            "eval/summary": np.array(json.dumps({k: float(v) for k, v in summary.items()}, sort_keys=True)),
+            "eval/scores": np.array(json.dumps({k: [float(x) for x in v] for k, v in scores.items()}, sort_keys=True))}
+
+
+def _tiny_depth_files():
+    import tempfile
+    d = tempfile.mkdtemp(prefix="dasa_dep_")
+    _, keys, vals = GI.io_tables()
+    np.save(os.path.join(d, "ids.npy"), keys)
+    np.save(os.path.join(d, "vals.npy"), vals)
+    return os.path.join(d, "ids.npy"), os.path.join(d, "vals.npy")
+
+
 FIXTURES = {
     "ops": per_op,
     "cfg1_rollout": lambda R: {**rollouts(R), **checkpoint_schema(R)},
@@ -457,6 +528,7 @@ FIXTURES = {
     "cfg2": cfg2,
     "cfg5": cfg5,
     "io": io_readers,
+    "eval": eval_score,
 }
 
 
