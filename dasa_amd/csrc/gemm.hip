@@ -1057,7 +1057,7 @@ __device__ __forceinline__ void split3_quad(const float4& x, const float4& y, ui
   split3_pair(y.z, y.w, h.w, m.w, l.w);
 }
 
-template <int BM, int BN, int WAVES_M, int WAVES_N, bool SEP>
+template <int BM, int BN, int WAVES_M, int WAVES_N, bool SEP, int PF = 1>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_f32x6_nt_kernel(GemmP p, long plane) {
   constexpr int NT = 64 * WAVES_M * WAVES_N;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N, TM = WM / 16, TN = WN / 16;
@@ -1143,7 +1143,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_f32x6_nt_kernel(G
         for (int pl = 0; pl < 3; ++pl) S[3 * PA + pl * PB + q * BN + row] = w[pl][i];
       }
     }
-  } stg;
+  } stg, stg2;
 
   auto compute = [&](const uint4* S) {
     const int q = lane >> 4;
@@ -1174,13 +1174,32 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_f32x6_nt_kernel(G
 
   const int nk = p.K / 32;
   stg.load(p, A, W, plane, m0, n0, 0, tid);
-  stg.store(smem, tid);
-  __syncthreads();
-  for (int t = 0; t < nk; ++t) {
-    stg.load(p, A, W, plane, m0, n0, 32 * min(t + 1, nk - 1), tid);   // unconditional (clamped re-read)
-    compute(smem + (t & 1) * STAGE);
-    stg.store(smem + ((t + 1) & 1) * STAGE, tid);
+  if (PF == 1) {
+    stg.store(smem, tid);
     __syncthreads();
+    for (int t = 0; t < nk; ++t) {
+      stg.load(p, A, W, plane, m0, n0, 32 * min(t + 1, nk - 1), tid);   // unconditional (clamped re-read)
+      compute(smem + (t & 1) * STAGE);
+      stg.store(smem + ((t + 1) & 1) * STAGE, tid);
+      __syncthreads();
+    }
+  } else {
+    // two register stages: the loads of tile t + 2 are issued before tile t's MFMAs, so each tile's
+    // global reads have two K steps of compute to land in (the L2 / MALL latency under full load)
+    stg2.load(p, A, W, plane, m0, n0, 32 * min(1, nk - 1), tid);
+    stg.store(smem, tid);
+    __syncthreads();
+    for (int t = 0; t < nk; t += 2) {
+      stg.load(p, A, W, plane, m0, n0, 32 * min(t + 2, nk - 1), tid);
+      compute(smem);
+      stg2.store(smem + STAGE, tid);
+      __syncthreads();
+      if (t + 1 >= nk) break;
+      stg2.load(p, A, W, plane, m0, n0, 32 * min(t + 3, nk - 1), tid);
+      compute(smem + STAGE);
+      stg.store(smem, tid);
+      __syncthreads();
+    }
   }
   if (SEP) {
 #pragma unroll
@@ -1469,11 +1488,13 @@ extern "C" int dasa_gemm_f32x6(const dasa_gemm_desc* d, int64_t plane, void* str
   p.aux = d->aux; p.ld_aux = d->ld_aux; p.sAux = d->strideAux;
   p.colscale = d->colscale; p.alpha = d->alpha; p.beta = d->beta;
   p.ws = nullptr;
-  // 256x128 tiles with the separate small-term accumulator: fastest form on every shape the plan
-  // routes here (profiles/r02/gemm_x6_sweep_a.txt); the others stay for sweeps
-  int cfg = 3;
+  // 128x128 tiles, separate small-term accumulator, two register stages of prefetch (form 8): the
+  // fastest accurate form on every shape the plan routes here (profiles/r02/gemm_x6_sweep_b.txt:
+  // 136-178 fp32-equivalent TFLOP/s on the 1600- to 20480-row language / LXRT / LSTM shapes); the
+  // others stay for sweeps
+  int cfg = 8;
   if (g_force_cfg >= kX6Force) cfg = (g_force_cfg - kX6Force) % 16;
-  const int bm = (cfg == 1 || cfg == 3) ? 256 : (cfg == 4 || cfg == 5) ? 64 : 128;
+  const int bm = (cfg == 1 || cfg == 3 || cfg == 6 || cfg == 7) ? 256 : (cfg == 4 || cfg == 5) ? 64 : 128;
   const int bn = cfg == 5 ? 64 : 128;
   p.group_m = cdiv(M, bm) >= 8 ? 4 : 1;
   dim3 grid((unsigned)cdiv(N, bn), (unsigned)cdiv(M, bm), batch);
@@ -1484,6 +1505,9 @@ extern "C" int dasa_gemm_f32x6(const dasa_gemm_desc* d, int64_t plane, void* str
     case 3: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<256, 128, 4, 2, true>), grid, dim3(512), 0, st, p, (long)plane); break;
     case 4: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<64, 128, 2, 2, true>), grid, dim3(256), 0, st, p, (long)plane); break;
     case 5: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<64, 64, 2, 2, true>), grid, dim3(256), 0, st, p, (long)plane); break;
+    case 6: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<256, 128, 4, 2, false, 2>), grid, dim3(512), 0, st, p, (long)plane); break;
+    case 7: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<256, 128, 4, 2, true, 2>), grid, dim3(512), 0, st, p, (long)plane); break;
+    case 8: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true, 2>), grid, dim3(512), 0, st, p, (long)plane); break;
     default: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true>), grid, dim3(512), 0, st, p, (long)plane); break;
   }
   DASA_CHECK_LAUNCH();

@@ -241,14 +241,14 @@ def _x6_weight(W):
 
 
 def _emu_ok(M, N, K, lda, x):
-    """Plan rule (profiles/r02/gemm_x6_sweep_a.txt): the 256x128-tile bf16x6 kernel beats the native fp32
-    MFMA kernels when its tiles fill the 256 CUs in whole rounds (>= 200 tiles, >= 85% of the last
-    round busy), e.g. the 12800-row language FFN / QKV and 1600 x 4096 shapes; elsewhere native fp32."""
+    """Plan rule (profiles/r02/gemm_x6_sweep_b.txt): the 128x128-tile bf16x6 kernel beats the native fp32
+    MFMA kernels (by 1.1-1.5x) once it has >= 128 output tiles — the 12800-row language stack, the
+    1600-row LSTM input projections and LXRT language branch, the 720 x 3072 vision FFN; the smaller
+    LXRT GEMMs (36-78 tiles) stay on the native fp32 kernels."""
     if not (_EMU["on"] and M >= _EMU["min_rows"] and K % 32 == 0 and N % 8 == 0 and lda % 4 == 0
             and x.data_ptr() % 16 == 0):
         return False
-    tiles = -(-M // 256) * -(-N // 128)
-    return tiles >= 200 and tiles / (-(-tiles // 256) * 256) >= 0.85
+    return -(-M // 128) * -(-N // 128) >= 128
 
 
 def gemm_f32x6(x, planes, out, *, M, N, K, lda, ldc, bias=None, act=None, aux=None, ld_aux=0, colscale=None,
