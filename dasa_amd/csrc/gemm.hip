@@ -1143,7 +1143,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_f32x6_nt_kernel(G
         for (int pl = 0; pl < 3; ++pl) S[3 * PA + pl * PB + q * BN + row] = w[pl][i];
       }
     }
-  } stg, stg2;
+  } stg, stg2, stg3;
 
   auto compute = [&](const uint4* S) {
     const int q = lane >> 4;
@@ -1179,6 +1179,28 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_f32x6_nt_kernel(G
     __syncthreads();
     for (int t = 0; t < nk; ++t) {
       stg.load(p, A, W, plane, m0, n0, 32 * min(t + 1, nk - 1), tid);   // unconditional (clamped re-read)
+      compute(smem + (t & 1) * STAGE);
+      stg.store(smem + ((t + 1) & 1) * STAGE, tid);
+      __syncthreads();
+    }
+  } else if (PF == 3) {
+    // three register stages: tile t + 3's loads issued before tile t's MFMAs
+    stg2.load(p, A, W, plane, m0, n0, 32 * min(1, nk - 1), tid);
+    stg3.load(p, A, W, plane, m0, n0, 32 * min(2, nk - 1), tid);
+    stg.store(smem, tid);
+    __syncthreads();
+    for (int t = 0; t < nk; t += 3) {
+      stg.load(p, A, W, plane, m0, n0, 32 * min(t + 3, nk - 1), tid);
+      compute(smem + (t & 1) * STAGE);
+      stg2.store(smem + ((t + 1) & 1) * STAGE, tid);
+      __syncthreads();
+      if (t + 1 >= nk) break;
+      stg2.load(p, A, W, plane, m0, n0, 32 * min(t + 4, nk - 1), tid);
+      compute(smem + ((t + 1) & 1) * STAGE);
+      stg3.store(smem + (t & 1) * STAGE, tid);
+      __syncthreads();
+      if (t + 2 >= nk) break;
+      stg3.load(p, A, W, plane, m0, n0, 32 * min(t + 5, nk - 1), tid);
       compute(smem + (t & 1) * STAGE);
       stg.store(smem + ((t + 1) & 1) * STAGE, tid);
       __syncthreads();
@@ -1508,6 +1530,7 @@ extern "C" int dasa_gemm_f32x6(const dasa_gemm_desc* d, int64_t plane, void* str
     case 6: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<256, 128, 4, 2, false, 2>), grid, dim3(512), 0, st, p, (long)plane); break;
     case 7: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<256, 128, 4, 2, true, 2>), grid, dim3(512), 0, st, p, (long)plane); break;
     case 8: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true, 2>), grid, dim3(512), 0, st, p, (long)plane); break;
+    case 9: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true, 3>), grid, dim3(512), 0, st, p, (long)plane); break;
     default: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true>), grid, dim3(512), 0, st, p, (long)plane); break;
   }
   DASA_CHECK_LAUNCH();

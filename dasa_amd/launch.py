@@ -5,10 +5,10 @@
 train.py does `from param import args`, `from agent_dg import Seq2SeqAgent`, and its helpers import
 `model`, `vilmodel`, `r2rmodel`. This launcher binds those module names to dasa_amd.r2r (whose
 classes, signatures, state_dict keys and args flags match the reference), parses the command line
-into the shared `args` like param.py does at import, and executes train.py as __main__. Everything
-else (env, utils, speaker, eval, tokenizers, MatterSim) is the reference's own code. Names the
-policy modules do not define (e.g. SpeakerEncoder/SpeakerDecoder, the alternative decoders) resolve
-to the reference's definitions, loaded under a private module name.
+into the shared `args` like param.py does at import, and executes train.py as __main__. The speaker
+(back-translation, `speaker` module) is ours as well. Everything else (env, utils, eval, tokenizers,
+MatterSim) is the reference's own code. Names the policy modules do not define (e.g. the alternative
+decoders) resolve to the reference's definitions, loaded under a private module name.
 """
 import importlib.util
 import os
@@ -55,8 +55,9 @@ def main(argv=None):
     from dasa_amd.r2r import param
     param.parse(sys.argv[1:], make_dirs=True)
     sys.modules["param"] = param
-    from dasa_amd.r2r import agent_dg, model, r2rmodel, vilmodel
-    for name, ours in (("model", model), ("vilmodel", vilmodel), ("r2rmodel", r2rmodel), ("agent_dg", agent_dg)):
+    from dasa_amd.r2r import agent_dg, model, r2rmodel, speaker, vilmodel
+    for name, ours in (("model", model), ("vilmodel", vilmodel), ("r2rmodel", r2rmodel), ("agent_dg", agent_dg),
+                       ("speaker", speaker)):
         sys.modules[name] = _proxy(ours, ref_dir, name)
     runpy.run_path(script, run_name="__main__")
     return 0

@@ -168,3 +168,97 @@ def adaptive_instance_normalization(content_feat, style_feat, out=None):
     differentiable in content and style (dasa_adain_musigma_bwd)."""
     assert content_feat.size() == style_feat.size()
     return DF.adain_musigma(content_feat, style_feat, out=out)
+
+
+# ----------------------------------------------------------------------------- speaker (back-translation)
+def _bilstm(lstm, x):
+    """A single-layer bidirectional nn.LSTM over the full padded length (no packing: speaker.py feeds
+    padded batches, model.py:1010 / 1025) on the persistent recurrence kernel."""
+    B, T, _ = x.shape
+    lens = torch.full((B,), T, dtype=torch.int32, device=x.device)
+    out, _, _ = DF.BiLSTMFn.apply(x.contiguous(), lens, lstm.weight_ih_l0, lstm.weight_hh_l0, lstm.bias_ih_l0,
+                                  lstm.bias_hh_l0, lstm.weight_ih_l0_reverse, lstm.weight_hh_l0_reverse,
+                                  lstm.bias_ih_l0_reverse, lstm.bias_hh_l0_reverse)
+    return out
+
+
+class SpeakerEncoder(nn.Module):
+    """model.py:984-1032: bi-LSTM over the trajectory's action (candidate) features, SoftDot attention of
+    each step over its 36-view panorama, a second bi-LSTM. Inference path (Speaker.infer_batch);
+    training the speaker is outside the policy hot path."""
+
+    def __init__(self, feature_size, hidden_size, dropout_ratio, bidirectional):
+        super().__init__()
+        self.num_directions = 2 if bidirectional else 1
+        self.hidden_size = hidden_size
+        self.num_layers = 1
+        self.feature_size = feature_size
+        if not bidirectional:
+            raise NotImplementedError("the DASA speaker is bidirectional (param.py --bidir default True)")
+        self.lstm = nn.LSTM(feature_size, self.hidden_size // self.num_directions, self.num_layers, batch_first=True,
+                            bidirectional=bidirectional)
+        self.drop = nn.Dropout(p=dropout_ratio)
+        self.drop3 = nn.Dropout(p=args.featdropout)
+        self.attention_layer = SoftDotAttention(self.hidden_size, feature_size)
+        self.post_lstm = nn.LSTM(self.hidden_size, self.hidden_size // self.num_directions, self.num_layers,
+                                 batch_first=True, bidirectional=bidirectional)
+
+    def forward(self, action_embeds, feature, lengths, already_dropfeat=False):
+        """action_embeds [B, T, F+A], feature [B, T, 36, F+A] -> ctx [B, T, hidden]."""
+        training = self.training
+        angle = args.angle_feat_size
+        x = action_embeds
+        if not already_dropfeat:
+            x = DF.feat_drop(x, self.drop3.p, training, angle)
+        ctx = DF.dropout(_bilstm(self.lstm, x), self.drop.p, training)
+        B, T, _ = ctx.shape
+        if not already_dropfeat:
+            feature = DF.feat_drop(feature, self.drop3.p, training, angle)
+        x, _ = self.attention_layer(ctx.contiguous().view(-1, self.hidden_size),
+                                    feature.contiguous().view(B * T, -1, self.feature_size))
+        x = DF.dropout(x.view(B, T, -1), self.drop.p, training)
+        return DF.dropout(_bilstm(self.post_lstm, x), self.drop.p, training)
+
+
+class SpeakerDecoder(nn.Module):
+    """model.py:1034-1080: word embedding -> LSTM -> masked SoftDot attention over the encoder context ->
+    vocabulary projection. Inference path (no autograd: infer_batch runs it under no_grad)."""
+
+    def __init__(self, vocab_size, embedding_size, padding_idx, hidden_size, dropout_ratio):
+        super().__init__()
+        self.hidden_size = hidden_size
+        self.embedding = torch.nn.Embedding(vocab_size, embedding_size, padding_idx)
+        self.lstm = nn.LSTM(embedding_size, hidden_size, batch_first=True)
+        self.drop = nn.Dropout(dropout_ratio)
+        self.attention_layer = SoftDotAttention(hidden_size, hidden_size)
+        self.projection = nn.Linear(hidden_size, vocab_size)
+        self.baseline_projection = nn.Sequential(nn.Linear(hidden_size, 128), nn.ReLU(), nn.Dropout(dropout_ratio),
+                                                 nn.Linear(128, 1))
+
+    def forward(self, words, ctx, ctx_mask, h0, c0):
+        """words [B, L] int64, ctx [B, T, H], ctx_mask [B, T] bool, h0 / c0 [1, B, H] ->
+        (logit [B, L, V], h1 [1, B, H], c1 [1, B, H])."""
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            raise NotImplementedError("SpeakerDecoder runs the inference path only (call it under torch.no_grad())")
+        B, L = words.shape
+        H, E = self.hidden_size, self.embedding.weight.shape[1]
+        training = self.training
+        emb = torch.empty(B * L, E, dtype=torch.float32, device=ctx.device)
+        ops.gather_rows(self.embedding.weight, words.reshape(-1).to(torch.int32), None, None, emb)
+        emb = DF.dropout(emb.view(B, L, E), self.drop.p, training)
+        lw = self.lstm
+        h, c = h0.reshape(B, H).contiguous(), c0.reshape(B, H).contiguous()
+        outs = []
+        for t in range(L):                       # nn.LSTM over the L words (L = 1 while decoding)
+            gates = ops.linear(emb[:, t], lw.weight_ih_l0, lw.bias_ih_l0)
+            ops.linear(h, lw.weight_hh_l0, lw.bias_hh_l0, out=gates, beta=1.0)
+            h, c, _ = ops.lstm_cell_fwd(gates, c)
+            outs.append(h)
+        x = outs[0].unsqueeze(1) if L == 1 else torch.stack(outs, 1)
+        x = DF.dropout(x, self.drop.p, training)
+        ctx_x = ctx if L == 1 else ctx.repeat_interleave(L, 0)
+        mask_x = ctx_mask if L == 1 else ctx_mask.repeat_interleave(L, 0)
+        x, _ = self.attention_layer(x.reshape(B * L, H), ctx_x.contiguous(), mask_x)
+        x = DF.dropout(x.view(B, L, H), self.drop.p, training)
+        logit = ops.linear(x, self.projection.weight, self.projection.bias)
+        return logit, h.unsqueeze(0), c.unsqueeze(0)

@@ -521,6 +521,57 @@ def _tiny_depth_files():
     return os.path.join(d, "ids.npy"), os.path.join(d, "vals.npy")
 
 
+def speaker(R):
+    """Speaker.infer_batch (speaker.py:265-350) of the reference: SpeakerEncoder over the teacher path's
+    candidate / panorama features, SpeakerDecoder argmax decoding. The reference's own Tokenizer on its
+    train_vocab.txt (a copy is tests/golden/train_vocab.txt). numpy 2 dropped the np.bool alias that
+    speaker.py:308 uses; it is re-exposed for this run. Records ctx, per-step logits, words, lengths."""
+    import contextlib
+    import importlib
+    import io
+    A = R.args
+    cfg = GI.SPEAKER
+    if not hasattr(np, "bool"):
+        np.bool = bool
+    A.maxDecode, A.batchSize, A.views = cfg["max_decode"], cfg["batch"], 36
+    with contextlib.redirect_stdout(io.StringIO()):
+        tok = R.utils.Tokenizer(vocab=R.utils.read_vocab(os.path.join(ROOT, "tests", "golden", "train_vocab.txt")),
+                                encoding_length=A.maxInput)
+    world = SynthWorld(n_viewpoints=cfg["viewpoints"], feat_seed=0, graph_seed=cfg["graph_seed"])
+    env = SynthR2RBatch(world, cfg["batch"], seed=cfg["env_seed"], mode="goal", instr_len=80, variable_len=True)
+    listener = make_agent(R, env, 5)
+    spk_mod = importlib.import_module("speaker")
+    with contextlib.redirect_stdout(io.StringIO()):
+        spk = spk_mod.Speaker(env, listener, tok)
+    init_params(spk.encoder, cfg["seed_enc"])
+    init_params(spk.decoder, cfg["seed_dec"])
+    rec = {"ctx": None, "logits": [], "h": []}
+    enc_fwd, dec_fwd = spk.encoder.forward, spk.decoder.forward
+
+    def enc_wrap(*a, **k):
+        r = enc_fwd(*a, **k)
+        rec["ctx"] = f32(r)
+        return r
+
+    def dec_wrap(*a, **k):
+        r = dec_fwd(*a, **k)
+        rec["logits"].append(f32(r[0]))
+        rec["h"].append(f32(r[1]))
+        return r
+    spk.encoder.forward, spk.decoder.forward = enc_wrap, dec_wrap
+    env.reset()
+    with torch.no_grad():
+        insts = spk.infer_batch()
+    out = {"spk/ctx": rec["ctx"], "spk/insts": np.asarray(insts, np.int64), "spk/steps": np.array(len(rec["logits"])),
+           "spk/schema_encoder": np.array(__import__("json").dumps({k: list(v.shape) for k, v in spk.encoder.state_dict().items()})),
+           "spk/schema_decoder": np.array(__import__("json").dumps({k: list(v.shape) for k, v in spk.decoder.state_dict().items()})),
+           "spk/vocab_size": np.array(tok.vocab_size())}
+    for t, (lg, h) in enumerate(zip(rec["logits"], rec["h"])):
+        out[f"spk/logit/{t}"] = lg
+        out[f"spk/h/{t}"] = h
+    return out
+
+
 FIXTURES = {
     "ops": per_op,
     "cfg1_rollout": lambda R: {**rollouts(R), **checkpoint_schema(R)},
@@ -529,6 +580,7 @@ FIXTURES = {
     "cfg5": cfg5,
     "io": io_readers,
     "eval": eval_score,
+    "speaker": speaker,
 }
 
 

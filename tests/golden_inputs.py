@@ -110,3 +110,7 @@ def io_tables():
     keys = np.array([["scanA", "vp00"], ["scanB", "vp07"], ["scanC", "vp03"]])
     vals = rng.random((3, 36, 2048), dtype=np.float32)
     return img, keys, vals
+
+# Speaker back-translation (speaker.py:265-350) at the auglistener batch: B=6 goal episodes (the teacher
+# path ends), weights seeded, eval mode, argmax decoding, maxDecode 12.
+SPEAKER = dict(batch=6, viewpoints=16, graph_seed=3, env_seed=41, max_decode=12, seed_enc=61, seed_dec=62)

@@ -109,17 +109,19 @@ def test_oracle_sort_and_masks():
 
 def test_dropin_launcher_binds_reference_module_names(tmp_path, monkeypatch):
     """dasa_amd.launch runs an unchanged train.py with param/agent_dg/model bound to dasa_amd.r2r and
-    reference-only names (e.g. SpeakerEncoder) falling back to the reference file."""
+    reference-only names (e.g. an alternative decoder) falling back to the reference file."""
     import subprocess
     import sys
-    (tmp_path / "model.py").write_text("SpeakerEncoder = 'reference-speaker-encoder'\n")
+    (tmp_path / "model.py").write_text("RefOnlyDecoder = 'reference-only-decoder'\n")
     (tmp_path / "train.py").write_text(
         "from param import args\n"
-        "import model, agent_dg\n"
+        "import model, agent_dg, speaker\n"
         "assert args.d_vl_layers == 3 and args.use_shift, args.d_vl_layers\n"
         "assert agent_dg.Seq2SeqAgent.__module__.startswith('dasa_amd.r2r')\n"
         "assert model.BAttnDecoderLSTM.__module__ == 'dasa_amd.r2r.model'\n"
-        "assert model.SpeakerEncoder == 'reference-speaker-encoder'\n"
+        "assert model.RefOnlyDecoder == 'reference-only-decoder'\n"
+        "assert model.SpeakerEncoder.__module__ == 'dasa_amd.r2r.model'\n"
+        "assert speaker.Speaker.__module__ == 'dasa_amd.r2r.speaker'\n"
         "print('DROPIN-OK')\n")
     from dasa_amd.r2r import param
     r = subprocess.run([sys.executable, "-m", "dasa_amd.launch", str(tmp_path / "train.py")] + param.README_TRAIN_FLAGS,

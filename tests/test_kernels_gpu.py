@@ -526,7 +526,7 @@ def test_gemm_f32x6(dev, M, N, K):
     ops.gemm(Ad, Wd, out_nat, M=M, N=N, K=K, lda=K + 8, ldb=K, ldc=N, bias=bias.to(dev))
     err_nat = (out_nat.cpu().double() - ref).abs().max().item()
     try:
-        for cfg in range(9):
+        for cfg in range(10):
             lib.dasa_gemm_force_config((1 << 21) + cfg)
             y = torch.empty(M, N, device=dev)
             ops.gemm_f32x6(Ad, planes, y, M=M, N=N, K=K, lda=K + 8, ldc=N, bias=bias.to(dev))
