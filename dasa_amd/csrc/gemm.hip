@@ -1057,8 +1057,15 @@ __device__ __forceinline__ void split3_quad(const float4& x, const float4& y, ui
   split3_pair(y.z, y.w, h.w, m.w, l.w);
 }
 
-template <int BM, int BN, int WAVES_M, int WAVES_N, bool SEP, int PF = 1>
-__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_f32x6_nt_kernel(GemmP p, long plane) {
+// Split-K form (SPL): blockIdx.z = batch * splitk + split; each split runs K range [split * kchunk,
+// +kchunk) and stores its tile partial write-through (sc1) into its own slab; the LAST split to arrive
+// (agent-scope ticket on the tile's counter, re-armed to 0) sums the slabs in split order
+// (deterministic) and runs the epilogue — the few-tile LXRT / vision GEMMs fill the chip without a
+// second reduce launch, and no workgroup ever waits on another.
+struct X6Split { unsigned* cnt; float* slab; int splitk, kchunk; };
+
+template <int BM, int BN, int WAVES_M, int WAVES_N, bool SEP, int PF = 1, bool SPL = false>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
   constexpr int NT = 64 * WAVES_M * WAVES_N;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N, TM = WM / 16, TN = WN / 16;
   constexpr int NA = BM * 4 / NT, NB = BN * 4 / NT;    // 16-B (8 x bf16) K quads per thread per plane
@@ -1080,9 +1087,10 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_f32x6_nt_kernel(G
     n0 = (wgid % gridDim.x) * BN;
     m0 = (wgid / gridDim.x) * BM;
   }
-  const int b = blockIdx.z;
-  const float* A = p.A + (long)b * p.sA;
-  const unsigned short* W = reinterpret_cast<const unsigned short*>(p.B) + (long)b * p.sB;
+  const int b = SPL ? blockIdx.z / xs.splitk : blockIdx.z, split = SPL ? blockIdx.z % xs.splitk : 0;
+  const int kb = SPL ? split * xs.kchunk : 0;
+  const float* A = p.A + (long)b * p.sA + kb;
+  const unsigned short* W = reinterpret_cast<const unsigned short*>(p.B) + (long)b * p.sB + kb;
 
   floatx4 big[TM][TN], small[SEP ? TM : 1][SEP ? TN : 1];
 #pragma unroll
@@ -1172,7 +1180,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_f32x6_nt_kernel(G
     }
   };
 
-  const int nk = p.K / 32;
+  const int nk = (SPL ? min(xs.kchunk, p.K - kb) : p.K) / 32;
   stg.load(p, A, W, plane, m0, n0, 0, tid);
   if (PF == 1) {
     stg.store(smem, tid);
@@ -1228,6 +1236,48 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_f32x6_nt_kernel(G
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) big[i][j] += small[SEP ? i : 0][SEP ? j : 0];
+  }
+  if constexpr (SPL) {
+    __shared__ int s_last;
+    const int tile = (b * (int)gridDim.y + m0 / BM) * (int)gridDim.x + n0 / BN;
+    constexpr int SLAB_B = BM * BN * 4;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(xs.slab, 0, 0x7fffffff, 0x00020000);
+    const long tbase = (long)tile * xs.splitk;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int off = (int)((tbase + split) * SLAB_B) + ((i * TN + j) * NT + tid) * 16;
+        const u32x4 u = {__float_as_uint(big[i][j][0]), __float_as_uint(big[i][j][1]),
+                         __float_as_uint(big[i][j][2]), __float_as_uint(big[i][j][3])};
+        __builtin_amdgcn_raw_buffer_store_b128(u, rs, off, 0, 16);   // sc1: write-through
+      }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0)
+      s_last = __hip_atomic_fetch_add(xs.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+               (unsigned)(xs.splitk - 1);
+    __syncthreads();
+    if (!s_last) return;
+    if (tid == 0) __hip_atomic_store(xs.cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler-only: sc1 loads below the ticket
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) big[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int s2 = 0; s2 < xs.splitk; ++s2) {     // fixed order: deterministic whoever arrives last
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int off = (int)((tbase + s2) * SLAB_B) + ((i * TN + j) * NT + tid) * 16;
+          const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);   // sc1
+          big[i][j][0] += __uint_as_float(u.x);
+          big[i][j][1] += __uint_as_float(u.y);
+          big[i][j][2] += __uint_as_float(u.z);
+          big[i][j][3] += __uint_as_float(u.w);
+        }
+    }
   }
   store_tile_mf<16, TM, TN, BM, BN>(p, big, b, 0, m0, n0, wm, wn, lane);
 }
@@ -1490,9 +1540,51 @@ extern "C" int dasa_gemm_bf16(const dasa_gemm_desc* d, void* stream) {
   return 0;
 }
 
+// bf16x6 plan: forms 0..9 = tile / accumulator / prefetch variants (sweeps: dasa_gemm_force_config(
+// kX6Force + cfg + 16 * splitk)). Default: 128x128 tiles, separate small-term accumulator, two register
+// stages of prefetch (form 8) — the fastest accurate form on every shape with >= 128 output tiles
+// (profiles/r02/gemm_x6_sweep_b.txt: 136-178 fp32-equivalent TFLOP/s on the 1600- to 20480-row
+// language / LXRT / LSTM shapes). Fewer tiles (the 720- / 1600-row LXRT and vision GEMMs: 36-108
+// tiles) split K over the tiles' workgroups until ~256 workgroups fill the chip, reduced in-kernel by
+// the last split to arrive (X6Split); needs the workspace.
+struct X6Plan { int cfg, bm, bn, splitk, kchunk; int64_t ws; };
+
+static X6Plan x6_plan(const dasa_gemm_desc* d) {
+  const int M = d->M, N = d->N, K = d->K, batch = d->batch < 1 ? 1 : d->batch;
+  X6Plan pl{8, 128, 128, 1, K, 0};
+  int fsplit = 0;
+  if (g_force_cfg >= kX6Force) {
+    pl.cfg = (g_force_cfg - kX6Force) % 16;
+    fsplit = ((g_force_cfg - kX6Force) / 16) % 64;
+  }
+  pl.bm = (pl.cfg == 1 || pl.cfg == 3 || pl.cfg == 6 || pl.cfg == 7) ? 256 : (pl.cfg == 4 || pl.cfg == 5) ? 64 : 128;
+  pl.bn = pl.cfg == 5 ? 64 : 128;
+  const long tiles = (long)cdiv(M, pl.bm) * cdiv(N, pl.bn) * batch;
+  // split count (profiles/r02/gemm_x6_splitk.txt): the most splits that keep tiles x splits <= 256
+  // (one wave of workgroups) with >= 8 32-deep K steps per split; forced splits may go to 4 steps
+  int splitk = 1;
+  if (fsplit > 0) splitk = fsplit < K / 128 ? fsplit : K / 128;
+  else if (tiles < 128) splitk = (int)(256 / tiles) < K / 256 ? (int)(256 / tiles) : K / 256;
+  const bool spl_form = pl.cfg == 8 || pl.cfg == 4 || pl.cfg == 5;
+  if (!spl_form || splitk < 1 || tiles * splitk > 32767 || tiles > kCntWords) splitk = 1;
+  if (splitk > 1) {
+    pl.kchunk = (int)(cdiv(cdiv(K, splitk), 32) * 32);
+    pl.splitk = (int)cdiv(K, pl.kchunk);
+  }
+  if (pl.splitk > 1) pl.ws = kCntBytes + tiles * pl.splitk * (int64_t)pl.bm * pl.bn * (int64_t)sizeof(float);
+  return pl;
+}
+
+extern "C" int64_t dasa_gemm_f32x6_workspace(const dasa_gemm_desc* d) {
+  if (!d || d->M < 0 || d->N < 0 || d->K < 0) return 0;
+  return x6_plan(d).ws;
+}
+
 // fp32-accurate GEMM on bf16 MFMA (bf16x6 split; see gemm_f32x6_nt_kernel). d->B = the hi plane of
-// the pre-split weight, planes `plane` bf16 elements apart.
-extern "C" int dasa_gemm_f32x6(const dasa_gemm_desc* d, int64_t plane, void* stream) {
+// the pre-split weight, planes `plane` bf16 elements apart. ws (zero-initialised once, counters
+// re-armed by every call; dasa_gemm_f32x6_workspace bytes) enables the split-K form; without it every
+// problem runs one workgroup per tile.
+extern "C" int dasa_gemm_f32x6_ws(const dasa_gemm_desc* d, int64_t plane, void* ws, int64_t ws_bytes, void* stream) {
   if (!d) return (int)hipErrorInvalidValue;
   const int M = d->M, N = d->N, K = d->K, batch = d->batch < 1 ? 1 : d->batch;
   if (M < 0 || N < 0 || K < 0 || d->opA != 0 || d->opB != 1) return (int)hipErrorInvalidValue;
@@ -1510,31 +1602,46 @@ extern "C" int dasa_gemm_f32x6(const dasa_gemm_desc* d, int64_t plane, void* str
   p.aux = d->aux; p.ld_aux = d->ld_aux; p.sAux = d->strideAux;
   p.colscale = d->colscale; p.alpha = d->alpha; p.beta = d->beta;
   p.ws = nullptr;
-  // 128x128 tiles, separate small-term accumulator, two register stages of prefetch (form 8): the
-  // fastest accurate form on every shape the plan routes here (profiles/r02/gemm_x6_sweep_b.txt:
-  // 136-178 fp32-equivalent TFLOP/s on the 1600- to 20480-row language / LXRT / LSTM shapes); the
-  // others stay for sweeps
-  int cfg = 8;
-  if (g_force_cfg >= kX6Force) cfg = (g_force_cfg - kX6Force) % 16;
-  const int bm = (cfg == 1 || cfg == 3 || cfg == 6 || cfg == 7) ? 256 : (cfg == 4 || cfg == 5) ? 64 : 128;
-  const int bn = cfg == 5 ? 64 : 128;
+  X6Plan pl = x6_plan(d);
+  if (pl.splitk > 1 && (ws == nullptr || ws_bytes < pl.ws)) { pl.splitk = 1; pl.kchunk = K; }
+  const int cfg = pl.cfg, bm = pl.bm, bn = pl.bn;
   p.group_m = cdiv(M, bm) >= 8 ? 4 : 1;
-  dim3 grid((unsigned)cdiv(N, bn), (unsigned)cdiv(M, bm), batch);
+  X6Split xs{};
   hipStream_t st = (hipStream_t)stream;
+  if (pl.splitk > 1) {
+    xs.cnt = (unsigned*)ws;
+    xs.slab = (float*)((char*)ws + kCntBytes);
+    xs.splitk = pl.splitk;
+    xs.kchunk = pl.kchunk;
+    p.group_m = 1;
+    dim3 grid((unsigned)cdiv(N, bn), (unsigned)cdiv(M, bm), batch * pl.splitk);
+    switch (cfg) {
+      case 4: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<64, 128, 2, 2, true, 2, true>), grid, dim3(256), 0, st, p, (long)plane, xs); break;
+      case 5: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<64, 64, 2, 2, true, 2, true>), grid, dim3(256), 0, st, p, (long)plane, xs); break;
+      default: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true, 2, true>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
+    }
+    DASA_CHECK_LAUNCH();
+    return 0;
+  }
+  dim3 grid((unsigned)cdiv(N, bn), (unsigned)cdiv(M, bm), batch);
   switch (cfg) {
-    case 1: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<256, 128, 4, 2, false>), grid, dim3(512), 0, st, p, (long)plane); break;
-    case 2: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, false>), grid, dim3(512), 0, st, p, (long)plane); break;
-    case 3: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<256, 128, 4, 2, true>), grid, dim3(512), 0, st, p, (long)plane); break;
-    case 4: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<64, 128, 2, 2, true>), grid, dim3(256), 0, st, p, (long)plane); break;
-    case 5: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<64, 64, 2, 2, true>), grid, dim3(256), 0, st, p, (long)plane); break;
-    case 6: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<256, 128, 4, 2, false, 2>), grid, dim3(512), 0, st, p, (long)plane); break;
-    case 7: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<256, 128, 4, 2, true, 2>), grid, dim3(512), 0, st, p, (long)plane); break;
-    case 8: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true, 2>), grid, dim3(512), 0, st, p, (long)plane); break;
-    case 9: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true, 3>), grid, dim3(512), 0, st, p, (long)plane); break;
-    default: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true>), grid, dim3(512), 0, st, p, (long)plane); break;
+    case 1: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<256, 128, 4, 2, false>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
+    case 2: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, false>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
+    case 3: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<256, 128, 4, 2, true>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
+    case 4: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<64, 128, 2, 2, true>), grid, dim3(256), 0, st, p, (long)plane, xs); break;
+    case 5: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<64, 64, 2, 2, true>), grid, dim3(256), 0, st, p, (long)plane, xs); break;
+    case 6: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<256, 128, 4, 2, false, 2>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
+    case 7: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<256, 128, 4, 2, true, 2>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
+    case 8: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true, 2>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
+    case 9: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true, 3>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
+    default: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
   }
   DASA_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int dasa_gemm_f32x6(const dasa_gemm_desc* d, int64_t plane, void* stream) {
+  return dasa_gemm_f32x6_ws(d, plane, nullptr, 0, stream);
 }
 
 extern "C" int dasa_f32_split3_bf16(const float* x, int64_t ldx, uint16_t* y, int32_t rows, int32_t cols,

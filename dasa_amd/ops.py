@@ -82,11 +82,12 @@ def _rows(t):
 
 # ------------------------------------------------------------------------------------------ GEMM
 _WS = {}
+_WS_OLD = []
 _WS_SK = (64 << 10) + 2 * 512 * 128 * 128 * 4    # counters + stream-K slabs (<= 512 workgroups)
 _WS_MIN = max(32 << 20, _WS_SK)
 
 
-def _gemm_ws(device, d):
+def _gemm_ws(device, d, need=0):
     """GEMM workspace (include/dasa_hip.h dasa_gemm_f32_workspace): one zero-initialised buffer per
     (device, stream), grown on demand and reused by every GEMM on that stream. Its leading stream-K
     arrival counters are left zero by every call (so it is zeroed only on allocation); split-K
@@ -98,9 +99,10 @@ def _gemm_ws(device, d):
         buf = torch.zeros(_WS_MIN // 4, dtype=torch.float32, device=device)
         _WS[key] = buf
     nbytes = buf.numel() * 4
-    if d.M * d.N * max(1, d.batch) * 16 * 4 + _WS_SK > nbytes:   # split-K is at most 16-way
-        need = _lib.lib().dasa_gemm_f32_workspace(ctypes.byref(d))
+    if need or d.M * d.N * max(1, d.batch) * 16 * 4 + _WS_SK > nbytes:   # split-K is at most 16-way
+        need = need or _lib.lib().dasa_gemm_f32_workspace(ctypes.byref(d))
         if need > nbytes:
+            _WS_OLD.append(buf)      # kernels already queued / captured in a graph still point at it
             buf = torch.zeros(need // 4 + 1, dtype=torch.float32, device=device)
             _WS[key] = buf
             nbytes = buf.numel() * 4
@@ -240,15 +242,26 @@ def _x6_weight(W):
     return planes
 
 
+def _x6_splitk(M, N, K):
+    """Split count of the bf16x6 plan (gemm.hip x6_plan): 1 at >= 128 output tiles of 128x128, else the
+    most splits keeping tiles x splits <= 256 with >= 8 32-deep K steps per split."""
+    tiles = -(-M // 128) * -(-N // 128)
+    return 1 if tiles >= 128 else max(1, min(256 // tiles, K // 256))
+
+
 def _emu_ok(M, N, K, lda, x):
-    """Plan rule (profiles/r02/gemm_x6_sweep_b.txt): the 128x128-tile bf16x6 kernel beats the native fp32
-    MFMA kernels (by 1.1-1.5x) once it has >= 128 output tiles — the 12800-row language stack, the
-    1600-row LSTM input projections and LXRT language branch, the 720 x 3072 vision FFN; the smaller
-    LXRT GEMMs (36-78 tiles) stay on the native fp32 kernels."""
+    """Plan rule (profiles/r02/gemm_x6_sweep_b.txt, gemm_x6_splitk.txt): the 128x128-tile bf16x6 kernel
+    beats the native fp32 MFMA kernels (by 1.1-1.5x) once it fills the chip — >= 128 output tiles (the
+    12800-row language stack, the 1600-row LSTM input projections and LXRT language branch, the 720 x 3072
+    vision FFN), or, at K >= 2048, >= 192 workgroups with K split over the tiles (the 1600 / 720 x 768 x
+    3072 FFN outputs, the 720 x 2048 x 2048 AdaIN gate). The short-K LXRT projections (36-108 tiles,
+    K = 768) stay on the native fp32 kernels: split there, they win in isolation but lose in the
+    iteration, where they share the chip with the concurrent language stream."""
     if not (_EMU["on"] and M >= _EMU["min_rows"] and K % 32 == 0 and N % 8 == 0 and lda % 4 == 0
             and x.data_ptr() % 16 == 0):
         return False
-    return -(-M // 128) * -(-N // 128) >= 128
+    tiles = -(-M // 128) * -(-N // 128)
+    return tiles >= 128 or (K >= 2048 and tiles * _x6_splitk(M, N, K) >= 192)
 
 
 def gemm_f32x6(x, planes, out, *, M, N, K, lda, ldc, bias=None, act=None, aux=None, ld_aux=0, colscale=None,
@@ -264,8 +277,15 @@ def gemm_f32x6(x, planes, out, *, M, N, K, lda, ldc, bias=None, act=None, aux=No
     d.aux, d.ld_aux, d.strideAux = _p(aux), int(ld_aux), 0
     d.colscale = _p(colscale)
     d.alpha, d.beta = float(alpha), float(beta)
-    _call("dasa_gemm_f32x6", "gemm_x6", _lib.lib().dasa_gemm_f32x6, ctypes.byref(d), int(N) * int(K), _stream(),
-          flops=2.0 * M * N * K, nbytes=4.0 * M * K + 6.0 * K * N + 4.0 * M * N, detail=(int(M), int(N), int(K)))
+    L = _lib.lib()
+    ws, ws_bytes = 0, 0
+    if -(-M // 128) * -(-N // 128) < 128:          # few tiles: the split-K form needs the workspace
+        need = L.dasa_gemm_f32x6_workspace(ctypes.byref(d))
+        if need:
+            ws, ws_bytes = _gemm_ws(out.device, d, need)
+    _call("dasa_gemm_f32x6", "gemm_x6", L.dasa_gemm_f32x6_ws, ctypes.byref(d), int(N) * int(K), ws, ws_bytes,
+          _stream(), flops=2.0 * M * N * K, nbytes=4.0 * M * K + 6.0 * K * N + 4.0 * M * N,
+          detail=(int(M), int(N), int(K)))
 
 
 def linear(x, W, b=None, act=None, out=None, aux=None, colscale=None, beta=0.0, alpha=1.0):

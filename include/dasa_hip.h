@@ -77,6 +77,12 @@ int dasa_f32_to_bf16(const float* x, uint16_t* y, int64_t n, void* stream);
  * Same fused epilogue as dasa_gemm_f32. Replaces the nn.Linear forwards (vilmodel.py BERT / LXRT
  * projections and FFN, model.py decoder linears, agent_dg.py:1519 DGAdaChannel.a_fc). */
 int dasa_gemm_f32x6(const dasa_gemm_desc* d, int64_t plane, void* stream);
+/* The same with a workspace (ws: zero-initialised once, >= dasa_gemm_f32x6_workspace(d) bytes; its
+ * leading counters are re-armed by every call, so one buffer serves every call on one stream): problems
+ * with few output tiles (< 128 of 128x128) split K over several workgroups per tile, reduced in-kernel
+ * by the last split to arrive in a fixed order (deterministic). Workspace 0 = no split needed. */
+int64_t dasa_gemm_f32x6_workspace(const dasa_gemm_desc* d);
+int dasa_gemm_f32x6_ws(const dasa_gemm_desc* d, int64_t plane, void* ws, int64_t ws_bytes, void* stream);
 /* x [rows][ldx] fp32 -> y = three bf16 planes [3][rows][cols] (hi, mid, lo; plane stride rows*cols),
  * x = hi + mid + lo exactly for normal fp32 values; cols % 8 == 0, 16-B aligned x and y. */
 int dasa_f32_split3_bf16(const float* x, int64_t ldx, uint16_t* y, int32_t rows, int32_t cols, void* stream);

@@ -543,6 +543,49 @@ def test_gemm_f32x6(dev, M, N, K):
         lib.dasa_gemm_force_config(-1)
 
 
+@pytest.mark.parametrize("M,N,K", [(517, 200, 768), (720, 768, 768), (1600, 768, 3072), (100, 2048, 2048),
+                                   (3, 24, 256)])
+def test_gemm_f32x6_splitk(dev, M, N, K):
+    """The split-K bf16x6 forms (few output tiles: K split over several workgroups per tile, reduced
+    in-kernel by the last split to arrive): error against fp64 at most the native kernel's (+10%), the
+    fused epilogue applied once, bitwise-deterministic repeats, and the arrival counters re-armed
+    (every call writes every element of a NaN-filled output)."""
+    from dasa_amd import _lib, ops
+    g = torch.Generator().manual_seed(M * 7 + N + K)
+    Abuf = torch.randn(M, K + 8, generator=g)
+    A = Abuf[:, 4:4 + K]
+    W = torch.randn(N, K, generator=g) * 0.05
+    bias = torch.randn(N, generator=g) * 0.1
+    aux = torch.rand(M, N, generator=g)
+    cs = torch.rand(N, generator=g)
+    c0 = torch.randn(M, N, generator=g)
+    ref = (A.double() @ W.double().t() + bias.double())
+    Ad, Wd, bd = Abuf.to(dev)[:, 4:4 + K], W.to(dev), bias.to(dev)
+    planes = ops.split3_bf16(Wd)
+    lib = _lib.lib()
+    out_nat = torch.empty(M, N, device=dev)
+    ops.gemm(Ad, Wd, out_nat, M=M, N=N, K=K, lda=K + 8, ldb=K, ldc=N, bias=bd)
+    err_nat = (out_nat.cpu().double() - ref).abs().max().item()
+    try:
+        for cfg, spl in ((8, 0), (8, 2), (8, 3), (4, 2), (4, 5), (5, 3)):
+            lib.dasa_gemm_force_config((1 << 21) + cfg + 16 * spl if spl else -1)
+            outs = []
+            for _ in range(3):
+                y = torch.full((M, N), float("nan"), device=dev)
+                ops.gemm_f32x6(Ad, planes, y, M=M, N=N, K=K, lda=K + 8, ldc=N, bias=bd)
+                outs.append(y.cpu())
+            err = (outs[0].double() - ref).abs().max().item()
+            assert err <= 1.1 * err_nat + 1e-7, (cfg, spl, err, err_nat)
+            assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2]), (cfg, spl)
+            y2 = c0.clone().to(dev)
+            ops.gemm_f32x6(Ad, planes, y2, M=M, N=N, K=K, lda=K + 8, ldc=N, bias=bd, act="sigmoid",
+                           aux=aux.to(dev), ld_aux=N, colscale=cs.to(dev), beta=0.5)
+            want = torch.sigmoid(ref) * aux.double() * cs.double() + 0.5 * c0.double()
+            assert (y2.cpu().double() - want).abs().max().item() < 1e-5, (cfg, spl)
+    finally:
+        lib.dasa_gemm_force_config(-1)
+
+
 @pytest.mark.parametrize("M,N,K", [(20, 2176, 1024), (20, 4096, 2240), (64, 1000, 512), (1, 1, 32), (7, 130, 96),
                                    (32, 3072, 3072)])
 def test_gemm_skinny(dev, M, N, K):

@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--shapes", nargs="*")
     ap.add_argument("--sweep", type=int, default=0, help="also time bf16x6 tile forms 0..N-1 (forced)")
+    ap.add_argument("--forms", nargs="*", default=[], help="forced bf16x6 form:splitk pairs to time, e.g. 8:3 4:2")
     a = ap.parse_args()
     shapes = [tuple(int(v) for v in s.split(",")) for s in a.shapes] if a.shapes else SHAPES
     dev = torch.device("cuda", 0)
@@ -78,6 +79,19 @@ def main():
             L.dasa_gemm_force_config(-1)
             out["x6_forms"] = forms
             print("   forms:", " ".join(f"{c}:{v[0]}TF/{v[1]:.1e}" for c, v in forms.items()), flush=True)
+        if a.forms:
+            from dasa_amd import _lib
+            L = _lib.lib()
+            forms = {}
+            for f in a.forms:
+                cfg, spl = (int(v) for v in f.split(":"))
+                L.dasa_gemm_force_config((1 << 21) + cfg + 16 * spl)
+                x6()
+                us = timeit(x6, a.reps)
+                forms[f] = (round(fl / us / 1e6, 1), (y2.double() - ref).abs().max().item() / scale)
+            L.dasa_gemm_force_config(-1)
+            out["x6_split_forms"] = forms
+            print("   form:split:", " ".join(f"{c}={v[0]}TF/{v[1]:.1e}" for c, v in forms.items()), flush=True)
         y3 = torch.addmm(bias, A, W.t())
         out["torch"] = dict(us=timeit(lambda: torch.addmm(bias, A, W.t(), out=y3), a.reps),
                             err=(y3.double() - ref).abs().max().item() / scale,
