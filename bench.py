@@ -52,6 +52,7 @@ def parse():
     p.add_argument("--fast-exit", action="store_true",
                    help="os._exit after the JSON line (skips interpreter teardown; used under rocprofv3)")
     p.add_argument("--no-cfg5", action="store_true", help="skip the BASELINE configs[4] (B=256, vl=6, bf16) leg")
+    p.add_argument("--no-host-input", action="store_true", help="skip the host-input (PCIe-inclusive) leg")
     p.add_argument("--cfg5-only", action="store_true", help="run only the configs[4] leg (tuning)")
     p.add_argument("--cfg5-steps", type=int, default=6, help="decision steps per configs[4] rollout")
     p.add_argument("--backend", default="nccl", help="nccl (= RCCL on ROCm) | gloo (rehearsal only)")
@@ -164,6 +165,32 @@ def cpu_baseline(a):
                           "container, 8 threads: cfg2 train 0.97, cfg2 fwd 0.86, cfg1 fwd 0.70)"}
 
 
+class _HostInputEnv:
+    """The env without device_input_feat: the agent takes the reference's own input path (numpy panorama /
+    candidate features in the obs dicts, packed on the host and copied H2D from pinned memory every step,
+    agent_dg.py:286-323)."""
+
+    def __init__(self, env):
+        self._e = env
+
+    def __getattr__(self, k):
+        if k in ("device_input_feat", "device_input_feat_steps"):
+            raise AttributeError(k)
+        return getattr(self._e, k)
+
+
+def host_input_leg(a, steps=2):
+    """The headline iteration with host-resident inputs (PCIe-inclusive): same config, features built on the
+    host per observation and copied to the device each step. Reported beside `value`, never as it."""
+    from dasa_amd.synth import SynthR2RBatch
+    agent, env = build_agent(a, 0, 1)
+    agent.env = _HostInputEnv(SynthR2RBatch(env.world, a.batch, seed=1000, mode="wander", instr_len=80))
+    train_step(agent)
+    u, dt = timed(lambda: train_step(agent), steps, 0, 1)
+    return {"value": round(u / dt, 2), "unit": "agent-decisions/s", "ms_per_step": round(dt / steps * 1e3, 2),
+            "note": "cfg2 training iteration with host-built observation features copied H2D (pinned) each step"}
+
+
 def cfg5_leg(a):
     """BASELINE configs[4]: B=256, d_vl_layers=6, 36x2048 synthetic feats, forward (eval/argmax rollout)
     with bf16 GEMM operands and fp32 accumulation (ops.bf16_matmul); the same rollout in fp32 beside it.
@@ -253,6 +280,8 @@ def main():
         out["hbm_kernels"] = kbench.hbm_kernels((a.batch, 256))
         out["hbm_kernels_note"] = ("AdaIN gate / mu-sigma and attention kernels in isolation, graph-replayed back to back "
                                    "(no host gaps); B=256 is BASELINE configs[4]'s batch; algorithmic bytes / time vs 8 TB/s")
+    if rank == 0 and world == 1 and not a.no_host_input:
+        out["host_input"] = host_input_leg(a)
     if rank == 0 and world == 1 and not a.no_cfg5:
         out["cfg5"] = cfg5_leg(a)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

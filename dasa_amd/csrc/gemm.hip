@@ -922,7 +922,7 @@ __device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
 
 __device__ __forceinline__ int bswz(int row) { return (row >> 1) & 7; }
 
-template <int BM, int BN, int WAVES_M, int WAVES_N>
+template <int BM, int BN, int WAVES_M, int WAVES_N, int PF = 1>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_nt_kernel(GemmP p) {
   constexpr int NT = 64 * WAVES_M * WAVES_N;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N, TM = WM / 16, TN = WN / 16;
@@ -988,7 +988,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_nt_kernel(Ge
         S[BM * 8 + row * 8 + (kq ^ bswz(row))] = b[i];
       }
     }
-  } stg;
+  } stg, stg2;
   // clamped rows: rows past M / N re-read the last valid row; the epilogue never stores them
   // lane l of a 16x16x32 MFMA holds A[row l & 15][k = 8 (l >> 4) + j]: K step s reads quad 4s + (l >> 4)
   auto compute = [&](const uint4* S) {
@@ -1018,13 +1018,31 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_nt_kernel(Ge
 
   const int nk = p.K / 64;
   stg.load(p, A, W, m0, n0, 0, tid);
-  stg.store(smem, tid);
-  __syncthreads();
-  for (int t = 0; t < nk; ++t) {
-    stg.load(p, A, W, m0, n0, 64 * min(t + 1, nk - 1), tid);   // unconditional (see gemm_nt_k64_kernel)
-    compute(smem + (t & 1) * STAGE);
-    stg.store(smem + ((t + 1) & 1) * STAGE, tid);
+  if (PF == 1) {
+    stg.store(smem, tid);
     __syncthreads();
+    for (int t = 0; t < nk; ++t) {
+      stg.load(p, A, W, m0, n0, 64 * min(t + 1, nk - 1), tid);   // unconditional (see gemm_nt_k64_kernel)
+      compute(smem + (t & 1) * STAGE);
+      stg.store(smem + ((t + 1) & 1) * STAGE, tid);
+      __syncthreads();
+    }
+  } else {
+    // two register stages (as gemm_f32x6_nt_kernel): tile t + 2's loads are issued before tile t's MFMAs
+    stg2.load(p, A, W, m0, n0, 64 * min(1, nk - 1), tid);
+    stg.store(smem, tid);
+    __syncthreads();
+    for (int t = 0; t < nk; t += 2) {
+      stg.load(p, A, W, m0, n0, 64 * min(t + 2, nk - 1), tid);
+      compute(smem);
+      stg2.store(smem + STAGE, tid);
+      __syncthreads();
+      if (t + 1 >= nk) break;
+      stg2.load(p, A, W, m0, n0, 64 * min(t + 3, nk - 1), tid);
+      compute(smem + STAGE);
+      stg.store(smem, tid);
+      __syncthreads();
+    }
   }
   store_tile_mf<16, TM, TN, BM, BN>(p, acc, b, 0, m0, n0, wm, wn, lane);
 }
@@ -1497,9 +1515,9 @@ extern "C" int dasa_gemm_f32(const dasa_gemm_desc* d, void* ws, int64_t ws_bytes
   return 0;
 }
 
-// bf16 plan: 128x128 tiles of 8 waves (4x2 of 32x64; 64 KB LDS, two workgroups per CU) won or tied on
-// every configs[4] shape of the sweep (profiles/r01e/gemm_bf16.txt); the other tile/wave forms stay for
-// sweeps: dasa_gemm_force_config(kBf16Force + cfg), cfg 0..6.
+// bf16 plan: 128x128 tiles of 8 waves (4x2 of 32x64; 64 KB LDS, two workgroups per CU), or 256x256 tiles
+// of 16 waves on large problems (profiles/r01e/gemm_bf16.txt, profiles/r02/gemm_bf16_sweep.txt); the
+// other tile/wave/prefetch forms stay for sweeps: dasa_gemm_force_config(kBf16Force + cfg), cfg 0..10.
 constexpr int kBf16Force = 1 << 20;
 constexpr int kX6Force = 1 << 21;   // dasa_gemm_force_config(kX6Force + cfg): bf16x6 tile forms 0..5
 
@@ -1521,9 +1539,12 @@ extern "C" int dasa_gemm_bf16(const dasa_gemm_desc* d, void* stream) {
   p.aux = d->aux; p.ld_aux = d->ld_aux; p.sAux = d->strideAux;
   p.colscale = d->colscale; p.alpha = d->alpha; p.beta = d->beta;
   p.ws = nullptr;
-  int cfg = 2;
-  if (g_force_cfg >= kBf16Force && g_force_cfg < kX6Force) cfg = (g_force_cfg - kBf16Force) % 8;
-  const int bm = (cfg == 1 || cfg == 5) ? 256 : 128, bn = cfg == 3 ? 64 : cfg == 6 ? 256 : 128;
+  // 256x256 tiles of 16 waves (128 KB LDS, one workgroup per CU) once there are >= 200 of them:
+  // +8-25% over 128x128 on the configs[4] shapes (profiles/r02/gemm_bf16_sweep.txt)
+  int cfg = cdiv(M, 256) * cdiv(N, 256) * batch >= 200 ? 9 : 2;
+  if (g_force_cfg >= kBf16Force && g_force_cfg < kX6Force) cfg = (g_force_cfg - kBf16Force) % 16;
+  const int bm = (cfg == 1 || cfg == 5 || cfg == 7 || cfg == 9) ? 256 : 128,
+            bn = cfg == 3 ? 64 : (cfg == 6 || cfg == 9 || cfg == 10) ? 256 : 128;
   p.group_m = cdiv(M, bm) >= 8 ? 4 : 1;
   dim3 grid((unsigned)cdiv(N, bn), (unsigned)cdiv(M, bm), batch);
   hipStream_t st = (hipStream_t)stream;
@@ -1534,6 +1555,10 @@ extern "C" int dasa_gemm_bf16(const dasa_gemm_desc* d, void* stream) {
     case 4: hipLaunchKernelGGL((gemm_bf16_nt_kernel<128, 128, 4, 4>), grid, dim3(1024), 0, st, p); break;
     case 5: hipLaunchKernelGGL((gemm_bf16_nt_kernel<256, 128, 8, 2>), grid, dim3(1024), 0, st, p); break;
     case 6: hipLaunchKernelGGL((gemm_bf16_nt_kernel<128, 256, 2, 4>), grid, dim3(512), 0, st, p); break;
+    case 7: hipLaunchKernelGGL((gemm_bf16_nt_kernel<256, 128, 4, 2, 2>), grid, dim3(512), 0, st, p); break;
+    case 8: hipLaunchKernelGGL((gemm_bf16_nt_kernel<128, 128, 4, 2, 2>), grid, dim3(512), 0, st, p); break;
+    case 9: hipLaunchKernelGGL((gemm_bf16_nt_kernel<256, 256, 4, 4>), grid, dim3(1024), 0, st, p); break;
+    case 10: hipLaunchKernelGGL((gemm_bf16_nt_kernel<128, 256, 2, 4, 2>), grid, dim3(512), 0, st, p); break;
     default: hipLaunchKernelGGL((gemm_bf16_nt_kernel<128, 128, 2, 2>), grid, dim3(256), 0, st, p); break;
   }
   DASA_CHECK_LAUNCH();

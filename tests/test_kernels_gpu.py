@@ -450,7 +450,7 @@ def test_gemm_bf16(dev, M, N, K):
     b = _rand(N, g=g)
     xb, Wb = x.to(torch.bfloat16).double(), W.to(torch.bfloat16).double()
     L = _lib.lib()
-    for cfg in [(1 << 20) + c for c in range(7)] + [-1]:
+    for cfg in [(1 << 20) + c for c in range(11)] + [-1]:
         L.dasa_gemm_force_config(cfg)
         try:
             with torch.no_grad(), ops.bf16_matmul():

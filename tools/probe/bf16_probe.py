@@ -29,11 +29,12 @@ for M, N, K in ((20480, 3072, 768), (20480, 768, 3072), (20480, 2304, 768), (204
     f32 = fl / bench(lambda: ops.linear(A, W)) / 1e9
     res = []
     with torch.no_grad(), ops.bf16_matmul():
-        for c in (-1, 0, 1, 2, 3, 4, 5, 6):
+        for c in (-1, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10):
             L.dasa_gemm_force_config(c if c < 0 else (1 << 20) + c)
             res.append(fl / bench(lambda: ops.linear(A, W)) / 1e9)
         L.dasa_gemm_force_config(-1)
         tb = fl / bench(lambda: A.to(torch.bfloat16) @ W.to(torch.bfloat16).t()) / 1e9
     print(f"M{M} N{N} K{K}: fp32 {f32:.0f} | bf16 auto {res[0]:.0f} c128x128w4 {res[1]:.0f} c256x128w8 {res[2]:.0f} "
           f"c128x128w8 {res[3]:.0f} c128x64w4 {res[4]:.0f} c128x128w16 {res[5]:.0f} c256x128w16 {res[6]:.0f} "
-          f"c128x256w8 {res[7]:.0f} | torch bf16 (incl. casts) {tb:.0f} TFLOP/s", flush=True)
+          f"c128x256w8 {res[7]:.0f} c256x128w8pf2 {res[8]:.0f} c128x128w8pf2 {res[9]:.0f} c256x256w16 {res[10]:.0f} "
+          f"c128x256w8pf2 {res[11]:.0f} | torch bf16 (incl. casts) {tb:.0f} TFLOP/s", flush=True)
