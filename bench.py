@@ -214,9 +214,9 @@ def cfg5_leg(a):
         with prof.collect() as rec:
             run()
         summ = rec.summary()
-        ent["kernels"] = {k: v for k, v in summ["kernels"].items() if k in ("gemm", "gemm_bf16", "mha", "bilstm",
-                                                                              "layernorm", "elementwise")}
-        fam = "gemm_bf16" if mode == "bf16" else "gemm"
+        ent["kernels"] = {k: v for k, v in summ["kernels"].items() if k in ("gemm", "gemm_x6", "gemm_bf16", "mha",
+                                                                              "bilstm", "layernorm", "elementwise")}
+        fam = "gemm_bf16" if mode == "bf16" else ("gemm_x6" if "gemm_x6" in summ["kernels"] else "gemm")
         if fam in summ["kernels"]:
             k = summ["kernels"][fam]
             ent["roofline"] = {"kernel": fam, "bound": "mfma", "achieved": k["achieved"], "peak": k["peak"],

@@ -80,6 +80,13 @@ class _Recorder:
                 "unit": d["unit"], "frac": d["frac"], "traffic": None,
                 "per_launch": {"avg_us": d["avg_launch_us"], "alg_flops": fam[dom_name]["flops"] / nl,
                                "alg_bytes": fam[dom_name]["bytes"] / nl}}
+        if dom_name == "gemm_x6":
+            # fp32 work on bf16 matrix cores: `peak` is the bf16 dense peak / 6 (six bf16 MFMA products per
+            # fp32 product), i.e. frac = the bf16 MFMA utilisation; against the fp32 MFMA peak the same
+            # achieved rate reads frac_vs_fp32_peak
+            roof["frac_vs_fp32_peak"] = round(d["achieved"] / peak_tf, 4)
+            roof["peak_note"] = ("fp32 GEMM as six exact bf16 products (bf16x6): peak = 2500 / 6 TFLOP/s "
+                                 "fp32-equivalent; native fp32 MFMA peak 157.3")
         pmc = _pmc_traffic()
         if pmc is not None and dom_name in pmc["families"]:
             pf = pmc["families"][dom_name]
