@@ -53,6 +53,7 @@ def parse():
                    help="os._exit after the JSON line (skips interpreter teardown; used under rocprofv3)")
     p.add_argument("--no-cfg5", action="store_true", help="skip the BASELINE configs[4] (B=256, vl=6, bf16) leg")
     p.add_argument("--no-host-input", action="store_true", help="skip the host-input (PCIe-inclusive) leg")
+    p.add_argument("--no-hoist", action="store_true", help="skip the --hoist_language (non-default mode) leg")
     p.add_argument("--cfg5-only", action="store_true", help="run only the configs[4] leg (tuning)")
     p.add_argument("--cfg5-steps", type=int, default=6, help="decision steps per configs[4] rollout")
     p.add_argument("--backend", default="nccl", help="nccl (= RCCL on ROCm) | gloo (rehearsal only)")
@@ -179,6 +180,23 @@ class _HostInputEnv:
         return getattr(self._e, k)
 
 
+def hoist_leg(agent, steps=2):
+    """The headline iteration with --hoist_language (not a reference flag): the detached
+    language stack computed once per rollout in train mode (one dropout draw per rollout instead of one
+    per step; no gradient changes). A different workload than `value`: reported beside it, never as it."""
+    from dasa_amd.r2r.param import args
+    prev = args.hoist_language
+    args.hoist_language = True
+    try:
+        train_step(agent)
+        u, dt = timed(lambda: train_step(agent), steps, 0, 1)
+    finally:
+        args.hoist_language = prev
+    return {"value": round(u / dt, 2), "unit": "agent-decisions/s", "ms_per_step": round(dt / steps * 1e3, 2),
+            "note": "cfg2 training iteration with --hoist_language (language stack once per rollout; "
+                    "non-default, not reference-faithful dropout draws)"}
+
+
 def host_input_leg(a, steps=2):
     """The headline iteration with host-resident inputs (PCIe-inclusive): same config, features built on the
     host per observation and copied to the device each step. Reported beside `value`, never as it."""
@@ -280,6 +298,8 @@ def main():
         out["hbm_kernels"] = kbench.hbm_kernels((a.batch, 256))
         out["hbm_kernels_note"] = ("AdaIN gate / mu-sigma and attention kernels in isolation, graph-replayed back to back "
                                    "(no host gaps); B=256 is BASELINE configs[4]'s batch; algorithmic bytes / time vs 8 TB/s")
+    if rank == 0 and world == 1 and not a.no_hoist:
+        out["hoist_language"] = hoist_leg(agent)
     if rank == 0 and world == 1 and not a.no_host_input:
         out["host_input"] = host_input_leg(a)
     if rank == 0 and world == 1 and not a.no_cfg5:

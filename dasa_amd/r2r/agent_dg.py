@@ -543,7 +543,7 @@ class Seq2SeqAgent(BaseAgent):
             # The env is stepped one chunk ahead: chunk k+1 is planned on the host right after chunk
             # k's encoder is enqueued, while the GPU runs it (the first chunk is half-size so the GPU
             # starts early).
-            self.encoder.cache_language(not self.encoder.training, steps=0)
+            self.encoder.cache_language(not self.encoder.training, steps=0, rows=batch_size)
             chunk = max(1, int(os.environ.get("DASA_TEACHER_CHUNK", "8")))
             t = 0
             plan = []
@@ -583,7 +583,7 @@ class Seq2SeqAgent(BaseAgent):
                     masks.append(s["mask"])
                 plan = nxt
         else:
-            self.encoder.cache_language(not self.encoder.training, steps=self.episode_len)
+            self.encoder.cache_language(not self.encoder.training, steps=self.episode_len, rows=batch_size)
             for t in range(self.episode_len):
                 # host-side inputs of the step's loss/action stage, copied up front without a sync (the
                 # reference builds them after the decoder with blocking copies; same values)

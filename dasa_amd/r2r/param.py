@@ -68,6 +68,10 @@ _FLAGS = [
     ("--depth_drop", None, "const", False), ("--use_shift", None, "const", False),
     ("--shift_kernel_size", None, int, 3), ("--consistent_drop", None, "const", False),
     ("--decoder_consistent_drop", None, "const", False), ("--ctx_v", None, "const", False),
+    # not a reference flag: compute the detached language stack once per rollout in train
+    # mode too (one dropout draw per rollout instead of one per step). Off = the reference's per-step
+    # recompute; no gradient changes either way (vilmodel.py:1377-1378 detaches the stack).
+    ("--hoist_language", None, "const", False),
 ]
 
 README_TRAIN_FLAGS = [

@@ -148,9 +148,10 @@ class DicEncoder(nn.Module):
         self.lang_units = int(os.environ.get("DASA_LANG_UNITS", "2"))   # pipe units pumped per encoder call
         self._lang_steps = 0
         self._lang_pipe = None
+        self._lang_rows = None
 
     # ------------------------------------------------------------------ language-stack cache
-    def cache_language(self, on=True, steps=0):
+    def cache_language(self, on=True, steps=0, rows=None):
         """Called by the agent at the start of every rollout (so nothing survives into the next batch).
         on: eval-mode cache (the stack is deterministic and detached: computed once per rollout).
         steps: train-mode pipeline budget. With dropout active the stack differs every step, but it
@@ -162,6 +163,7 @@ class DicEncoder(nn.Module):
         self._lang_cache = None
         self._lang_steps = int(steps)
         self._lang_pipe = None
+        self._lang_rows = rows
 
     def lang_pump(self, units=2):
         """Advance the train-mode language pipe by `units` (kept for callers; the encoder itself pumps
@@ -174,6 +176,17 @@ class DicEncoder(nn.Module):
         trainable = bert.update_lang_bert and torch.is_grad_enabled()
         if trainable:
             return None
+        if bert.training and getattr(args, "hoist_language", False):
+            # --hoist_language: one dropout draw of the stack per rollout, for the rollout's `rows`
+            # sequences (cache_language() drops it at the start of every rollout); the batched teacher
+            # encoder's T-fold repeated sequences reuse it T times
+            R, rows = ids.shape[0], self._lang_rows or ids.shape[0]
+            if self._lang_cache is None or self._lang_cache[0] != rows:
+                ext = ((1.0 - att_mask[:rows].float()) * -10000.0).unsqueeze(1).unsqueeze(2)
+                with torch.no_grad():
+                    self._lang_cache = (rows, bert.language(ids[:rows], ext))
+            out = self._lang_cache[1]
+            return out if R == rows else out.repeat(R // rows, 1, 1)
         if self._lang_cache_on and not bert.training:
             key = (ids.data_ptr(), tuple(ids.shape), ids._version, att_mask.data_ptr())
             if self._lang_cache is None or self._lang_cache[0] != key:

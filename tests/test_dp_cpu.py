@@ -35,7 +35,9 @@ def _worker(rank, world, port, q):
     sync()
     out = {k: (p.grad.clone() if p.grad is not None else None) for k, p in m.named_parameters()}
     weights = {k: p.detach().clone() for k, p in m.named_parameters()}
-    q.put((rank, local, out, weights))
+    # by value (numpy): shared-memory tensors would need this process alive until the parent reads them
+    npd = lambda d: {k: (v.numpy() if v is not None else None) for k, v in d.items()}  # noqa: E731
+    q.put((rank, npd(local), npd(out), npd(weights)))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -50,7 +52,8 @@ def test_grad_allreduce_world2():
     res = {}
     for _ in range(2):
         r, local, out, w = q.get(timeout=120)
-        res[r] = (local, out, w)
+        tt = lambda d: {k: (torch.from_numpy(v) if v is not None else None) for k, v in d.items()}  # noqa: E731
+        res[r] = (tt(local), tt(out), tt(w))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

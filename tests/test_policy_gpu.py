@@ -283,6 +283,57 @@ def test_train_iteration_grads(R, dev, deferred):
     assert n == 30
 
 
+def test_hoist_language_train(R, dev):
+    """--hoist_language (non-default): (1) with every dropout p = 0 the detached language
+    stack is deterministic, so the hoisted iteration reproduces the reference's loss and gradients
+    (cfg1 golden); (2) with dropout on, the stack runs once per rollout (twice per iteration: teacher +
+    sample) instead of once per step."""
+    param = R[0]
+    G = golden("cfg1_rollout")
+    cfg = GI.CFG1
+
+    def make(p0):
+        env = SynthR2RBatch(SynthWorld(16, 0, 3), cfg["batch"], seed=8, mode="goal", instr_len=cfg["instr_len"],
+                            variable_len=True)
+        ag = _agent(R, env, cfg["max_action"])
+        if p0:
+            for m in ag.models:
+                for sub in m.modules():
+                    if isinstance(sub, torch.nn.Dropout):
+                        sub.p = 0.0
+        ag.sample_fn = lambda p: p.argmax(-1)
+        return ag
+    param.args.ml_weight = param.args.ml_weight_org
+    param.args.hoist_language = True
+    try:
+        ag = make(True)
+        ag.zero_grad()
+        ag.accumulate_gradient("sample")
+        assert abs(ag.loss.item() - float(G["train/loss"])) < TOL * max(1.0, abs(float(G["train/loss"])))
+        ag.loss.backward()
+        n = 0
+        for name, mod in (("encoder", ag.encoder), ("decoder", ag.decoder), ("critic", ag.critic),
+                          ("adaIn", ag.adaIn)):
+            n += check_grads(G, f"train/{name}.", [(k, p.grad) for k, p in mod.named_parameters()], rtol=2e-3)
+        assert n == 30
+        counts = {}
+        for hoist in (True, False):
+            param.args.hoist_language = hoist
+            ag = make(False)
+            calls = []
+            lang = ag.encoder.bert.language
+            ag.encoder.bert.language = lambda *a, **k: (calls.append(1), lang(*a, **k))[1]
+            ag.zero_grad()
+            ag.accumulate_gradient("sample")
+            assert torch.isfinite(ag.loss).item()
+            counts[hoist] = (len(calls), ag.logs["viewsteps/teacher"][-1] + ag.logs["viewsteps/sample"][-1])
+        # one stack per rollout; the default path computes one per step (the teacher's batched encoder
+        # call over T x B sequences and the sampled rollout's language pipe)
+        assert counts[True][0] == 2, counts
+    finally:
+        param.args.hoist_language = False
+
+
 @pytest.mark.parametrize("deferred", [False, True])
 def test_finetune_train_iteration_grads(R, dev, monkeypatch, deferred):
     """cfg4 finetune path (--d_update_add_layer True): the LXRT stack and VisionEncoder are trained.
