@@ -127,7 +127,7 @@ def _pmc_traffic():
 
 
 # the committed PMC summary the roofline's `traffic` / `mfma_busy` come from (tools/pmc_summary.py)
-PMC_FILE = "profiles/r02/pmc.json"
+PMC_FILE = "profiles/r02/prof_b/pmc.json"
 
 
 def active():
