@@ -69,6 +69,7 @@ SIGNATURES = {
     "dasa_bilstm_set_mode": (i32, [i32]),
     "dasa_set_error_word": (i32, [vp]),
     "dasa_persist_force_timeout": (i32, [i32]),
+    "dasa_persist_stamps": (i32, [vp]),
     "dasa_bilstm_bwd_workspace": (i64, [i32, i32]),
     "dasa_adain_musigma_fwd": (i32, [vp, i64, vp, i64, vp, i64, vp, i32, i32, f32, vp]),
     "dasa_adain_musigma_bwd": (i32, [vp, i64, vp, i64, vp, i64, vp, i64, vp, i64, i32, i32, f32, vp]),

@@ -11,7 +11,8 @@
 // every handed-off word is stored sc1 (write-through), every storing wave drains vmcnt, the workgroup
 // barriers, ONE lane adds to the direction's arrival counter (agent-scope atomic), then polls it with
 // sc1 loads (bounded by a wall-clock limit that sets a timeout word instead of hanging); the other
-// waves join at a workgroup barrier and read the state with sc1 loads only.
+// waves join at a workgroup barrier and read the state with sc1 loads only. (A per-workgroup flag array
+// polled by one wave measured slower: profiles/r02/lstm_stamps.txt.)
 // Residency: one 1024-thread workgroup per CU, 2*H/8 <= 256 workgroups; the grid is checked against
 // the occupancy query once (the caller uses the step kernels if it would not be co-resident). The
 // callers run nothing concurrently with it (the encoder's side stream is joined before the LSTM).
@@ -97,7 +98,18 @@ struct PFwd {
   unsigned* err;          // library error word (dasa_set_error_word) or NULL
   int force_tmo;          // test hook: every barrier times out
   int B, L, H;
+  unsigned long long* stamps;   // diagnostic (dasa_persist_stamps): workgroup 0's per-step phase clocks
 };
+
+__device__ __forceinline__ void stamp(unsigned long long* buf, int i) {
+  if (buf && blockIdx.x == 0 && threadIdx.x == 0) {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    buf[i] = t;
+  }
+}
 
 // NG = H / 128: K-groups of 8 per wave (the wave's K slice is H / 16). NBT = 32-row batch tiles
 // (B <= 32 * NBT): every timestep runs the MFMA pass, the 16-wave reduction and the cell update once
@@ -131,6 +143,7 @@ __global__ __launch_bounds__(1024) void bilstm_persist_fwd_kernel(PFwd a) {
   }
   const int b = lane & 31;
   for (int s = 0; s < L; ++s) {
+    stamp(a.stamps, 8 * s);
     const int t = dir == 0 ? s : L - 1 - s;
     const float* hin = a.hbuf + (long)((s & 1) * 2 + dir) * B * H;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)hin, (short)0, B * H * 4, 0x00020000);
@@ -153,9 +166,14 @@ __global__ __launch_bounds__(1024) void bilstm_persist_fwd_kernel(PFwd a) {
             acc = __builtin_amdgcn_mfma_f32_32x32x2f32(f4e(hf[g], e), f4e(wf[g], e), acc, 0, 0, 0);
       }
       // C[b][n] partial over this wave's K slice: lane -> col n, reg r -> row (r&3) + 8(r>>2) + 4hh
+      if (bt == 0) {
+        asm volatile("" :: "v"(acc[0]));
+        stamp(a.stamps, 8 * s + 1);
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) smem[w * 1024 + r * 64 + lane] = acc[r];
       __syncthreads();
+      if (bt == 0) stamp(a.stamps, 8 * s + 2);
       {   // sum the 16 wave partials: thread i owns element i of the 32x32 tile
         float sum = 0.f;
 #pragma unroll
@@ -197,8 +215,10 @@ __global__ __launch_bounds__(1024) void bilstm_persist_fwd_kernel(PFwd a) {
       // the owners read slot 0 before the next tile's partials overwrite it
       if (bt + 1 < NBT && (bt + 1) * 32 < B) __syncthreads();
     }
+    stamp(a.stamps, 8 * s + 3);
     if (s + 1 < L && !dir_barrier(&a.sync[dir], (unsigned)(s + 1) * G, &a.sync[2], &smem[PW * 1024], a.force_tmo))
       break;
+    stamp(a.stamps, 8 * s + 4);
   }
   const bool failed = launch_failed(&a.sync[2], a.err, 1u, &smem[PW * 1024]);
   const float qnan = __builtin_nanf("");
@@ -357,10 +377,19 @@ __global__ __launch_bounds__(1024) void bilstm_persist_bwd_kernel(PBwd a) {
 // Library error word (device pointer, dasa_set_error_word) and the forced-timeout test hook.
 static unsigned* g_err_word = nullptr;
 static int g_force_tmo = 0;
+static unsigned long long* g_stamps = nullptr;
 extern "C" int dasa_set_error_word(uint32_t* dev_word) {
   g_err_word = reinterpret_cast<unsigned*>(dev_word);
   return 0;
 }
+// Diagnostic hook: when buf != NULL, workgroup 0 of every persistent forward launch writes s_memtime
+// clocks per timestep s into buf[8s + i]: i = 0 step start, 1 after the h loads + recurrent MFMAs, 2 after
+// the wave-partial exchange, 3 after the cell update / state stores, 4 after the direction barrier.
+extern "C" int dasa_persist_stamps(uint64_t* buf) {
+  g_stamps = reinterpret_cast<unsigned long long*>(buf);
+  return 0;
+}
+
 extern "C" int dasa_persist_force_timeout(int32_t on) {
   g_force_tmo = on ? 1 : 0;
   return 0;
@@ -405,7 +434,7 @@ int bilstm_persist_fwd(const float* xproj, const float* whh_fwd, const float* wh
                        float* out, float* h_n, float* c_n, float* save_act, float* save_c, int B, int L, int H,
                        float* hbuf, unsigned* sync, hipStream_t st) {
   PFwd a{xproj, whh_fwd, whh_bwd, lengths, out, save_act, save_c, h_n, c_n, hbuf, sync, g_err_word, g_force_tmo,
-         B, L, H};
+         B, L, H, g_stamps};
   const int grid = 2 * H / PU;
   if (B > 32) {
     if (H != 1024 || B > 192) return (int)hipErrorInvalidValue;

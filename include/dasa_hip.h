@@ -187,6 +187,11 @@ int dasa_bilstm_set_mode(int mode);
  * Host-only setting. dasa_persist_force_timeout(1) is a test hook: every barrier times out. */
 int dasa_set_error_word(uint32_t* dev_word);
 int dasa_persist_force_timeout(int32_t on);
+/* Diagnostic: buf (device, >= 8 * L uint64 words) != NULL makes workgroup 0 of every persistent bi-LSTM
+ * forward launch record s_memtime clocks per timestep s at buf[8s + i] (i = 0 step start, 1 after the
+ * recurrent MFMAs, 2 after the partial-sum exchange, 3 after the cell update, 4 after the barrier);
+ * NULL turns it off. Host-only setting, not used by the product path. */
+int dasa_persist_stamps(uint64_t* buf);
 int dasa_bilstm_hprev(const float* out, float* hprev, int32_t B, int32_t L, int32_t H, void* stream);
 
 /* ---- AdaIN mu/sigma (model.py:1822-1840, adaIn_type default) ---------------------------------
