@@ -8,7 +8,9 @@ bracketed by HIP events, so the per-launch time excludes host launch latency (in
 same kernels sit between dependent kernels, where the host is ahead of the GPU). `bytes` is the
 algorithmic (compulsory) traffic per launch: every input read once, every output written once. At B=20
 a launch's working set (3-34 MB) stays resident in the 256 MB Infinity Cache across replays, so those
-rates are cache-assisted; B=256 (80-330 MB per launch) streams from HBM."""
+rates are cache-assisted; B=256 (80-330 MB per launch) streams from HBM. `step_chain` replays one decision
+step's AdaIN gate + shift / instruction / candidate attention back to back; `launch_floor` is a kernel
+with no work to speak of, the per-launch time no kernel gets under."""
 import torch
 
 from . import ops
@@ -78,6 +80,13 @@ def _cases(B, dev):
     cases.append(("ada_gate_bwd", 16.0 * R * F, lambda: ops.ada_gate_bwd(dout[:, :F], s, f[:, :F], noise)))
     # mu/sigma AdaIN (adaIn_type default, model.py:1822-1840) on the same rows
     cases.append(("adain_musigma", 12.0 * R * F, lambda: ops.adain_musigma(f[:, :F], dout[:, :F], out=out[:, :F])))
+    # the decision step's AdaIN + attention chain as it runs per step (gate, shift, instruction SoftDot,
+    # candidate logits back to back): its bytes over its time
+    chain = [c for c in cases if c[0] in ("ada_gate", "shift_attn", "softdot", "cand_logit")]
+    cases.append(("step_chain", sum(c[1] for c in chain), lambda: [c[2]() for c in chain]))
+    # launch floor: a one-row column scale (8 KB) — the time any launch takes inside a replayed graph
+    f1, o1 = rnd(1, F), torch.empty(1, F, device=dev)
+    cases.append(("launch_floor", 8.0 * F, lambda: ops.colscale(f1, noise, o1)))
     return cases
 
 
