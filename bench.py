@@ -268,7 +268,8 @@ def main():
     out = {
         "metric": "agent decision-steps/sec at B=20, 36x2048 feats, maxAction=35; 1/2/4/8 MI355X",
         "value": round(value, 2), "unit": "agent-decisions/s", "n_gpus": world, "steps": a.steps,
-        "warmup": a.warmup, "ms_per_step": round(1000 * dt / a.steps, 2), "higher_is_better": True,
+        "warmup": a.warmup, "ms_per_step": round(1000 * dt / a.steps, 2),
+        "batched_steps_per_s": round(value / (a.batch * world), 2), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
         "config": {"workload": "cfg2 auglistener training iteration (teacher + sample rollout, backward, "
                                "grad all-reduce, RMSprop), README flags",

@@ -90,9 +90,23 @@ def _cases(B, dev):
     return cases
 
 
+def hbm_stream(rows=131072, cols=2048):
+    """Peak check (confirm the datasheet 8 TB/s on the box): a 1 GiB -> 1 GiB column
+    scale (ops.colscale, float4 streaming) timed back to back in a graph; returns GB/s of read + write."""
+    dev = torch.device("cuda", torch.cuda.current_device())
+    x = torch.rand(rows, cols, device=dev)
+    y = torch.empty_like(x)
+    s = torch.rand(cols, device=dev)
+    us = _time_graph(lambda: ops.colscale(x, s, y), reps=10)
+    nbytes = 8.0 * rows * cols
+    del x, y
+    return {"us": round(us, 1), "bytes": int(nbytes), "GB/s": round(nbytes / (us * 1e-6) / 1e9, 1),
+            "frac": round(nbytes / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+
+
 def hbm_kernels(batches=(20, 256)):
     dev = torch.device("cuda", torch.cuda.current_device())
-    res = {}
+    res = {"hbm_stream": hbm_stream()}
     for B in batches:
         for name, nbytes, fn in _cases(B, dev):
             us = _time_graph(fn)

@@ -84,3 +84,51 @@ def test_speaker_infer_batch_vs_reference(dev):
         assert np.array_equal(np.asarray(insts), G["spk/insts"])
     finally:
         param.readme_train(["--d_vl_layers", "1", "--batchSize", "2", "--maxAction", "5"])
+
+
+@pytest.mark.gpu
+def test_speaker_featdropmask_and_sampling(dev):
+    """The shared env-drop mask path (speaker.py:293-295, ops.colscale on the RGB columns): an all-ones
+    mask reproduces the unmasked instructions and a zero mask changes the context; sampled decoding
+    yields vocabulary ids with <PAD> after each row's <EOS>."""
+    cfg = GI.SPEAKER
+    from dasa_amd.r2r import param
+    param.readme_train(["--maxDecode", str(cfg["max_decode"]), "--batchSize", str(cfg["batch"])])
+    try:
+        from dasa_amd.r2r import agent_dg, speaker
+        from dasa_amd.synth import SynthR2RBatch, SynthWorld, init_params
+        import contextlib
+        import io
+        world = SynthWorld(cfg["viewpoints"], 0, cfg["graph_seed"])
+
+        def make():
+            env = SynthR2RBatch(world, cfg["batch"], seed=cfg["env_seed"], mode="goal", instr_len=80,
+                                variable_len=True)
+            with contextlib.redirect_stdout(io.StringIO()):
+                listener = agent_dg.Seq2SeqAgent(env, "", None, 5, "Dic")
+            spk = speaker.Speaker(env, listener, _tok())
+            init_params(spk.encoder, cfg["seed_enc"])
+            init_params(spk.decoder, cfg["seed_dec"])
+            env.reset()
+            return spk
+        base = make().infer_batch()
+        ones = make().infer_batch(featdropmask=torch.ones(2048, device=dev))
+        assert np.array_equal(base, ones)
+        ctxs = []
+        for m in (torch.ones(2048, device=dev), torch.zeros(2048, device=dev)):
+            spk = make()
+            fwd = spk.encoder.forward
+            spk.encoder.forward = lambda *a, _f=fwd, **k: (ctxs.append(_f(*a, **k)), ctxs[-1])[1]
+            spk.infer_batch(featdropmask=m)
+        assert not torch.allclose(ctxs[0], ctxs[1])
+        spk = make()
+        w2i = spk.tok.word_to_index
+        insts = spk.infer_batch(sampling=True)
+        assert insts.dtype.kind in "iu" and insts.min() >= 0 and insts.max() < spk.tok.vocab_size()
+        assert not (insts == w2i["<UNK>"]).any()
+        for row in insts:
+            eos = np.nonzero(row == w2i["<EOS>"])[0]
+            if len(eos):
+                assert (row[eos[0] + 1:] == w2i["<PAD>"]).all()
+    finally:
+        param.readme_train(["--d_vl_layers", "1", "--batchSize", "2", "--maxAction", "5"])
