@@ -27,6 +27,12 @@ from . import _lib
 from . import prof
 
 ENABLED = os.environ.get("DASA_GRAPH", "1") != "0"
+_NESTED = [0]    # > 0 while an enclosing region is being warmed up / captured: inner regions run inline
+
+
+def capturing():
+    """True while a StepGraphs region is being captured (or warmed up for capture)."""
+    return _NESTED[0] > 0
 
 
 class _Entry:
@@ -66,21 +72,25 @@ class StepGraphs:
         # and the GEMM / attention workspaces, which ops.py keys by stream) outside the capture, as
         # torch.cuda.graphs requires; the capture then reuses them (one workspace per StepGraphs)
         self.stream.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(self.stream), torch.no_grad():
-            fn(*static_in)
-        torch.cuda.current_stream().wait_stream(self.stream)
-        torch.cuda.synchronize(dev)
-        g = torch.cuda.CUDAGraph()
-        L = _lib.lib()
-        ctr = ctypes.c_void_p(self.counter.data_ptr())
-        L.dasa_set_seed_source(ctr)
+        _NESTED[0] += 1
         try:
-            with torch.cuda.graph(g, stream=self.stream), torch.no_grad():
-                _lib.check(L.dasa_seed_bump(ctr, ctypes.c_void_p(self.stream.cuda_stream)),
-                           "dasa_seed_bump")
-                out = fn(*static_in)
+            with torch.cuda.stream(self.stream), torch.no_grad():
+                fn(*static_in)
+            torch.cuda.current_stream().wait_stream(self.stream)
+            torch.cuda.synchronize(dev)
+            g = torch.cuda.CUDAGraph()
+            L = _lib.lib()
+            ctr = ctypes.c_void_p(self.counter.data_ptr())
+            L.dasa_set_seed_source(ctr)
+            try:
+                with torch.cuda.graph(g, stream=self.stream), torch.no_grad():
+                    _lib.check(L.dasa_seed_bump(ctr, ctypes.c_void_p(self.stream.cuda_stream)),
+                               "dasa_seed_bump")
+                    out = fn(*static_in)
+            finally:
+                L.dasa_set_seed_source(None)
         finally:
-            L.dasa_set_seed_source(None)
+            _NESTED[0] -= 1
         e = _Entry()
         e.graph, e.static_in, e.static_out = g, static_in, out
         e.pkey = self._param_key()
@@ -89,7 +99,9 @@ class StepGraphs:
 
     def run(self, key, fn, inputs):
         """fn(*inputs) -> tuple of tensors, forward-only; returns fresh copies of its outputs."""
-        if prof.active():     # per-launch HIP-event profiling (bench.py's kernel table) runs eagerly
+        if prof.active() or _NESTED[0]:
+            # per-launch HIP-event profiling (bench.py's kernel table) runs eagerly; inside an enclosing
+            # region's capture this region becomes part of that graph
             with torch.no_grad():
                 return fn(*inputs)
         e = self.entries.get(key)

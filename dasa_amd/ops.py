@@ -683,6 +683,8 @@ def register_concurrent_stream(st):
 
 
 def _exclusive(dev):
+    if torch.cuda.is_current_stream_capturing():
+        return      # a captured region is joined before its replay (Seq2SeqAgent's step graph)
     cur = torch.cuda.current_stream(dev)
     for st in _CONCURRENT:
         if st.device == dev and st != cur:

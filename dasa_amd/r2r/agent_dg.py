@@ -23,7 +23,9 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import functional as DF
+from .. import graph
 from .. import ops
+from .. import prof
 from . import model
 from . import utils
 from .param import args
@@ -193,6 +195,7 @@ class Seq2SeqAgent(BaseAgent):
         self.criterion = nn.CrossEntropyLoss(ignore_index=args.ignoreid, reduction="sum")
         self.logs = defaultdict(list)
         self.sample_fn = None        # test hook: probs -> actions, replaces Categorical sampling
+        self._step_graphs = None     # captured forward-only decision steps (_graph_step)
         self.grad_sync = None        # data-parallel hook set by dasa_amd.dp
 
     def _load_pretrained_bert(self, path):
@@ -425,16 +428,65 @@ class Seq2SeqAgent(BaseAgent):
                 cat([p[3].reshape(-1, p[3].shape[-1]) for p in parts]),
                 cat([p[4].reshape(-1, p[4].shape[-1]) for p in parts]), cinfo)
 
-    def _encode_steps(self, obs_steps, seq, seq_mask, lens_dev, noise, consistent_drop):
+    def _graph_step_ok(self, t, consistent_drop, noise, speaker):
+        """A forward-only argmax decision step (eval rollouts) whose whole device work — AdaIN, the
+        encoder (VisionEncoder + LXRT + bi-LSTM + init projections), the decoder and the policy head —
+        replays as ONE captured hipGraph (dasa_amd/graph.py), keyed by the candidate count: every step
+        after the first of a rollout, once the rollout's language stack is cached."""
+        enc = self.encoder
+        return (graph.ENABLED and t > 0 and self.feedback == "argmax" and not torch.is_grad_enabled()
+                and not enc.training and not self.decoder.training and speaker is None
+                and not (consistent_drop and noise is not None) and not args.submit and not args.pred_back
+                and self.sample_fn is None and os.environ.get("DASA_FUSED_HEAD", "1") != "0"
+                and os.environ.get("DASA_STEP_GRAPH", "1") != "0"
+                and enc._lang_cache_on and enc._lang_cache is not None and not prof.active()
+                # a caller that wraps or hooks the modules observes every per-step call: run eagerly
+                and all("forward" not in m.__dict__ and not m._forward_hooks and not m._forward_pre_hooks
+                        for m in (enc, self.decoder, self.adaIn)))
+
+    def _graph_step(self, perm_obs, target, h_t, h1, c_t, seq, seq_mask, lens_dev, ctx_mask):
+        """agent_dg.py:725-886 for one argmax step as a graph replay. The observation gather (host index
+        arrays -> dasa_gather_rows) stays outside the graph; the replay reads the gathered blocks, the
+        recurrent state, the rollout's cached language stack and the step's host-built candidate lengths
+        / teacher targets from its static buffers. Returns (candidate lengths, (h_t, c_t, logit, h1,
+        ce, log-prob of the action, action))."""
+        inputs = self._step_inputs([perm_obs])
+        a, f, d, cf, cd, cinfo = inputs
+        _, C, leng = cinfo[0]
+        B = a.shape[0]
+        cand_lens = self._lens_dev(leng)
+        text = self.encoder._lang_cache[1]
+        if self._step_graphs is None:
+            self._step_graphs = graph.StepGraphs([self.encoder, self.decoder, self.adaIn])
+
+        def step(a, f, d, cf, cd, seq, seq_mask, lens_dev, h_t, h1, c_t, ctx_mask, cand_lens, target, text):
+            self.encoder._text_in = text
+            try:
+                (e,) = self._encode_steps(None, seq, seq_mask, lens_dev, None, False,
+                                          inputs=(a, f, d, cf, cd, [(0, C, leng)]))
+            finally:
+                self.encoder._text_in = None
+            h_t2, c_t2, logit, h1_2, _ = self.decoder(e["a"], e["df"], e["cand"], h_t, h1, c_t, e["ctx"], ctx_mask,
+                                                      already_dropfeat=False)
+            ce, _, lpa, a_dev = DF.policy_head(logit, cand_lens, target, "argmax")
+            return h_t2, c_t2, logit, h1_2, ce, lpa, a_dev
+        ops._exclusive(self.device)
+        outs = self._step_graphs.run((B, C, seq.shape[1]), step, (a, f, d, cf, cd, seq, seq_mask, lens_dev, h_t, h1,
+                                                                  c_t, ctx_mask, cand_lens, target, text))
+        return leng, outs
+
+    def _encode_steps(self, obs_steps, seq, seq_mask, lens_dev, noise, consistent_drop, inputs=None):
         """Feature stage of the step loop (agent_dg.py:725-805): features -> env drop -> AdaIN ->
         DicEncoder, for one or several steps' observations at once (every op in it is per row, so
         stacking T steps along the batch computes each step's values; dropout draws stay independent
         per row and step). Returns per step: angle input, AdaIN'd panorama, AdaIN'd candidates,
         candidate lengths, ctx and the encoder's decoder-init states."""
-        T = len(obs_steps)
-        B = len(obs_steps[0])
         angle = args.angle_feat_size
-        input_a_t, f_t, d_t, candidate_feat, candidate_dfeat, cinfo = self._step_inputs(obs_steps)
+        if inputs is None:
+            inputs = self._step_inputs(obs_steps)
+        input_a_t, f_t, d_t, candidate_feat, candidate_dfeat, cinfo = inputs
+        T = len(cinfo)
+        B = input_a_t.shape[0] // T
         stage = args.env_drop_stage
         use_noise = consistent_drop and noise is not None
         all_img_feats = f_t                  # the raw panorama (agent_dg.py:730)
@@ -589,6 +641,26 @@ class Seq2SeqAgent(BaseAgent):
                 # reference builds them after the decoder with blocking copies; same values)
                 target_np = self._teacher_action_np(perm_obs, ended)
                 target = self._to_dev(target_np)
+                if self._graph_step_ok(t, consistent_drop, noise, speaker):
+                    candidate_leng, (h_t, c_t, logit, h1, ce, lpa, a_t) = self._graph_step(
+                        perm_obs, target, h_t, h1, c_t, *enc_args[:3], ctx_mask)
+                    hidden_states.append(h_t)
+                    total_forth_loss += ce
+                    policy_log_probs.append(lpa.unsqueeze(1))
+                    cpu_a_t = a_t.cpu().numpy().copy()      # the step's one device->host sync
+                    for i, next_id in enumerate(cpu_a_t):
+                        if next_id == (candidate_leng[i] - 1) or next_id == args.ignoreid:
+                            cpu_a_t[i] = -1
+                    self.make_equiv_action(cpu_a_t, perm_obs, perm_idx, traj)
+                    obs = np.array(self.env._get_obs())
+                    perm_obs = obs[perm_idx]
+                    reward, mask = self._step_reward(perm_obs, cpu_a_t, ended, last_dist)
+                    rewards.append(reward)
+                    masks.append(mask)
+                    ended[:] = np.logical_or(ended, (cpu_a_t == -1))
+                    if ended.all():
+                        break
+                    continue
                 (e,) = self._encode_steps([perm_obs], *enc_args)
                 candidate_leng = e["leng"]
                 ctx = e["ctx"]

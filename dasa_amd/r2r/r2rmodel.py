@@ -149,6 +149,7 @@ class DicEncoder(nn.Module):
         self._lang_steps = 0
         self._lang_pipe = None
         self._lang_rows = None
+        self._text_in = None
 
     # ------------------------------------------------------------------ language-stack cache
     def cache_language(self, on=True, steps=0, rows=None):
@@ -176,6 +177,8 @@ class DicEncoder(nn.Module):
         trainable = bert.update_lang_bert and torch.is_grad_enabled()
         if trainable:
             return None
+        if self._text_in is not None:     # a captured decision step passes the rollout's stack in
+            return self._text_in
         if bert.training and getattr(args, "hoist_language", False):
             # --hoist_language: one dropout draw of the stack per rollout, for the rollout's `rows`
             # sequences (cache_language() drops it at the start of every rollout); the batched teacher

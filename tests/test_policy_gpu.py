@@ -750,3 +750,47 @@ def test_checkpoint_roundtrip(R, dev, tmp_path):
     assert len(a) == len(b)
     for x, y in zip(a, b):
         assert torch.equal(x["logit"], y["logit"]) and torch.equal(x["value"], y["value"])
+
+
+@pytest.mark.parametrize("cfg_name", ["cfg1", "cfg2"])
+def test_step_graph_matches_eager(R, dev, cfg_name, monkeypatch):
+    """Forward-only argmax rollouts replay every decision step after the first as ONE captured hipGraph
+    (Seq2SeqAgent._graph_step: AdaIN, encoder, decoder and policy head). Against the same rollout run
+    eagerly (DASA_STEP_GRAPH=0): identical trajectories, the summed per-step CE within 1e-5, and the
+    graphs were captured and replayed."""
+    param = R[0]
+    if cfg_name == "cfg1":
+        cfg = GI.CFG1
+
+        def env():
+            return SynthR2RBatch(SynthWorld(16, 0, 3), cfg["batch"], seed=7, mode="goal", instr_len=cfg["instr_len"],
+                                 variable_len=True)
+        T = cfg["max_action"]
+    else:
+        cfg = GI.CFG2
+        param.readme_train(["--d_vl_layers", str(cfg["vl_layers"]), "--batchSize", str(cfg["batch"]),
+                            "--maxAction", "12"])
+
+        def env():
+            return SynthR2RBatch(SynthWorld(32, 0, 5), cfg["batch"], seed=11, mode="wander", instr_len=80)
+        T = 12
+    try:
+        res = {}
+        for mode in ("0", "1"):
+            monkeypatch.setenv("DASA_STEP_GRAPH", mode)
+            ag = _agent(R, env(), T)
+            ag.feedback = "argmax"
+            ag.loss = 0
+            for m in (ag.encoder, ag.decoder, ag.critic):
+                m.eval()
+            with torch.no_grad():
+                traj = ag.vl_rollout(train_ml=None, train_rl=False, reset=True)
+            res[mode] = (traj, float(ag.logs["ml_loss"][-1]) if ag.logs.get("ml_loss") else None,
+                         ag._step_graphs)
+        (t0, l0, g0), (t1, l1, g1) = res["0"], res["1"]
+        assert g0 is None and g1 is not None and g1.captures >= 1 and g1.replays >= 1
+        assert [x["path"] for x in t0] == [x["path"] for x in t1]
+        if l0 is not None:
+            assert abs(l0 - l1) <= 1e-5 * max(1.0, abs(l0)), (l0, l1)
+    finally:
+        param.readme_train(["--d_vl_layers", "1", "--batchSize", "2", "--maxAction", "5"])
