@@ -104,6 +104,10 @@ class StepGraphs:
             # region's capture this region becomes part of that graph
             with torch.no_grad():
                 return fn(*inputs)
+        from . import ops
+        # the GEMM numerics mode is part of what a graph captured (bf16 operands for configs[4], the
+        # bf16x6 fp32 emulation switch): a replay in another mode would run the captured one
+        key = (key, ops._BF16["on"], ops._EMU["on"], ops._EMU["min_rows"])
         e = self.entries.get(key)
         if e is not None and e.pkey != self._param_key():
             del self.entries[key]

@@ -794,3 +794,23 @@ def test_step_graph_matches_eager(R, dev, cfg_name, monkeypatch):
             assert abs(l0 - l1) <= 1e-5 * max(1.0, abs(l0)), (l0, l1)
     finally:
         param.readme_train(["--d_vl_layers", "1", "--batchSize", "2", "--maxAction", "5"])
+
+
+def test_graph_cache_keyed_by_numerics_mode(R, dev):
+    """Captured regions are keyed by the GEMM numerics mode: an fp32 rollout after a bf16 one on the same
+    agent replays fp32 graphs (its logits equal a fresh agent's fp32 rollout), not the bf16 captures."""
+    cfg = GI.CFG1
+
+    def env():
+        return SynthR2RBatch(SynthWorld(16, 0, 3), cfg["batch"], seed=7, mode="goal", instr_len=cfg["instr_len"],
+                             variable_len=True)
+    ag = _agent(R, env(), cfg["max_action"])
+    r16, _ = _record_eval(ag, "argmax", bf16=True)
+    ag.env = env()
+    r32, _ = _record_eval(ag, "argmax")
+    ag2 = _agent(R, env(), cfg["max_action"])
+    ref, _ = _record_eval(ag2, "argmax")
+    assert len(r32) == len(ref)
+    for a, b in zip(r32, ref):
+        assert torch.allclose(a["logit"], b["logit"], rtol=1e-6, atol=1e-6)
+    assert any(not torch.allclose(a["logit"], b["logit"], rtol=1e-6, atol=1e-6) for a, b in zip(r16, ref))
