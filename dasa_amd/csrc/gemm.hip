@@ -1323,6 +1323,252 @@ __global__ void f32_to_bf16_kernel(const float* __restrict__ x, unsigned* __rest
   }
 }
 
+// ------------------------------------------------------------------------------- skinny GEMMs
+// The per-step decoder / critic / attention projections at B <= 32 rows (model.py:263-264, 437,
+// 970-982; M = 20 at the headline batch) and their input gradients dX = dY.W are weight streaming:
+// every weight element is used M <= 32 times, so the kernel's job is to read W once at HBM rate.
+// The f32 MFMA 16x16x4 runs with the WEIGHT on the 16-row side and the activations (M padded to 16 or
+// 32) on the 16-column side, so both operands come straight from global memory in float4 per lane
+// (K-permuted: in each 32-deep step, lane group g = lane >> 4 supplies k = 8g + e to MFMA e): no LDS
+// staging of W, no cross-lane reduction, one HBM pass. A workgroup of 4 waves splits its K range
+// between the waves (summed through LDS in fixed order); K ranges beyond one workgroup are split over
+// blockIdx.y with the partials handed to the last-arriving workgroup (write-through stores, agent
+// ticket, fixed-order sum: deterministic), which runs the fused epilogue.
+struct SkinnyP {
+  unsigned* cnt;   // per-column-block arrival counters (workspace head; zero on entry, re-armed)
+  float* slab;     // split partials: [cols][splits][NACC][64 lanes] float4
+  int splits;
+};
+
+// Fused epilogue of a lane's E output elements (m[e], n[e]): every optional operand is gathered for
+// all E elements inside one uniform branch before it is used (a per-element branch around a load
+// makes the compiler wait for each load in turn).
+template <int E>
+__device__ __forceinline__ void skinny_store(const GemmP& p, const int (&m)[E], const int (&n)[E], float (&v)[E]) {
+  int mc[E], nc[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    mc[e] = min(m[e], p.M - 1);
+    nc[e] = min(n[e], p.N - 1);
+    v[e] *= p.alpha;
+  }
+  if (p.bias) {
+    float b[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) b[e] = p.bias[nc[e]];
+#pragma unroll
+    for (int e = 0; e < E; ++e) v[e] += b[e];
+  }
+  if (p.act != DASA_ACT_NONE) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) v[e] = apply_act(v[e], p.act);
+  }
+  if (p.aux) {
+    float a[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) a[e] = p.aux[(long)mc[e] * p.ld_aux + nc[e]];
+#pragma unroll
+    for (int e = 0; e < E; ++e) v[e] *= a[e];
+  }
+  if (p.colscale) {
+    float c[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) c[e] = p.colscale[nc[e]];
+#pragma unroll
+    for (int e = 0; e < E; ++e) v[e] *= c[e];
+  }
+  if (p.beta != 0.f) {
+    float c[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) c[e] = p.C[(long)mc[e] * p.ldc + nc[e]];
+#pragma unroll
+    for (int e = 0; e < E; ++e) v[e] += p.beta * c[e];
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e)
+    if (m[e] < p.M && n[e] < p.N) p.C[(long)m[e] * p.ldc + n[e]] = v[e];
+}
+
+// Sum the 4 waves' accumulators (fixed order), then either run the epilogue (one split) or hand the
+// workgroup partial to the last arriver of its column block. Returns true in the wave that holds the
+// final sum (wave 0 of the single / last-arriving workgroup); acc then holds it.
+template <int NACC>
+__device__ __forceinline__ bool skinny_reduce(floatx4 (&acc)[NACC], const SkinnyP& sp, int col, int split) {
+  __shared__ floatx4 red[3][NACC][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (w > 0) {
+#pragma unroll
+    for (int a = 0; a < NACC; ++a) red[w - 1][a][lane] = acc[a];
+  }
+  __syncthreads();
+  if (w > 0) return false;
+#pragma unroll
+  for (int v = 0; v < 3; ++v)
+#pragma unroll
+    for (int a = 0; a < NACC; ++a) acc[a] += red[v][a][lane];
+  if (sp.splits == 1) return true;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(sp.slab, 0, 0x7fffffff, 0x00020000);
+  const long base = (long)col * sp.splits;
+#pragma unroll
+  for (int a = 0; a < NACC; ++a) {
+    const int off = (int)((((base + split) * NACC + a) * 64 + lane) * 16);
+    const u32x4 u = {__float_as_uint(acc[a][0]), __float_as_uint(acc[a][1]), __float_as_uint(acc[a][2]),
+                     __float_as_uint(acc[a][3])};
+    __builtin_amdgcn_raw_buffer_store_b128(u, rs, off, 0, 16);   // sc1: write-through
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  unsigned t = 0;
+  if (lane == 0) t = __hip_atomic_fetch_add(sp.cnt + col, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  t = __shfl(t, 0, 64);
+  if (t != (unsigned)(sp.splits - 1)) return false;
+  if (lane == 0) __hip_atomic_store(sp.cnt + col, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler-only: sc1 loads below the ticket
+#pragma unroll
+  for (int a = 0; a < NACC; ++a) acc[a] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int s2 = 0; s2 < sp.splits; ++s2) {   // fixed order: deterministic whoever arrives last
+#pragma unroll
+    for (int a = 0; a < NACC; ++a) {
+      const int off = (int)((((base + s2) * NACC + a) * 64 + lane) * 16);
+      const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);   // sc1
+      acc[a][0] += __uint_as_float(u.x);
+      acc[a][1] += __uint_as_float(u.y);
+      acc[a][2] += __uint_as_float(u.z);
+      acc[a][3] += __uint_as_float(u.w);
+    }
+  }
+  return true;
+}
+
+__device__ __forceinline__ float4 ldg4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+// NT: Y[M,N] = epi(X[M,K] . W[N,K]^T). Workgroup = 16 output features (rows of W) x 4 waves x KS
+// 32-deep steps per wave; MFMA rows = features, columns = the M <= 16*MT activation rows.
+// Lane (r = lane & 15, g = lane >> 4) loads W[n0 + r][k .. k+7] and X[16t + r][k .. k+7], k = step*32 + 8g.
+template <int MT, int KS>
+__global__ __launch_bounds__(256, 2) void gemm_skinny_nt_kernel(GemmP p, SkinnyP sp) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, g = lane >> 4;
+  const int col = blockIdx.x, split = blockIdx.y, n0 = col * 16;
+  const int K = p.K, kq = K - 4;   // last whole quad (K % 4 == 0)
+  const float* wrow = p.B + (long)min(n0 + r, p.N - 1) * p.ldb;
+  const float* xrow[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) xrow[t] = p.A + (long)min(16 * t + r, p.M - 1) * p.lda;
+  const int kbase = (split * 4 + w) * KS * 32 + 8 * g;
+  // every load first (clamped, unconditional: out-of-range quads re-read the last one and are zeroed
+  // below), so each wave has KS x 2 KB of W in flight
+  float4 wv[KS][2], xv[KS][MT][2];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int k = kbase + 32 * s;
+    wv[s][0] = ldg4(wrow + min(k, kq));
+    wv[s][1] = ldg4(wrow + min(k + 4, kq));
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      xv[s][t][0] = ldg4(xrow[t] + min(k, kq));
+      xv[s][t][1] = ldg4(xrow[t] + min(k + 4, kq));
+    }
+  }
+  // keep every load above the MFMAs (the scheduler would otherwise sink each load to its use and
+  // leave one step in flight); the waitcnt pass then waits step by step
+  __builtin_amdgcn_sched_barrier(0);
+  floatx4 acc[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int k = kbase + 32 * s;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const bool ok = k + 4 * h < K;
+      const float4 a = sel4(ok, wv[s][h]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(f4get(a, e), f4get(sel4(ok, xv[s][t][h]), e), acc[t], 0, 0, 0);
+      }
+    }
+  }
+  if (!skinny_reduce<MT>(acc, sp, col, split)) return;
+  // C[feature = 4g + j][act row = r]  ->  Y[16t + r][n0 + 4g + j]
+  int mm[4 * MT], nn[4 * MT];
+  float v[4 * MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      mm[4 * t + j] = 16 * t + r;
+      nn[4 * t + j] = n0 + 4 * g + j;
+      v[4 * t + j] = acc[t][j];
+    }
+  skinny_store<4 * MT>(p, mm, nn, v);
+}
+
+// NN: Y[M,N] = epi(X[M,K] . B[K,N]) with B row-major (ldb) - the input gradient dX = dY . W of an
+// nn.Linear (W [out, in] read along its rows). Workgroup = 64 output columns x 4 waves x KS steps.
+// Lane (r, g) loads B[k + e][n0 + 4r .. +3] for e = 0..7 (k = step*32 + 8g: four 256-B row pieces per
+// instruction) and X[16t + r][k .. k+7]; MFMA (e, c) takes component c of the B quad as the 16-row
+// operand, so accumulator c holds output columns n0 + 4*row + c.
+template <int MT, int KS>
+__global__ __launch_bounds__(256, 2) void gemm_skinny_nn_kernel(GemmP p, SkinnyP sp) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, g = lane >> 4;
+  const int col = blockIdx.x, split = blockIdx.y, n0 = col * 64;
+  const int K = p.K, kq = K - 4;
+  const float* bcol = p.B + min(n0 + 4 * r, p.N - 4);
+  const float* xrow[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) xrow[t] = p.A + (long)min(16 * t + r, p.M - 1) * p.lda;
+  const int kbase = (split * 4 + w) * KS * 32 + 8 * g;
+  float4 bv[KS][8], xv[KS][MT][2];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int k = kbase + 32 * s;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bv[s][e] = ldg4(bcol + (long)min(k + e, K - 1) * p.ldb);
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      xv[s][t][0] = ldg4(xrow[t] + min(k, kq));
+      xv[s][t][1] = ldg4(xrow[t] + min(k + 4, kq));
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  floatx4 acc[4 * MT];
+#pragma unroll
+  for (int a = 0; a < 4 * MT; ++a) acc[a] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int k = kbase + 32 * s;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const bool ok = k + e < K;
+      const float4 b = sel4(ok, bv[s][e]);
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const float xs = ok ? f4get(xv[s][t][e >> 2], e & 3) : 0.f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          acc[4 * t + c] = __builtin_amdgcn_mfma_f32_16x16x4f32(f4get(b, c), xs, acc[4 * t + c], 0, 0, 0);
+      }
+    }
+  }
+  if (!skinny_reduce<4 * MT>(acc, sp, col, split)) return;
+  // accumulator (t, c): C[row = 4g + j][act row = r]  ->  Y[16t + r][n0 + 16g + 4j + c]
+  int mm[16 * MT], nn[16 * MT];
+  float v[16 * MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int e = 16 * t + 4 * j + c;
+        mm[e] = 16 * t + r;
+        nn[e] = n0 + 16 * g + 4 * j + c;
+        v[e] = acc[4 * t + c][j];
+      }
+  skinny_store<16 * MT>(p, mm, nn, v);
+}
+
 }  // namespace
 
 struct Plan { int cfg, splitk, kchunk; int64_t ws; int sk_grid, sk_dp, sk_tiles, sk_ipt; int group_m; };
@@ -1440,6 +1686,100 @@ static Plan make_plan(const dasa_gemm_desc* d) {
   return pl;
 }
 
+// Skinny plan (gemm_skinny_*_kernel): M <= 32, one batch, X K-contiguous, W either [N][K] (NT, the
+// nn.Linear forward) or [K][N] (NN, dX = dY . W), 16-B aligned float4-able rows. KS (32-deep steps per
+// wave) is the largest that still gives >= `target` waves (default 1024 = 4 per CU: enough W requests
+// in flight to stream HBM), the K range left over is split across workgroups.
+struct SkinnyPlan { bool ok, nn; int mt, ks, cols, splits; int64_t ws; };
+static int g_skinny_waves = -2;   // DASA_SKINNY_WAVES=<n>: target wave count; 0 disables the skinny kernels
+static int g_skinny_ks = -2;      // DASA_SKINNY_KS=<1|2|4|8>: pin KS (sweeps)
+
+static SkinnyPlan skinny_plan(const dasa_gemm_desc* d) {
+  if (g_skinny_waves == -2) {
+    const char* e = getenv("DASA_SKINNY_WAVES");
+    g_skinny_waves = e ? atoi(e) : -1;
+    const char* e2 = getenv("DASA_SKINNY_KS");
+    g_skinny_ks = e2 ? atoi(e2) : -1;
+  }
+  SkinnyPlan sp{};
+  const int M = d->M, N = d->N, K = d->K;
+  if (g_skinny_waves == 0 || d->batch > 1 || M < 1 || M > 32 || N < 1 || d->opA != 0 || K < 4 || (K & 3)) return sp;
+  const bool nn = d->opB == 0;
+  const uintptr_t am = (uintptr_t)d->A | (uintptr_t)d->B;
+  if ((am & 15) || (d->lda & 3) || (d->ldb & 3) || (nn && (N & 3))) return sp;
+  sp.nn = nn;
+  sp.mt = M <= 16 ? 1 : 2;
+  const long ksteps = cdiv(K, 32);
+  sp.cols = (int)(nn ? cdiv(N, 64) : cdiv(N, 16));
+  // target: 1024 waves for the NT form at M > 16, 512 otherwise (tools/skinny_probe.py sweep,
+  // profiles/r02/skinny_probe.txt); the first KS from the top that reaches it while padding the K range
+  // by <= 10 % (K steps beyond K still issue their MFMAs on zeros)
+  const long target = g_skinny_waves > 0 ? g_skinny_waves : (!nn && sp.mt == 2 ? 1024 : 512);
+  const int kmax = nn ? (sp.mt == 2 ? 2 : 4) : 8;
+  int ks = kmax;
+  for (; ks > 1; ks >>= 1) {
+    const long spl = cdiv(ksteps, 4 * ks);
+    if ((long)sp.cols * spl * 4 >= target && (spl * 4 * ks - ksteps) * 10 <= ksteps) break;
+  }
+  if (g_skinny_ks > 0) {
+    ks = 1;
+    while (ks * 2 <= g_skinny_ks && ks * 2 <= kmax) ks *= 2;
+  }
+  sp.ks = ks;
+  const long splits = cdiv(ksteps, 4 * ks);
+  const int nacc = nn ? 4 * sp.mt : sp.mt;
+  const int64_t slab = (int64_t)sp.cols * splits * nacc * 64 * 16;
+  if (splits > 65535 || (splits > 1 && (sp.cols > kCntWords || slab >= (1LL << 31)))) return sp;
+  sp.splits = (int)splits;
+  sp.ws = splits > 1 ? kCntBytes + slab : 0;
+  sp.ok = true;
+  return sp;
+}
+
+template <int MT, int KS>
+static void skinny_launch(bool nn, dim3 grid, hipStream_t st, const GemmP& p, const SkinnyP& s) {
+  if constexpr (KS <= 4) {
+    if (nn) {
+      hipLaunchKernelGGL((gemm_skinny_nn_kernel<MT, KS>), grid, dim3(256), 0, st, p, s);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((gemm_skinny_nt_kernel<MT, KS>), grid, dim3(256), 0, st, p, s);
+}
+
+static int launch_skinny(const SkinnyPlan& pl, const GemmP& p, void* ws, hipStream_t st) {
+  SkinnyP s{};
+  s.splits = pl.splits;
+  if (pl.splits > 1) {
+    s.cnt = (unsigned*)ws;
+    s.slab = (float*)((char*)ws + kCntBytes);
+  }
+  const dim3 grid(pl.cols, pl.splits);
+  if (pl.mt == 1) {
+    switch (pl.ks) {
+      case 1: skinny_launch<1, 1>(pl.nn, grid, st, p, s); break;
+      case 2: skinny_launch<1, 2>(pl.nn, grid, st, p, s); break;
+      case 4: skinny_launch<1, 4>(pl.nn, grid, st, p, s); break;
+      default: skinny_launch<1, 8>(pl.nn, grid, st, p, s); break;
+    }
+  } else {
+    switch (pl.ks) {
+      case 1: skinny_launch<2, 1>(pl.nn, grid, st, p, s); break;
+      case 2: skinny_launch<2, 2>(pl.nn, grid, st, p, s); break;
+      case 4: skinny_launch<2, 4>(pl.nn, grid, st, p, s); break;
+      default: skinny_launch<2, 8>(pl.nn, grid, st, p, s); break;
+    }
+  }
+  DASA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dasa_gemm_skinny_tune(int target_waves, int ks) {
+  g_skinny_waves = target_waves;
+  g_skinny_ks = ks;
+  return 0;
+}
+
 extern "C" int dasa_gemm_force_config(int cfg) {
   g_force_cfg = cfg;
   if (cfg < 0) g_force_group = -1;
@@ -1448,6 +1788,8 @@ extern "C" int dasa_gemm_force_config(int cfg) {
 
 extern "C" int64_t dasa_gemm_f32_workspace(const dasa_gemm_desc* d) {
   if (!d || d->M < 0 || d->N < 0 || d->K < 0) return 0;
+  const SkinnyPlan sk = skinny_plan(d);
+  if (sk.ok && g_force_cfg < 0) return sk.ws;
   return make_plan(d).ws;
 }
 
@@ -1488,6 +1830,11 @@ extern "C" int dasa_gemm_f32(const dasa_gemm_desc* d, void* ws, int64_t ws_bytes
     g_force_group = e ? atoi(e) : -1;
   }
   p.group_m = g_force_group > 0 ? g_force_group : pl.group_m;
+  if (g_force_cfg < 0) {
+    const SkinnyPlan skp = skinny_plan(d);
+    if (skp.ok && (skp.splits == 1 || (ws != nullptr && ws_bytes >= skp.ws)))
+      return launch_skinny(skp, p, ws, (hipStream_t)stream);
+  }
   SkP sk{};
   if (pl.sk_grid > 0) {
     sk.grid = pl.sk_grid;

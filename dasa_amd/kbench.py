@@ -84,6 +84,46 @@ def _cases(B, dev):
     # candidate logits back to back): its bytes over its time
     chain = [c for c in cases if c[0] in ("ada_gate", "shift_attn", "softdot", "cand_logit")]
     cases.append(("step_chain", sum(c[1] for c in chain), lambda: [c[2]() for c in chain]))
+    # the attention modules' weight-streaming projections at this batch (gemm_skinny_* kernels at
+    # B <= 32): SoftDot / Shift linear_in (model.py:263, 311), the decoder LSTMCell input + recurrent
+    # products (model.py:437), linear_out of the instruction attention (model.py:264), and the input
+    # gradient of the LSTMCell input projection (dX = dY . W_ih). "_cold" rotates over enough weight
+    # copies (> 512 MB) that every launch streams its weight from HBM, as inside the rollout where the
+    # language stack's traffic evicts the Infinity Cache between decision steps.
+    lin = {"linear_in_feat": (D, H), "linear_in_instr": (2 * H, H), "lstm_ih": (4 * H, 64 + D),
+           "lstm_hh": (4 * H, H), "linear_out": (H, 3 * H)}
+    for name, (N, Kd) in lin.items():
+        x = rnd(B, Kd)
+        y = torch.empty(B, N, device=dev)
+        ncopy = max(2, int(512e6 // (4 * N * Kd)) + 1)
+        Ws = [rnd(N, Kd) * 0.05 for _ in range(ncopy)]
+        nb = 4.0 * (N * Kd + B * Kd + B * N)
+        cases.append((f"skinny_{name}", nb, lambda x=x, W=Ws[0], y=y: ops.linear(x, W, out=y)))
+        it = iter(range(1 << 30))
+        cases.append((f"skinny_{name}_cold", nb,
+                      lambda x=x, Ws=Ws, y=y, it=it: ops.linear(x, Ws[next(it) % len(Ws)], out=y)))
+    dy, Wih = rnd(B, 4 * H), rnd(4 * H, 64 + D) * 0.05
+    cases.append(("skinny_lstm_ih_dx", 4.0 * (4 * H * (64 + D) + B * 4 * H + B * (64 + D)),
+                  lambda: ops.matmul_nn(dy, Wih)))
+    # the attention modules end to end as one decision step runs them: linear_in + shift attention,
+    # linear_in + instruction SoftDot + linear_out, linear_in + candidate logits (weights cache-warm)
+    Wf, Wi, Wo, Wc = rnd(D, H) * 0.05, rnd(2 * H, H) * 0.05, rnd(H, 3 * H) * 0.05, rnd(D, H) * 0.05
+    h1 = rnd(B, H)
+    qf, qi2, qc2 = torch.empty(B, D, device=dev), torch.empty(B, 2 * H, device=dev), torch.empty(B, D, device=dev)
+    cat = rnd(B, 3 * H)
+    htl = torch.empty(B, H, device=dev)
+
+    def attn_modules():
+        ops.linear(h1, Wf, out=qf)
+        ops.shift_attn_fwd(qf, feat, z)
+        ops.linear(h1, Wi, out=qi2)
+        ops.softdot_fwd(qi2, ctx, mask)
+        ops.linear(cat, Wo, act="tanh", out=htl)
+        ops.linear(h1, Wc, out=qc2)
+        ops.softdot_fwd(qc2, cand, None, want_probs=False, want_wctx=False)
+    nb_mod = (4.0 * (D * H + 2 * H * H + 3 * H * H + D * H) + 4.0 * B * (8 * H + 2 * D)
+              + 4.0 * B * (V * D + 2 * D + 3 * V) + 4.0 * B * (L * 2 * H + 2 * 2 * H + 3 * L) + 4.0 * B * (C * D + D + C))
+    cases.append(("attn_modules", nb_mod, attn_modules))
     # launch floor: a one-row column scale (8 KB) — the time any launch takes inside a replayed graph
     f1, o1 = rnd(1, F), torch.empty(1, F, device=dev)
     cases.append(("launch_floor", 8.0 * F, lambda: ops.colscale(f1, noise, o1)))

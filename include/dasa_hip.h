@@ -50,7 +50,7 @@ typedef struct dasa_gemm_desc {
   float alpha, beta;
 } dasa_gemm_desc;
 /* Workspace bytes for this descriptor: 64 KiB of stream-K arrival counters, then split-K partials
- * (skinny-M decoder GEMMs) or stream-K partial-tile slabs (mid-size GEMMs that do not fill the CUs).
+ * (the skinny M <= 32 decoder GEMMs' split-K partials) or stream-K partial-tile slabs (mid-size GEMMs that do not fill the CUs).
  * The buffer must be ZERO-FILLED when first allocated; every call leaves the counters zero again,
  * so one buffer can be reused by consecutive calls on one stream (never by overlapping calls).
  * Passing ws == NULL (or too small) runs the GEMM without split-K / stream-K instead. */
@@ -59,6 +59,10 @@ int64_t dasa_gemm_f32_workspace(const dasa_gemm_desc* d);
  * subsequent calls (-1 = automatic choice).
  * Returns the number of configurations. Host-only; not thread-safe with concurrent GEMM planning. */
 int dasa_gemm_force_config(int cfg);
+/* Tuning hook for the skinny (M <= 32) weight-streaming GEMMs: target wave count of the plan (0 = do
+ * not use the skinny kernels, -1 = default 1024) and a pinned K-steps-per-wave (1/2/4/8, -1 = plan).
+ * Host-only; returns 0. */
+int dasa_gemm_skinny_tune(int target_waves, int ks);
 int dasa_gemm_f32(const dasa_gemm_desc* d, void* ws, int64_t ws_bytes, void* stream);
 /* bf16-operand nn.Linear forward for BASELINE configs[4] (B = 256, bf16 with fp32 accumulation):
  * C = epilogue(A . B^T) with A fp32 [M][lda] rounded to bf16 (RNE) on load and B a bf16 weight copy

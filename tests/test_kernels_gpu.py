@@ -604,3 +604,72 @@ def test_gemm_skinny(dev, M, N, K):
                beta=0.25)
     want = torch.tanh(z) * aux.double() * cs.double() + 0.25 * c0.double()
     assert (out.cpu().double() - want).abs().max().item() < 1e-5
+
+
+# (M, N, K): the decoder / critic / attention shapes at B = 20 (model.py:263-264, 437, 970-982) and
+# their input gradients, M at the 16 / 32 column-tile edges, N not a multiple of the 16 / 64 column
+# block, K not a multiple of the 32-deep step, K shorter than one step, many K splits.
+SKINNY_NT = [(20, 2176, 1024), (20, 4096, 2240), (20, 1024, 2048), (20, 4096, 1024), (20, 1024, 3072),
+             (1, 5, 1024), (16, 64, 128), (17, 2000, 700), (32, 130, 36), (2, 4096, 8), (31, 48, 12288)]
+SKINNY_NN = [(20, 1024, 2176), (20, 2240, 4096), (20, 2048, 1024), (20, 3072, 1024), (1, 8, 1024),
+             (16, 68, 100), (17, 1000, 4), (32, 4096, 300), (5, 2176, 12288)]
+
+
+def _skinny_modes():
+    """(target waves, ks) plans to force: the default, the widest-K and the narrowest-K form."""
+    return [(-1, -1), (-1, 8), (100000, 1)]
+
+
+@pytest.mark.parametrize("M,N,K", SKINNY_NT)
+def test_gemm_skinny_nt_kernel(dev, M, N, K):
+    """The weight-streaming skinny NT kernel (gemm_skinny_nt_kernel: W on the MFMA row side, K split in
+    and across workgroups, last-arriver partial sum) in its default and forced K-split forms, plain and
+    with the full fused epilogue, against fp64; bitwise deterministic across repeats."""
+    from dasa_amd import _lib, ops
+    lib = _lib.lib()
+    g = torch.Generator().manual_seed(M * 131 + N + K)
+    Abuf = _rand(M, K + 8, g=g)
+    W, b = _rand(N, K, g=g, scale=0.05), _rand(N, g=g)
+    aux, cs, c0 = _rand(M, N, g=g), _rand(N, g=g), _rand(M, N, g=g)
+    z = Abuf[:, :K].double() @ W.double().t() + b.double()
+    tol = 2e-6 * max(1.0, z.abs().max().item()) * math.sqrt(max(1, K) / 256)
+    Ad, Wd, bd = Abuf.to(dev)[:, :K], W.to(dev), b.to(dev)
+    try:
+        for waves, ks in _skinny_modes():
+            lib.dasa_gemm_skinny_tune(waves, ks)
+            y = ops.linear(Ad, Wd, bd)
+            y2 = ops.linear(Ad, Wd, bd)
+            assert torch.equal(y, y2), (waves, ks)
+            assert (y.cpu().double() - z).abs().max().item() < tol, (waves, ks)
+            out = c0.clone().to(dev)
+            ops.linear(Ad, Wd, bd, act="sigmoid", aux=aux.to(dev), colscale=cs.to(dev), out=out, beta=0.5)
+            want = torch.sigmoid(z) * aux.double() * cs.double() + 0.5 * c0.double()
+            assert (out.cpu().double() - want).abs().max().item() < 1e-5, (waves, ks)
+    finally:
+        lib.dasa_gemm_skinny_tune(-1, -1)
+
+
+@pytest.mark.parametrize("M,N,K", SKINNY_NN)
+def test_gemm_skinny_nn_kernel(dev, M, N, K):
+    """The skinny NN kernel (gemm_skinny_nn_kernel: dX = dY . W of an nn.Linear, W read along its rows)
+    in its default and forced forms, with beta accumulation and a strided dY, against fp64."""
+    from dasa_amd import _lib, ops
+    lib = _lib.lib()
+    g = torch.Generator().manual_seed(M * 17 + N * 3 + K)
+    Abuf = _rand(M, K + 4, g=g)
+    B = _rand(K, N, g=g, scale=0.05)
+    c0 = _rand(M, N, g=g)
+    z = Abuf[:, :K].double() @ B.double()
+    tol = 2e-6 * max(1.0, z.abs().max().item()) * math.sqrt(max(1, K) / 256)
+    Ad, Bd = Abuf.to(dev)[:, :K], B.to(dev)
+    try:
+        for waves, ks in _skinny_modes():
+            lib.dasa_gemm_skinny_tune(waves, ks)
+            y = ops.matmul_nn(Ad, Bd)
+            assert torch.equal(y, ops.matmul_nn(Ad, Bd)), (waves, ks)
+            assert (y.cpu().double() - z).abs().max().item() < tol, (waves, ks)
+            out = c0.clone().to(dev)
+            ops.matmul_nn(Ad, Bd, out=out, beta=1.0)
+            assert (out.cpu().double() - (z + c0.double())).abs().max().item() < tol + 1e-6, (waves, ks)
+    finally:
+        lib.dasa_gemm_skinny_tune(-1, -1)

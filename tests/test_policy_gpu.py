@@ -67,7 +67,8 @@ def test_softdot(R, dev):
     h1 = _req(h, dev)
     ht, alpha = att(h1, ctx.to(dev), mask.to(dev))
     close(ht.detach().cpu(), G["softdot/h_tilde"], 1e-5, "h_tilde")
-    close(alpha.cpu(), G["softdot/alpha"], 1e-6, "alpha")
+    # probabilities of scores summed over K = 2048 products: summation order moves them by ~2e-6
+    close(alpha.cpu(), G["softdot/alpha"], 1e-5, "alpha")
     (ht * g1.to(dev)).sum().backward()
     # input gradients are sums over K = 2048..3200 products with |dh| up to ~40: bound relative to scale
     close(h1.grad.cpu(), G["softdot/dh"], max(1e-4, 1e-5 * np.abs(G["softdot/dh"]).max()), "dh")
