@@ -1082,8 +1082,11 @@ __device__ __forceinline__ void split3_quad(const float4& x, const float4& y, ui
 // second reduce launch, and no workgroup ever waits on another.
 struct X6Split { unsigned* cnt; float* slab; int splitk, kchunk; };
 
+// (at most 2 waves per SIMD fit the LDS of the 128-row forms anyway: telling the register allocator so
+// lets it use 256 VGPRs instead of spilling to reach an occupancy the LDS forbids)
 template <int BM, int BN, int WAVES_M, int WAVES_N, bool SEP, int PF = 1, bool SPL = false>
-__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) __attribute__((amdgpu_waves_per_eu(1, 2)))
+void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
   constexpr int NT = 64 * WAVES_M * WAVES_N;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N, TM = WM / 16, TN = WN / 16;
   constexpr int NA = BM * 4 / NT, NB = BN * 4 / NT;    // 16-B (8 x bf16) K quads per thread per plane
@@ -1125,7 +1128,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_f32x6_nt_kernel(G
   // unit u -> (row, quad): 8 consecutive lanes take 8 consecutive rows of one quad (coalesced 128-B
   // row segments per 4 x 8 lanes on the global side, conflict-free ds_write_b128 groups on the LDS side)
   struct Stage {
-    float4 a[NA][2];
+    uint4 a[NA][2];   // 8 fp32 of A as bit patterns (uint4 storage keeps the stages out of scratch)
     uint4 w[3][NB];
     __device__ __forceinline__ static void unit(int u, int& row, int& q) {
       q = (u >> 3) & 3;
@@ -1138,8 +1141,8 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_f32x6_nt_kernel(G
         int row, q;
         unit(tid + NT * i, row, q);
         const float* src = A + (long)min(m0 + row, p.M - 1) * p.lda + k0 + 8 * q;
-        a[i][0] = *reinterpret_cast<const float4*>(src);
-        a[i][1] = *reinterpret_cast<const float4*>(src + 4);
+        a[i][0] = *reinterpret_cast<const uint4*>(src);
+        a[i][1] = *reinterpret_cast<const uint4*>(src + 4);
       }
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
@@ -1156,7 +1159,7 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_f32x6_nt_kernel(G
         int row, q;
         unit(tid + NT * i, row, q);
         uint4 h, m, l;
-        split3_quad(a[i][0], a[i][1], h, m, l);
+        split3_quad(__builtin_bit_cast(float4, a[i][0]), __builtin_bit_cast(float4, a[i][1]), h, m, l);
         S[0 * PA + q * BM + row] = h;
         S[1 * PA + q * BM + row] = m;
         S[2 * PA + q * BM + row] = l;
