@@ -32,13 +32,28 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
   const int N4 = N >> 2;
   const float4* x4 = reinterpret_cast<const float4*>(x + (long)row * N);
   const float4* r4 = res ? reinterpret_cast<const float4*>(res + (long)row * N) : nullptr;
-  float4 v[VPL];
+  const float4* g4 = reinterpret_cast<const float4*>(gamma);
+  const float4* b4 = reinterpret_cast<const float4*>(beta);
+  // every load of the row first (clamped quads, unconditional; gamma / beta too), so one memory
+  // round trip per wave instead of one per operand
+  float4 v[VPL], rv[VPL], gv[VPL], bv[VPL];
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = min(lane + 64 * i, N4 - 1);
+    v[i] = x4[c];
+    gv[i] = g4[c];
+    bv[i] = b4[c];
+  }
+  if (r4) {
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) rv[i] = r4[min(lane + 64 * i, N4 - 1)];
+  }
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
     const int c = lane + 64 * i;
     if (c < N4) {
-      float4 a = x4[c];
+      float4 a = v[i];
       if (p > 0.f) {
         const uint64_t base = (uint64_t)row * N + 4 * c;
         a.x *= dasa_dropout_scale(p, seed, base + 0);
@@ -47,8 +62,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
         a.w *= dasa_dropout_scale(p, seed, base + 3);
       }
       if (r4) {
-        const float4 b = r4[c];
-        a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+        a.x += rv[i].x; a.y += rv[i].y; a.z += rv[i].z; a.w += rv[i].w;
       }
       v[i] = a;
       s += (a.x + a.y) + (a.z + a.w);
@@ -68,15 +82,13 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
   }
   const float var = wave_sum(q) / N;
   const float rstd = rsqrtf(var + eps);
-  const float4* g4 = reinterpret_cast<const float4*>(gamma);
-  const float4* b4 = reinterpret_cast<const float4*>(beta);
   float4* y4 = reinterpret_cast<float4*>(y + (long)row * N);
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
     const int c = lane + 64 * i;
     if (c < N4) {
       if (xsum) reinterpret_cast<float4*>(xsum + (long)row * N)[c] = v[i];
-      const float4 g = g4[c], bb = b4[c];
+      const float4 g = gv[i], bb = bv[i];
       float4 o;
       o.x = (v[i].x - mean) * rstd * g.x + bb.x;
       o.y = (v[i].y - mean) * rstd * g.y + bb.y;
@@ -242,26 +254,37 @@ __global__ __launch_bounds__(256) void mha_fwd_kernel(MhaArgs a, int nqt) {
   const int h = bh % a.heads, b = bh / a.heads;
   const int Lq = a.Lq, Lk = a.Lk;
   const uint64_t seed = a.p > 0.f ? eff_seed(a.seed, a.seed_src) : 0;
-  // stage K / V rows (zero past Lk) and the additive key mask
-  for (int idx = threadIdx.x; idx < NKT * 32 * (kDh / 4); idx += blockDim.x) {
-    const int row = idx / (kDh / 4), c4 = idx % (kDh / 4);
-    float4 kx = make_float4(0.f, 0.f, 0.f, 0.f), vx = kx;
-    if (row < Lk) {
-      kx = reinterpret_cast<const float4*>(a.K + ((long)b * Lk + row) * a.ldk + h * kDh)[c4];
-      vx = reinterpret_cast<const float4*>(a.V + ((long)b * Lk + row) * a.ldv + h * kDh)[c4];
-    }
-    *reinterpret_cast<float4*>(Ks + row * kKvLd + 4 * c4) = kx;
-    *reinterpret_cast<float4*>(Vs + row * kKvLd + 4 * c4) = vx;
-  }
-  for (int k = threadIdx.x; k < NKT * 32; k += blockDim.x)
-    Ms[k] = k < Lk ? (a.mask ? a.mask[(long)b * Lk + k] : 0.f) : -INFINITY;
   const int qt = w, q0 = qt * 32;
   const int j = lane & 31, hh = lane >> 5;
+  // Every global load of the workgroup is issued before the first is waited for (one HBM round trip
+  // per workgroup instead of one per staging pass): this wave's Q fragment, the K / V rows (clamped,
+  // zeroed past Lk when written to LDS) and the key mask.
   // B operand of S^T: Q^T, lane (query j, half hh) holds Q[q0 + j][8g + 4hh .. +3] (K-permuted)
   const float* qp = a.Q + ((long)b * Lq + min(q0 + j, Lq - 1)) * a.ldq + h * kDh + 4 * hh;
   float4 qf[8];
 #pragma unroll
   for (int g = 0; g < 8; ++g) qf[g] = *reinterpret_cast<const float4*>(qp + 8 * g);
+  constexpr int NF = NKT * 32 * (kDh / 4) / 256;   // float4 of K (and of V) per thread (blockDim = 256)
+  float4 kx[NF], vx[NF];
+#pragma unroll
+  for (int i = 0; i < NF; ++i) {
+    const int idx = threadIdx.x + 256 * i, row = min(idx / (kDh / 4), Lk - 1), c4 = idx % (kDh / 4);
+    kx[i] = reinterpret_cast<const float4*>(a.K + ((long)b * Lk + row) * a.ldk + h * kDh)[c4];
+    vx[i] = reinterpret_cast<const float4*>(a.V + ((long)b * Lk + row) * a.ldv + h * kDh)[c4];
+  }
+  const int mk = min((int)threadIdx.x, Lk - 1);
+  const float mv = a.mask ? a.mask[(long)b * Lk + mk] : 0.f;
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < NF; ++i) {
+    const int idx = threadIdx.x + 256 * i, row = idx / (kDh / 4), c4 = idx % (kDh / 4);
+    const float k = row < Lk ? 1.f : 0.f;   // component-wise (a whole-float4 select goes through scratch)
+    *reinterpret_cast<float4*>(Ks + row * kKvLd + 4 * c4) =
+        make_float4(k * kx[i].x, k * kx[i].y, k * kx[i].z, k * kx[i].w);
+    *reinterpret_cast<float4*>(Vs + row * kKvLd + 4 * c4) =
+        make_float4(k * vx[i].x, k * vx[i].y, k * vx[i].z, k * vx[i].w);
+  }
+  if (threadIdx.x < NKT * 32) Ms[threadIdx.x] = (int)threadIdx.x < Lk ? mv : -INFINITY;
   __syncthreads();
   if (qt >= nqt) return;   // (no barrier below)
   floatx16 st[NKT];
@@ -610,7 +633,8 @@ extern "C" int dasa_mha_fwd(const float* Q, int64_t ldq, const float* K, int64_t
             drop_p > 0.f ? dasa_seed_src_host() : nullptr};
   const int nqt = cdivi(Lq, 32);
   if (nqt > 4) return (int)hipErrorInvalidValue;   // one wave per 32-query tile, Lq <= 128
-  const dim3 grid(B * heads), block(64 * nqt);
+  // 4 waves always: all of them stage K / V, waves past the query tiles then leave
+  const dim3 grid(B * heads), block(256);
   hipStream_t st = (hipStream_t)stream;
   switch (cdivi(Lk, 32)) {
     case 1: hipLaunchKernelGGL(mha_fwd_kernel<1>, grid, block, 0, st, a, nqt); break;

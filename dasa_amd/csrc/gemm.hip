@@ -1928,6 +1928,10 @@ static X6Plan x6_plan(const dasa_gemm_desc* d) {
   const int M = d->M, N = d->N, K = d->K, batch = d->batch < 1 ? 1 : d->batch;
   X6Plan pl{8, 128, 128, 1, K, 0};
   int fsplit = 0;
+  // 256x128 tiles (form 7: the same products and order as form 8, bitwise equal) on the wide
+  // 12800-row language GEMMs: +4-8 % on 12800 x 2304 / 3072 x 768, slower on N = 768 and on fewer rows
+  // (profiles/r02/x6_forms.txt)
+  if (M >= 4096 && N >= 2048) pl.cfg = 7;
   if (g_force_cfg >= kX6Force) {
     pl.cfg = (g_force_cfg - kX6Force) % 16;
     fsplit = ((g_force_cfg - kX6Force) / 16) % 64;
