@@ -17,7 +17,7 @@ PEAK_TF = {"gemm_bf16": 2500.0, "gemm_x6": 2500.0 / 6}
 # family -> (roofline bound, kernel name prefix in rocprof)
 FAMILIES = {
     "gemm": ("mfma", "gemm_f32_kernel"),
-    "gemm_skinny": ("hbm", "gemm_f32_kernel (M <= 64; rocprof cannot split it from gemm)"),
+    "gemm_skinny": ("hbm", "gemm_skinny_nt_kernel / gemm_skinny_nn_kernel (M <= 32)"),
     "gemm_bf16": ("mfma", "gemm_bf16_nt_kernel"),
     "gemm_x6": ("mfma", "gemm_f32x6_nt_kernel"),
     "bilstm": ("mfma", "bilstm_step_fused_kernel"),
@@ -127,7 +127,7 @@ def _pmc_traffic():
 
 
 # the committed PMC summary the roofline's `traffic` / `mfma_busy` come from (tools/pmc_summary.py)
-PMC_FILE = "profiles/r02/prof_b/pmc.json"
+PMC_FILE = "profiles/r02/prof_f/pmc.json"
 
 
 def active():

@@ -8,6 +8,7 @@ from collections import defaultdict
 FAMILY_PREFIX = [
     ("gemm_x6", ("gemm_f32x6_nt_kernel",)),
     ("gemm_bf16", ("gemm_bf16_nt_kernel",)),
+    ("gemm_skinny", ("gemm_skinny_nt_kernel", "gemm_skinny_nn_kernel")),
     ("gemm", ("gemm_f32_kernel", "gemm_nt_k64_kernel", "gemm_nt_glds_kernel")),   # (split-K reduce apart)
     ("gemm_splitk_reduce", ("splitk_reduce_kernel",)),
     ("bilstm", ("bilstm_persist_fwd_kernel", "bilstm_step_fused_kernel", "bilstm_step_cell_kernel")),
@@ -42,10 +43,6 @@ def main(stats_csv, bench_json=None):
     if bench_json:
         line = [ln for ln in open(bench_json).read().splitlines() if ln.startswith('{"metric"') or ln.startswith('{"profile_only"')][-1]
         bench = json.loads(line).get("kernels", {})
-        if "gemm_skinny" in bench and "gemm" in bench:   # rocprof cannot tell them apart: compare merged
-            g, k = bench["gemm"], bench["gemm_skinny"]
-            n = g["launches"] + k["launches"]
-            bench = dict(bench, gemm=dict(g, avg_launch_us=round(1e3 * (g["device_ms"] + k["device_ms"]) / n, 2)))
     print(f"{'family':<34}{'calls':>8}{'total ms':>11}{'share':>8}{'avg us':>10}{'bench avg us':>14}")
     for k, (n, ns) in sorted(fam.items(), key=lambda kv: -kv[1][1])[:25]:
         b = bench.get(k, {}).get("avg_launch_us", "")
