@@ -203,7 +203,8 @@ def gemm_bf16(x, Wb, out, *, M, N, K, lda, ldc, bias=None, act=None, aux=None, l
 # split inside the kernel. fp32-accurate (the six kept bf16 products are exact, dropped terms are below
 # fp32 rounding); DASA_GEMM_EMU=0 routes every nn.Linear back to the native fp32 MFMA kernels.
 _X6 = {}
-_EMU = {"on": os.environ.get("DASA_GEMM_EMU", "1") != "0", "min_rows": int(os.environ.get("DASA_GEMM_EMU_MIN_M", "512"))}
+_EMU = {"on": os.environ.get("DASA_GEMM_EMU", "1") != "0", "min_rows": int(os.environ.get("DASA_GEMM_EMU_MIN_M", "512")),
+        "short_k": int(os.environ.get("DASA_X6_SHORTK_TILES", "0"))}   # A/B: x6 split-K on few-tile short-K GEMMs
 
 
 def set_gemm_emulation(on=None, min_rows=None):
@@ -261,6 +262,8 @@ def _emu_ok(M, N, K, lda, x):
             and x.data_ptr() % 16 == 0):
         return False
     tiles = -(-M // 128) * -(-N // 128)
+    if _EMU["short_k"] and tiles >= _EMU["short_k"] and K >= 512:
+        return True
     return tiles >= 128 or (K >= 2048 and tiles * _x6_splitk(M, N, K) >= 192)
 
 
@@ -682,7 +685,14 @@ def register_concurrent_stream(st):
         _CONCURRENT.append(st)
 
 
+# DASA_LSTM_MODE=1 (per-timestep bi-LSTM kernels only) needs no exclusive GPU: with DASA_LSTM_SHARED=1
+# the bi-LSTM launches do not join the concurrent streams (A/B switch)
+_LSTM_SHARED = os.environ.get("DASA_LSTM_MODE") == "1" and os.environ.get("DASA_LSTM_SHARED") == "1"
+
+
 def _exclusive(dev):
+    if _LSTM_SHARED:
+        return
     if torch.cuda.is_current_stream_capturing():
         return      # a captured region is joined before its replay (Seq2SeqAgent's step graph)
     cur = torch.cuda.current_stream(dev)
