@@ -1447,8 +1447,17 @@ __device__ __forceinline__ float4 ldg4(const float* p) { return *reinterpret_cas
 // NT: Y[M,N] = epi(X[M,K] . W[N,K]^T). Workgroup = 16 output features (rows of W) x 4 waves x KS
 // 32-deep steps per wave; MFMA rows = features, columns = the M <= 16*MT activation rows.
 // Lane (r = lane & 15, g = lane >> 4) loads W[n0 + r][k .. k+7] and X[16t + r][k .. k+7], k = step*32 + 8g.
-template <int MT, int KS>
+// XR = 4 (hybrid, 16 < M <= 20, the headline batch): one MFMA column tile for rows 0..15 and the last
+// M - 16 rows on the VALU from the W values already in registers (8 fma per row per step, X rows staged
+// in LDS once per workgroup, summed over the 4 lane groups at the end) instead of a second 16-column
+// MFMA tile that would be 3/4 padding.
+template <int MT, int KS, int XR = 0>
 __global__ __launch_bounds__(256, 2) void gemm_skinny_nt_kernel(GemmP p, SkinnyP sp) {
+  static_assert(XR == 0 || (XR == 4 && MT == 1), "hybrid form: one MFMA tile + 4 VALU rows");
+  constexpr int KSPAN = 4 * KS * 32;                  // the workgroup's K range
+  constexpr int NXQ = XR * KSPAN / 4;                 // float4 of the staged extra rows
+  constexpr int NXI = XR ? (NXQ + 255) / 256 : 1;
+  __shared__ float4 xs[XR ? NXQ : 1];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, g = lane >> 4;
   const int col = blockIdx.x, split = blockIdx.y, n0 = col * 16;
   const int K = p.K, kq = K - 4;   // last whole quad (K % 4 == 0)
@@ -1457,6 +1466,15 @@ __global__ __launch_bounds__(256, 2) void gemm_skinny_nt_kernel(GemmP p, SkinnyP
 #pragma unroll
   for (int t = 0; t < MT; ++t) xrow[t] = p.A + (long)min(16 * t + r, p.M - 1) * p.lda;
   const int kbase = (split * 4 + w) * KS * 32 + 8 * g;
+  float4 xe[NXI];
+  if constexpr (XR > 0) {   // issued first, so storing them below waits for these loads only
+#pragma unroll
+    for (int i = 0; i < NXI; ++i) {
+      const int idx = min((int)threadIdx.x + 256 * i, NXQ - 1), q = idx / (KSPAN / 4);
+      const int k = split * KSPAN + 4 * (idx % (KSPAN / 4));
+      xe[i] = ldg4(p.A + (long)min(16 + q, p.M - 1) * p.lda + min(k, kq));
+    }
+  }
   // every load first (clamped, unconditional: out-of-range quads re-read the last one and are zeroed
   // below), so each wave has KS x 2 KB of W in flight
   float4 wv[KS][2], xv[KS][MT][2];
@@ -1474,9 +1492,22 @@ __global__ __launch_bounds__(256, 2) void gemm_skinny_nt_kernel(GemmP p, SkinnyP
   // keep every load above the MFMAs (the scheduler would otherwise sink each load to its use and
   // leave one step in flight); the waitcnt pass then waits step by step
   __builtin_amdgcn_sched_barrier(0);
-  floatx4 acc[MT];
+  if constexpr (XR > 0) {
 #pragma unroll
-  for (int t = 0; t < MT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < NXI; ++i) {
+      const int idx = (int)threadIdx.x + 256 * i;
+      if (idx < NXQ) {
+        const int q = idx / (KSPAN / 4), k = split * KSPAN + 4 * (idx % (KSPAN / 4));
+        const float z = (16 + q < p.M && k < K) ? 1.f : 0.f;
+        xs[idx] = make_float4(z * xe[i].x, z * xe[i].y, z * xe[i].z, z * xe[i].w);
+      }
+    }
+    __syncthreads();
+  }
+  constexpr int NA = MT + (XR ? 1 : 0);
+  floatx4 acc[NA];
+#pragma unroll
+  for (int t = 0; t < NA; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     const int k = kbase + 32 * s;
@@ -1490,12 +1521,35 @@ __global__ __launch_bounds__(256, 2) void gemm_skinny_nt_kernel(GemmP p, SkinnyP
         for (int t = 0; t < MT; ++t)
           acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(f4get(a, e), f4get(sel4(ok, xv[s][t][h]), e), acc[t], 0, 0, 0);
       }
+      if constexpr (XR > 0) {   // rows 16..19: k .. k+3 of this quad against the staged X rows
+        const int kl = (w * KS * 32 + 32 * s + 8 * g) / 4 + h;
+#pragma unroll
+        for (int q = 0; q < XR; ++q) {
+          const float4 x = xs[q * (KSPAN / 4) + kl];
+          float v = acc[MT][q];
+          v = fmaf(a.x, x.x, v);
+          v = fmaf(a.y, x.y, v);
+          v = fmaf(a.z, x.z, v);
+          v = fmaf(a.w, x.w, v);
+          acc[MT][q] = v;
+        }
+      }
     }
   }
-  if (!skinny_reduce<MT>(acc, sp, col, split)) return;
-  // C[feature = 4g + j][act row = r]  ->  Y[16t + r][n0 + 4g + j]
-  int mm[4 * MT], nn[4 * MT];
-  float v[4 * MT];
+  if constexpr (XR > 0) {   // sum the 4 lane groups (k slices) of each feature row
+#pragma unroll
+    for (int q = 0; q < XR; ++q) {
+      float v = acc[MT][q];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      acc[MT][q] = v;
+    }
+  }
+  if (!skinny_reduce<NA>(acc, sp, col, split)) return;
+  // C[feature = 4g + j][act row = r]  ->  Y[16t + r][n0 + 4g + j]; hybrid rows: lane group 0 of
+  // feature row r holds Y[16 + q][n0 + r]
+  int mm[4 * NA], nn[4 * NA];
+  float v[4 * NA];
 #pragma unroll
   for (int t = 0; t < MT; ++t)
 #pragma unroll
@@ -1504,7 +1558,15 @@ __global__ __launch_bounds__(256, 2) void gemm_skinny_nt_kernel(GemmP p, SkinnyP
       nn[4 * t + j] = n0 + 4 * g + j;
       v[4 * t + j] = acc[t][j];
     }
-  skinny_store<4 * MT>(p, mm, nn, v);
+  if constexpr (XR > 0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      mm[4 * MT + q] = g == 0 ? 16 + q : p.M;   // p.M: not stored
+      nn[4 * MT + q] = n0 + r;
+      v[4 * MT + q] = acc[MT][q];
+    }
+  }
+  skinny_store<4 * NA>(p, mm, nn, v);
 }
 
 // NN: Y[M,N] = epi(X[M,K] . B[K,N]) with B row-major (ldb) - the input gradient dX = dY . W of an
@@ -1693,9 +1755,10 @@ static Plan make_plan(const dasa_gemm_desc* d) {
 // nn.Linear forward) or [K][N] (NN, dX = dY . W), 16-B aligned float4-able rows. KS (32-deep steps per
 // wave) is the largest that still gives >= `target` waves (default 1024 = 4 per CU: enough W requests
 // in flight to stream HBM), the K range left over is split across workgroups.
-struct SkinnyPlan { bool ok, nn; int mt, ks, cols, splits; int64_t ws; };
+struct SkinnyPlan { bool ok, nn; int mt, xr, ks, cols, splits; int64_t ws; };
 static int g_skinny_waves = -2;   // DASA_SKINNY_WAVES=<n>: target wave count; 0 disables the skinny kernels
 static int g_skinny_ks = -2;      // DASA_SKINNY_KS=<1|2|4|8>: pin KS (sweeps)
+static int g_skinny_hybrid = -2;  // DASA_SKINNY_HYBRID=0: 17..20-row NT GEMMs on two MFMA tiles instead
 
 static SkinnyPlan skinny_plan(const dasa_gemm_desc* d) {
   if (g_skinny_waves == -2) {
@@ -1711,13 +1774,22 @@ static SkinnyPlan skinny_plan(const dasa_gemm_desc* d) {
   const uintptr_t am = (uintptr_t)d->A | (uintptr_t)d->B;
   if ((am & 15) || (d->lda & 3) || (d->ldb & 3) || (nn && (N & 3))) return sp;
   sp.nn = nn;
+  if (g_skinny_hybrid == -2) {
+    const char* e = getenv("DASA_SKINNY_HYBRID");
+    g_skinny_hybrid = e ? atoi(e) : 1;
+  }
   sp.mt = M <= 16 ? 1 : 2;
+  sp.xr = 0;
+  if (!nn && M > 16 && M <= 20 && g_skinny_hybrid) {
+    sp.mt = 1;
+    sp.xr = 4;
+  }
   const long ksteps = cdiv(K, 32);
   sp.cols = (int)(nn ? cdiv(N, 64) : cdiv(N, 16));
-  // target: 1024 waves for the NT form at M > 16, 512 otherwise (tools/skinny_probe.py sweep,
-  // profiles/r02/skinny_probe.txt); the first KS from the top that reaches it while padding the K range
+  // target: 1024 waves for the NT form at M > 16 (two tiles or the hybrid), 512 otherwise
+  // (tools/skinny_probe.py sweeps, profiles/r02/skinny_probe*.txt); the first KS from the top that reaches it while padding the K range
   // by <= 10 % (K steps beyond K still issue their MFMAs on zeros)
-  const long target = g_skinny_waves > 0 ? g_skinny_waves : (!nn && sp.mt == 2 ? 1024 : 512);
+  const long target = g_skinny_waves > 0 ? g_skinny_waves : (!nn && (sp.mt == 2 || sp.xr) ? 1024 : 512);
   const int kmax = nn ? (sp.mt == 2 ? 2 : 4) : 8;
   int ks = kmax;
   for (; ks > 1; ks >>= 1) {
@@ -1730,7 +1802,7 @@ static SkinnyPlan skinny_plan(const dasa_gemm_desc* d) {
   }
   sp.ks = ks;
   const long splits = cdiv(ksteps, 4 * ks);
-  const int nacc = nn ? 4 * sp.mt : sp.mt;
+  const int nacc = nn ? 4 * sp.mt : sp.mt + (sp.xr ? 1 : 0);
   const int64_t slab = (int64_t)sp.cols * splits * nacc * 64 * 16;
   if (splits > 65535 || (splits > 1 && (sp.cols > kCntWords || slab >= (1LL << 31)))) return sp;
   sp.splits = (int)splits;
@@ -1740,7 +1812,13 @@ static SkinnyPlan skinny_plan(const dasa_gemm_desc* d) {
 }
 
 template <int MT, int KS>
-static void skinny_launch(bool nn, dim3 grid, hipStream_t st, const GemmP& p, const SkinnyP& s) {
+static void skinny_launch(bool nn, dim3 grid, hipStream_t st, const GemmP& p, const SkinnyP& s, int xr = 0) {
+  if constexpr (MT == 1) {
+    if (xr) {
+      hipLaunchKernelGGL((gemm_skinny_nt_kernel<1, KS, 4>), grid, dim3(256), 0, st, p, s);
+      return;
+    }
+  }
   if constexpr (KS <= 4) {
     if (nn) {
       hipLaunchKernelGGL((gemm_skinny_nn_kernel<MT, KS>), grid, dim3(256), 0, st, p, s);
@@ -1760,10 +1838,10 @@ static int launch_skinny(const SkinnyPlan& pl, const GemmP& p, void* ws, hipStre
   const dim3 grid(pl.cols, pl.splits);
   if (pl.mt == 1) {
     switch (pl.ks) {
-      case 1: skinny_launch<1, 1>(pl.nn, grid, st, p, s); break;
-      case 2: skinny_launch<1, 2>(pl.nn, grid, st, p, s); break;
-      case 4: skinny_launch<1, 4>(pl.nn, grid, st, p, s); break;
-      default: skinny_launch<1, 8>(pl.nn, grid, st, p, s); break;
+      case 1: skinny_launch<1, 1>(pl.nn, grid, st, p, s, pl.xr); break;
+      case 2: skinny_launch<1, 2>(pl.nn, grid, st, p, s, pl.xr); break;
+      case 4: skinny_launch<1, 4>(pl.nn, grid, st, p, s, pl.xr); break;
+      default: skinny_launch<1, 8>(pl.nn, grid, st, p, s, pl.xr); break;
     }
   } else {
     switch (pl.ks) {
@@ -1778,8 +1856,11 @@ static int launch_skinny(const SkinnyPlan& pl, const GemmP& p, void* ws, hipStre
 }
 
 extern "C" int dasa_gemm_skinny_tune(int target_waves, int ks) {
+  // ks >= 16: the 17..20-row hybrid form off (KS pinned to ks - 16, or the plan's at 16) - sweeps
+  // compare it with two MFMA tiles
+  g_skinny_hybrid = ks >= 16 ? 0 : 1;
   g_skinny_waves = target_waves;
-  g_skinny_ks = ks;
+  g_skinny_ks = ks >= 16 ? (ks > 16 ? ks - 16 : -1) : ks;
   return 0;
 }
 

@@ -60,8 +60,8 @@ int64_t dasa_gemm_f32_workspace(const dasa_gemm_desc* d);
  * Returns the number of configurations. Host-only; not thread-safe with concurrent GEMM planning. */
 int dasa_gemm_force_config(int cfg);
 /* Tuning hook for the skinny (M <= 32) weight-streaming GEMMs: target wave count of the plan (0 = do
- * not use the skinny kernels, -1 = default 1024) and a pinned K-steps-per-wave (1/2/4/8, -1 = plan).
- * Host-only; returns 0. */
+ * not use the skinny kernels, -1 = default) and a pinned K-steps-per-wave (1/2/4/8, -1 = plan);
+ * ks + 16 (16 = plan's KS) also turns the 17..20-row hybrid MFMA + VALU form off. Host-only; returns 0. */
 int dasa_gemm_skinny_tune(int target_waves, int ks);
 int dasa_gemm_f32(const dasa_gemm_desc* d, void* ws, int64_t ws_bytes, void* stream);
 /* bf16-operand nn.Linear forward for BASELINE configs[4] (B = 256, bf16 with fp32 accumulation):

@@ -610,14 +610,16 @@ def test_gemm_skinny(dev, M, N, K):
 # their input gradients, M at the 16 / 32 column-tile edges, N not a multiple of the 16 / 64 column
 # block, K not a multiple of the 32-deep step, K shorter than one step, many K splits.
 SKINNY_NT = [(20, 2176, 1024), (20, 4096, 2240), (20, 1024, 2048), (20, 4096, 1024), (20, 1024, 3072),
-             (1, 5, 1024), (16, 64, 128), (17, 2000, 700), (32, 130, 36), (2, 4096, 8), (31, 48, 12288)]
+             (1, 5, 1024), (16, 64, 128), (17, 2000, 700), (32, 130, 36), (2, 4096, 8), (31, 48, 12288),
+             (19, 37, 12), (20, 520, 5000)]
 SKINNY_NN = [(20, 1024, 2176), (20, 2240, 4096), (20, 2048, 1024), (20, 3072, 1024), (1, 8, 1024),
              (16, 68, 100), (17, 1000, 4), (32, 4096, 300), (5, 2176, 12288)]
 
 
 def _skinny_modes():
-    """(target waves, ks) plans to force: the default, the widest-K and the narrowest-K form."""
-    return [(-1, -1), (-1, 8), (100000, 1)]
+    """(target waves, ks) plans to force: the default, the widest-K and the narrowest-K form, and the
+    17..20-row shapes without the hybrid MFMA + VALU form (ks + 16)."""
+    return [(-1, -1), (-1, 8), (100000, 1), (-1, 16), (100000, 17)]
 
 
 @pytest.mark.parametrize("M,N,K", SKINNY_NT)

@@ -14,7 +14,7 @@ from dasa_amd.kbench import _time_graph  # noqa: E402
 
 NT = [(20, 2176, 1024), (20, 2048, 1024), (20, 4096, 2240), (20, 4096, 1024), (20, 1024, 3072), (2, 2176, 1024)]
 NN = [(20, 1024, 2176), (20, 2240, 4096), (20, 1024, 4096), (20, 1024, 2048)]
-MODES = [(0, -1), (-1, -1), (512, -1), (2048, -1), (-1, 8), (-1, 4), (-1, 2), (-1, 1)]
+MODES = [(0, -1), (-1, -1), (-1, 16), (-1, 8), (-1, 24), (-1, 4), (-1, 20), (-1, 2)]
 
 
 def main():
@@ -37,7 +37,7 @@ def main():
                 else:
                     hot = _time_graph(lambda: ops.matmul_nn(x, Ws[0], out=y))
                     cold = _time_graph(lambda: ops.matmul_nn(x, Ws[next(it) % ncopy], out=y))
-                tag = "tiles" if waves == 0 else f"w{waves}k{ks}"
+                tag = "tiles" if waves == 0 else (f"k{ks - 16 if ks > 16 else 'plan'}-2tile" if ks >= 16 else f"k{ks}")
                 line += f" | {tag} {hot:6.2f}/{cold:6.2f}us {gb / cold * 1e6:5.0f}GB/s"
             lib.dasa_gemm_skinny_tune(-1, -1)
             print(line, flush=True)
