@@ -153,6 +153,17 @@ def hbm_kernels(batches=(20, 256)):
             gbs = nbytes / (us * 1e-6) / 1e9
             res.setdefault(name, {})[f"B{B}"] = {"us": round(us, 2), "bytes": int(nbytes), "GB/s": round(gbs, 1),
                                                   "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    # BASELINE.json north star: ">= 40 % achieved HBM bandwidth on the AdaIN + attention kernels" - their
+    # bytes over their time, each kernel timed alone (byte-weighted aggregate of the five forward kernels)
+    fam = ("ada_gate", "adain_musigma", "shift_attn", "softdot", "cand_logit")
+    agg = {}
+    for B in batches:
+        k = f"B{B}"
+        nb = sum(res[f][k]["bytes"] for f in fam)
+        us = sum(res[f][k]["us"] for f in fam)
+        gbs = nb / (us * 1e-6) / 1e9
+        agg[k] = {"us": round(us, 2), "bytes": int(nb), "GB/s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    res["adain_attention_aggregate"] = dict(agg, kernels=list(fam))
     return res
 
 
