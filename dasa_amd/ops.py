@@ -685,14 +685,7 @@ def register_concurrent_stream(st):
         _CONCURRENT.append(st)
 
 
-# DASA_LSTM_MODE=1 (per-timestep bi-LSTM kernels only) needs no exclusive GPU: with DASA_LSTM_SHARED=1
-# the bi-LSTM launches do not join the concurrent streams (A/B switch)
-_LSTM_SHARED = os.environ.get("DASA_LSTM_MODE") == "1" and os.environ.get("DASA_LSTM_SHARED") == "1"
-
-
 def _exclusive(dev):
-    if _LSTM_SHARED:
-        return
     if torch.cuda.is_current_stream_capturing():
         return      # a captured region is joined before its replay (Seq2SeqAgent's step graph)
     cur = torch.cuda.current_stream(dev)
