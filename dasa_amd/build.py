@@ -37,8 +37,15 @@ def build(force=False, verbose=True):
         return OUT
     os.makedirs(BUILD_DIR, exist_ok=True)
 
+    headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    headers.append(os.path.join(os.path.dirname(HERE), "include", "dasa_hip.h"))
+    newest_header = max(os.path.getmtime(h) for h in headers)
+
     def compile_one(src):
         obj = os.path.join(BUILD_DIR, os.path.basename(src) + ".o")
+        if (not force and os.path.exists(obj) and os.path.getmtime(obj) > os.path.getmtime(src)
+                and os.path.getmtime(obj) > newest_header):
+            return obj        # up to date (every source includes the headers, so a header edit rebuilds all)
         cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:

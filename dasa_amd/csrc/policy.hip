@@ -24,7 +24,7 @@ struct PolicyFwd {
   float* ce_sum;            // [1] sum over rows of -logp[target] (rows with target == ignore skipped)
   float* ent;               // [B] entropy, or NULL
   float* logp_a;            // [B] log-probability of the chosen action, or NULL
-  int64_t* action;          // [B] chosen action, or NULL (mode TEACHER)
+  int64_t* action;          // [B] chosen action, or NULL (mode TEACHER); the input in mode FORCED
   float* ce_rows;           // [B] scratch
   int B, C, mode, ignore;
   uint64_t seed;
@@ -112,11 +112,13 @@ __global__ __launch_bounds__(1024) void policy_head_fwd_kernel(PolicyFwd a) {
         last = max(last, __shfl_xor(last, o, 64));
       }
       act = pick == 0x7fffffff ? last : pick;   // u beyond the rounded total: the last valid candidate
+    } else if (a.mode == DASA_POLICY_FORCED) {   // the caller's action (it guarantees 0 <= action < len)
+      act = (int)a.action[b];
     }
     if (lane == 0) {
       a.ce_rows[b] = ce;
       if (a.ent) a.ent[b] = h;
-      if (a.action && act >= 0) a.action[b] = act;
+      if (a.action && act >= 0 && a.mode != DASA_POLICY_FORCED) a.action[b] = act;
     }
     if (a.logp_a && act >= 0) {
 #pragma unroll
@@ -172,7 +174,8 @@ extern "C" int dasa_policy_head_fwd(const float* logit, int64_t ld, const int32_
   if (B <= 0) return 0;
   if (C <= 0 || C > 64 * kVpl || ld < C || !logit || !cand_len || !logp || !ce_sum || !ws)
     return (int)hipErrorInvalidValue;
-  if (mode != DASA_POLICY_TEACHER && mode != DASA_POLICY_ARGMAX && mode != DASA_POLICY_SAMPLE)
+  if (mode != DASA_POLICY_TEACHER && mode != DASA_POLICY_ARGMAX && mode != DASA_POLICY_SAMPLE &&
+      mode != DASA_POLICY_FORCED)
     return (int)hipErrorInvalidValue;
   if (mode != DASA_POLICY_TEACHER && !action) return (int)hipErrorInvalidValue;
   PolicyFwd a{logit, (long)ld, cand_len, target, logp, ce_sum, ent, logp_a, action, ws, B, C, mode, ignore_index,

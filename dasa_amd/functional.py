@@ -278,8 +278,28 @@ class AdaINMuSigmaFn(torch.autograd.Function):
         return dc, ds, None
 
 
+def _overlaps(a, b):
+    """Do the storage byte ranges of a and b intersect (a conservative alias test)?"""
+    if a.untyped_storage().data_ptr() != b.untyped_storage().data_ptr():
+        return False
+    def span(t):
+        lo = t.data_ptr()
+        hi = lo + sum((n - 1) * st for n, st in zip(t.shape, t.stride())) * t.element_size() + t.element_size()
+        return lo, hi
+    (a0, a1), (b0, b1) = span(a), span(b)
+    return a0 < b1 and b0 < a1
+
+
 def adain_musigma(content, style, eps=1e-5, out=None):
     if torch.is_grad_enabled() and (content.requires_grad or style.requires_grad):
+        if out is not None:
+            # backward reads the saved content / style; an `out` aliasing them (the agent's in-place
+            # f_t[..., :F] = adain(f_t[..., :F], d_t[..., :F]), agent_dg.py:774-777) would overwrite
+            # the saved values, so the Function gets private copies
+            if _overlaps(out, content):
+                content = content.clone()
+            if _overlaps(out, style):
+                style = style.clone()
         y = AdaINMuSigmaFn.apply(content, style, eps)
         if out is not None:
             out.copy_(y)
@@ -389,8 +409,9 @@ class PolicyHeadFn(torch.autograd.Function):
     entropy and log-probability. Returns (ce_sum, entropy [B], logp_action [B], action [B] int64)."""
 
     @staticmethod
-    def forward(ctx, logit, cand_len_i32, target, mode, seed, ignore_index):
-        ce, ent, lpa, action, logp = ops.policy_head_fwd(logit, cand_len_i32, target, mode, seed, ignore_index)
+    def forward(ctx, logit, cand_len_i32, target, mode, seed, ignore_index, forced=None):
+        ce, ent, lpa, action, logp = ops.policy_head_fwd(logit, cand_len_i32, target, mode, seed, ignore_index,
+                                                         forced)
         ctx.save_for_backward(logp, cand_len_i32, target, action, ent)
         ctx.ignore = ignore_index
         if action is None:   # teacher mode: no action drawn
@@ -407,12 +428,13 @@ class PolicyHeadFn(torch.autograd.Function):
                                      d_ce.reshape(1).contiguous() if d_ce is not None else None,
                                      d_lpa.contiguous() if d_lpa is not None else None,
                                      d_ent.contiguous() if d_ent is not None else None, ctx.ignore)
-        return dlogit, None, None, None, None, None
+        return dlogit, None, None, None, None, None, None
 
 
-def policy_head(logit, cand_len_i32, target, mode, ignore_index=-100):
+def policy_head(logit, cand_len_i32, target, mode, ignore_index=-100, forced=None):
+    """mode teacher / argmax / sample; "forced" = sample with `forced` [B] as the drawn action."""
     seed = new_seed() if mode == "sample" else 0
-    return PolicyHeadFn.apply(logit, cand_len_i32, target, mode, seed, ignore_index)
+    return PolicyHeadFn.apply(logit, cand_len_i32, target, mode, seed, ignore_index, forced)
 
 
 # ----------------------------------------------------------------------------------- LSTM

@@ -5,10 +5,14 @@
 train.py does `from param import args`, `from agent_dg import Seq2SeqAgent`, and its helpers import
 `model`, `vilmodel`, `r2rmodel`. This launcher binds those module names to dasa_amd.r2r (whose
 classes, signatures, state_dict keys and args flags match the reference), parses the command line
-into the shared `args` like param.py does at import, and executes train.py as __main__. The speaker
-(back-translation, `speaker` module) is ours as well. Everything else (env, utils, eval, tokenizers,
-MatterSim) is the reference's own code. Names the policy modules do not define (e.g. the alternative
-decoders) resolve to the reference's definitions, loaded under a private module name.
+into the shared `args` like param.py does at import, and executes train.py as __main__. In the
+listener modes (the speaker only back-translates through `infer_batch`) the speaker module and its
+model classes are ours as well; `--train speaker` / `validspeaker` / `all` train or validate the
+speaker (train, valid, teacher_forcing, beam_search), which is outside the policy path, so there the
+reference's `speaker` module and `model.SpeakerEncoder/SpeakerDecoder` are used unchanged. Everything
+else (env, utils, eval, tokenizers, MatterSim) is the reference's own code. Names the policy modules do
+not define (e.g. the alternative decoders) resolve to the reference's definitions, loaded under a
+private module name.
 """
 import importlib.util
 import os
@@ -25,10 +29,16 @@ def _load_reference(name, path):
     return mod
 
 
-def _proxy(ours, ref_dir, name):
-    """Module `name`: our definitions, falling back to the reference module for anything else."""
+# train.py modes whose speaker only runs infer_batch (train.py:165-171, agent_dg.py:656-677)
+SPEAKER_INFER_MODES = ("listener", "validlistener", "auglistener")
+SPEAKER_NAMES = ("SpeakerEncoder", "SpeakerDecoder")
+
+
+def _proxy(ours, ref_dir, name, exclude=()):
+    """Module `name`: our definitions (minus `exclude`), falling back to the reference module for
+    anything else."""
     px = types.ModuleType(name)
-    px.__dict__.update({k: v for k, v in vars(ours).items() if not k.startswith("__")})
+    px.__dict__.update({k: v for k, v in vars(ours).items() if not k.startswith("__") and k not in exclude})
     ref_path = os.path.join(ref_dir, name + ".py")
     state = {}
 
@@ -56,9 +66,13 @@ def main(argv=None):
     param.parse(sys.argv[1:], make_dirs=True)
     sys.modules["param"] = param
     from dasa_amd.r2r import agent_dg, model, r2rmodel, speaker, vilmodel
-    for name, ours in (("model", model), ("vilmodel", vilmodel), ("r2rmodel", r2rmodel), ("agent_dg", agent_dg),
-                       ("speaker", speaker)):
-        sys.modules[name] = _proxy(ours, ref_dir, name)
+    ours_speaker = param.args.train in SPEAKER_INFER_MODES
+    binds = [("model", model), ("vilmodel", vilmodel), ("r2rmodel", r2rmodel), ("agent_dg", agent_dg)]
+    if ours_speaker:
+        binds.append(("speaker", speaker))
+    for name, ours in binds:
+        excl = SPEAKER_NAMES if (name == "model" and not ours_speaker) else ()
+        sys.modules[name] = _proxy(ours, ref_dir, name, excl)
     runpy.run_path(script, run_name="__main__")
     return 0
 

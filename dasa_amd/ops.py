@@ -170,15 +170,36 @@ def to_bf16(x, out=None):
     return out
 
 
+def _stream_safe(entry_ev, entry_stream, tensors):
+    """A derived weight copy built on `entry_stream` and used from the current stream: the user waits
+    for the build (event) and the allocator keeps the copy alive for the user's stream, as
+    vilmodel._fused_weights does (the LXRT layer runs the shared visual_attention on two streams)."""
+    if _stream() == entry_stream or torch.cuda.is_current_stream_capturing():
+        return          # same stream, or built by the pre-capture warm-up the capture stream follows
+    cur = torch.cuda.current_stream()
+    cur.wait_event(entry_ev)
+    for t in tensors:
+        t.record_stream(cur)
+
+
+def _built_here():
+    """(event recorded after the build, the building stream's raw handle)."""
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream())
+    return ev, _stream()
+
+
 def _bf16_weight(W):
     key = (W.data_ptr(), W._version, tuple(W.shape), W.stride(0))
-    t = _bf16_w.get(key)
-    if t is None:
+    e = _bf16_w.get(key)
+    if e is None:
         if len(_bf16_w) > 1024:
             _bf16_w.clear()
         t = to_bf16(W)
-        _bf16_w[key] = t
-    return t
+        _bf16_w[key] = (t,) + _built_here()
+        return t
+    _stream_safe(e[1], e[2], (e[0],))
+    return e[0]
 
 
 def gemm_bf16(x, Wb, out, *, M, N, K, lda, ldc, bias=None, act=None, aux=None, ld_aux=0, colscale=None,
@@ -232,6 +253,7 @@ def _x6_weight(W):
     wid = id(W)
     e = _X6.get(wid)
     if e is not None and e[0]() is W and e[1] == W._version and e[2] == W.data_ptr():
+        _stream_safe(e[4], e[5], (e[3],))
         return e[3]
     planes = split3_bf16(W)
 
@@ -239,7 +261,7 @@ def _x6_weight(W):
         ent = _X6.get(wid)
         if ent is not None and ent[0] is ref:
             del _X6[wid]
-    _X6[wid] = (weakref.ref(W, _drop), W._version, W.data_ptr(), planes)
+    _X6[wid] = (weakref.ref(W, _drop), W._version, W.data_ptr(), planes) + _built_here()
     return planes
 
 
@@ -500,11 +522,12 @@ def mha_bwd(Q, K, V, probs, dout, heads, scale, drop_p=0.0, seed=0):
 
 
 # ------------------------------------------------------------------------------ policy head
-POLICY_MODES = {"teacher": 0, "argmax": 1, "sample": 2}
+POLICY_MODES = {"teacher": 0, "argmax": 1, "sample": 2, "forced": 3}
 
 
-def policy_head_fwd(logit, cand_len_i32, target, mode, seed, ignore_index=-100):
+def policy_head_fwd(logit, cand_len_i32, target, mode, seed, ignore_index=-100, forced=None):
     """One step's candidate mask + CE + action (include/dasa_hip.h dasa_policy_head_fwd).
+    mode "forced": `forced` [B] int64 (device) is the action, entropy / log-prob as in "sample".
     Returns (ce_sum [], ent [B], logp_a [B], action [B] int64 or None, logp [B, C])."""
     _f32(logit, "policy_head.logit")
     B, C = logit.shape
@@ -515,7 +538,12 @@ def policy_head_fwd(logit, cand_len_i32, target, mode, seed, ignore_index=-100):
     ent = torch.empty(B, dtype=torch.float32, device=dev)
     logp_a = torch.empty(B, dtype=torch.float32, device=dev)
     m = POLICY_MODES[mode]
-    action = torch.empty(B, dtype=torch.int64, device=dev) if m != 0 else None
+    if m == 3:
+        if forced is None or forced.dtype != torch.int64 or forced.shape != (B,):
+            raise _lib.DasaError("policy_head mode 'forced' needs an int64 [B] action tensor")
+        action = forced.contiguous()
+    else:
+        action = torch.empty(B, dtype=torch.int64, device=dev) if m != 0 else None
     ws = torch.empty(B, dtype=torch.float32, device=dev)
     tgt = target.contiguous() if target is not None else None
     _call("dasa_policy_head_fwd", "policy_head", _lib.lib().dasa_policy_head_fwd, _p(logit), logit.stride(0),
@@ -716,9 +744,22 @@ def bilstm_fwd(xproj, whh_f, whh_b, lengths_i32, H, save=False):
     return out, h_n, c_n, ((sa, sc) if save else None)
 
 
+_PERSIST_BWD = [False]
+
+
+def persistent_bwd_ran():
+    """True (once) if a persistent bi-LSTM BPTT (B <= 32, lstm_persist.hip bilstm_persist_ok) was
+    enqueued since the last call: its barrier timeout poisons dgates and is only visible through
+    the device error word, so the caller checks it before the gradients are used."""
+    r, _PERSIST_BWD[0] = _PERSIST_BWD[0], False
+    return r
+
+
 def bilstm_bwd(whh_f, whh_b, lengths_i32, saved, dout, dh_n, dc_n, H):
     sa, sc = saved
     L, _, B, _ = sa.shape
+    if B <= 32 and H % 256 == 0 and 256 <= H <= 1024:
+        _PERSIST_BWD[0] = True
     dev = sa.device
     dgates = torch.empty(B, L, 2, 4 * H, dtype=torch.float32, device=dev)
     ws = torch.empty(_lib.lib().dasa_bilstm_bwd_workspace(B, H) // 4 + 4, dtype=torch.float32, device=dev)

@@ -131,6 +131,73 @@ class DGAdaChannel(nn.Module):
         return out
 
 
+# the pretraining heads of r2rpretrain_class.py:106-147 / :150-199 that a `.bert` hand-off drops
+PRETRAIN_HEADS = {"DicAddActionPreTrain": ("next_action.", "mlmhead."),
+                  "DicPMActionPreTrain": ("next_action.", "mlmhead.", "critic.")}
+
+
+def _legacy_key(k):
+    """pytorch_transformers' from_pretrained renames TF-style LayerNorm keys (gamma/beta)."""
+    return k.replace("gamma", "weight") if "gamma" in k else (k.replace("beta", "bias") if "beta" in k else k)
+
+
+def load_pretrained_bert(path, model_type="DicAddActionPreTrain"):
+    """The DicModel of a pretrained checkpoint (agent_dg.py:165-188), loaded with the safe loader.
+
+    * DicAddActionPreTrain (the README flag): `path` is a from_pretrained directory — config.json gives
+      the architecture (vl_layers, la_layers, hidden sizes), pytorch_model.bin the weights.
+    * DicPMActionPreTrain: `path` is a torch.save({'state_dict': ...}) file; the architecture is
+      bert-base with the command line's d_vl_layers / d_la_layers (agent_dg.py:166-177).
+    Stricter than pytorch_transformers' non-strict load: every DicModel key must be present, and every
+    other key must belong to the model type's pretraining heads (PRETRAIN_HEADS); anything else raises
+    instead of leaving randomly initialised layers behind silently."""
+    from .vilmodel import BertConfig, DicModel
+    from .._lib import DasaError
+    if model_type not in PRETRAIN_HEADS:
+        raise DasaError("--pretrain_model_type %r is not a DASA pretraining model" % model_type)
+    if model_type == "DicPMActionPreTrain":
+        cfg = BertConfig.from_pretrained("bert-base-uncased")
+        cfg.img_feature_dim, cfg.img_feature_type = 2048 + args.angle_feat_size, ""
+        cfg.update_lang_bert = cfg.update_add_layer = True
+        cfg.vl_layers, cfg.la_layers, cfg.action_space = args.d_vl_layers, args.d_la_layers, 36
+        states = torch.load(path, map_location="cpu", weights_only=True)
+        if not isinstance(states, dict) or "state_dict" not in states:
+            raise DasaError("%s: a DicPMActionPreTrain checkpoint is {'state_dict': ...}" % path)
+        sd = states["state_dict"]
+    else:
+        if not os.path.isdir(path):
+            raise DasaError("%s: a DicAddActionPreTrain checkpoint is a directory (config.json + "
+                            "pytorch_model.bin)" % path)
+        with open(os.path.join(path, "config.json")) as f:
+            cfg = BertConfig(**json.load(f))
+        sd = torch.load(os.path.join(path, "pytorch_model.bin"), map_location="cpu", weights_only=True)
+    for need in ("img_feature_dim", "vl_layers", "la_layers"):
+        if not hasattr(cfg, need):
+            raise DasaError("%s: the checkpoint config has no %r" % (path, need))
+    if not hasattr(cfg, "img_feature_type"):
+        cfg.img_feature_type = ""
+    for flag in ("update_lang_bert", "update_add_layer"):
+        if not hasattr(cfg, flag):
+            setattr(cfg, flag, True)
+    bert = DicModel(cfg)
+    heads = PRETRAIN_HEADS[model_type]
+    bert_sd, stray = {}, []
+    for k, v in sd.items():
+        k = _legacy_key(k)
+        if k.startswith("bert."):
+            bert_sd[k[len("bert."):]] = v
+        elif not k.startswith(heads):
+            stray.append(k)
+    want = set(bert.state_dict())
+    missing, unexpected = sorted(want - set(bert_sd)), sorted(set(bert_sd) - want)
+    if stray or missing or unexpected:
+        raise DasaError("%s: not a %s checkpoint of this architecture (keys outside bert.* and the heads %s: "
+                        "%s; missing: %s; unexpected: %s)" % (path, model_type, heads, stray[:5], missing[:5],
+                                                              unexpected[:5]))
+    bert.load_state_dict(bert_sd, strict=True)
+    return bert
+
+
 class Seq2SeqAgent(BaseAgent):
     """agent_dg.py:102-1510 (encoder_type 'Dic' — the DASA configuration)."""
 
@@ -194,17 +261,22 @@ class Seq2SeqAgent(BaseAgent):
         self.losses = []
         self.criterion = nn.CrossEntropyLoss(ignore_index=args.ignoreid, reduction="sum")
         self.logs = defaultdict(list)
-        self.sample_fn = None        # test hook: probs -> actions, replaces Categorical sampling
+        self.sample_fn = None        # test hook: probs -> actions, replaces Categorical sampling (torch head)
+        # test hook: (step, candidate lengths) -> int64 [B] actions replacing the draw of the sampled
+        # rollout while the one-kernel policy head stays on (dasa_policy_head_fwd mode FORCED)
+        self.force_action_fn = None
         self._step_graphs = None     # captured forward-only decision steps (_graph_step)
         self.grad_sync = None        # data-parallel hook set by dasa_amd.dp
 
     def _load_pretrained_bert(self, path):
-        """--pretrain_model_name: load `bert.*` weights from a local state dict file (safe loader)."""
-        fn = os.path.join(path, "pytorch_model.bin") if os.path.isdir(path) else path
-        sd = torch.load(fn, map_location="cpu", weights_only=True)
-        sd = sd.get("state_dict", sd)
-        bert_sd = {k[len("bert."):]: v for k, v in sd.items() if k.startswith("bert.")}
-        self.encoder.bert.load_state_dict(bert_sd, strict=False)
+        """--pretrain_model_name (agent_dg.py:165-188): the encoder's DicModel becomes the pretrained
+        model's `.bert` — its depth (vl_layers / la_layers) is the checkpoint's, not the command line's —
+        then dropout and the update flags are reset from args as the reference does."""
+        bert = load_pretrained_bert(path, args.pretrain_model_type)
+        self.encoder.bert = bert.to(self.device)
+        self.encoder.drop = nn.Dropout(p=args.d_dropout_ratio)
+        self.encoder.bert.update_lang_bert = self.encoder.bert.config.update_lang_bert = args.d_transformer_update
+        self.encoder.bert.update_add_layer = self.encoder.bert.config.update_add_layer = args.d_update_add_layer
 
     # ------------------------------------------------------------------ observation -> tensors
     def _sort_batch(self, obs):
@@ -674,7 +746,12 @@ class Seq2SeqAgent(BaseAgent):
                 hidden_states.append(h_t)
                 fused = self._fused_head(logit)
                 if fused:          # mask + CE + action + entropy / log-prob in one kernel (policy.hip)
-                    ce, ent, lpa, a_dev = DF.policy_head(logit, self._lens_dev(candidate_leng), target, self.feedback)
+                    mode, forced = self.feedback, None
+                    if mode == "sample" and self.force_action_fn is not None:
+                        mode = "forced"
+                        forced = self._to_dev(np.asarray(self.force_action_fn(t, list(candidate_leng)), np.int64))
+                    ce, ent, lpa, a_dev = DF.policy_head(logit, self._lens_dev(candidate_leng), target, mode,
+                                                         forced=forced)
                     total_forth_loss += ce
                     if self.feedback == "argmax":
                         a_t = a_dev
@@ -862,6 +939,8 @@ class Seq2SeqAgent(BaseAgent):
             self.loss.backward()
         DF.flush_bilstm_backward()
         DF.flush_weight_grads()
+        if ops.persistent_bwd_ran():
+            ops.check_device_errors()   # a timed-out BPTT barrier NaN-poisons dgates: raise before any step
         if self.grad_sync is not None:
             self.grad_sync()
         torch.nn.utils.clip_grad_norm_(self.encoder.parameters(), 40.0)

@@ -49,7 +49,10 @@ class NavGraph:
         self.dist = dijkstra(adj, directed=False)
 
     def distance(self, a, b):
-        return float(self.dist[self.index[a], self.index[b]])
+        d = float(self.dist[self.index[a], self.index[b]])
+        if not np.isfinite(d):   # networkx's all-pairs dict has no entry here: the reference raises KeyError
+            raise KeyError("no path between %s and %s in the navigation graph" % (a, b))
+        return d
 
 
 def load_nav_graphs(scans, conn_dir="connectivity"):

@@ -109,15 +109,22 @@ class BAttnDecoderLSTM(nn.Module):
         self.input_noise = self.drop(torch.ones(shape, device=dev))
         self.output_noise = self.drop(torch.ones(shape, device=dev))
 
+    def _drop_env_feat(self, feat, angle):
+        """feat[..., :-angle] = drop_env(feat[..., :-angle]) (model.py:506-508, 556-557), out of place:
+        the counter-RNG dropout kernel for an nn.Dropout, else the module itself (a caller's stand-in)."""
+        if isinstance(self.drop_env, nn.Dropout):
+            return DF.feat_drop(feat, self.drop_env.p, self.training, angle)
+        return torch.cat((self.drop_env(feat[..., :-angle]), feat[..., -angle:]), -1)
+
     def forward(self, action, feature, cand_feat, h_0, prev_h1, c_0, ctx, ctx_mask=None, already_dropfeat=False):
         training = self.training
-        p, pf = self.drop.p, self.drop_env.p
+        p = self.drop.p
         angle = args.angle_feat_size
         aux_outputs = {}
         a_emb = DF.linear(action, self.embedding[0].weight, self.embedding[0].bias, "tanh")
         a_emb = DF.dropout(a_emb, p, training)
         if not already_dropfeat:
-            feature = DF.feat_drop(feature, pf, training, angle)
+            feature = self._drop_env_feat(feature, angle)
         prev_h1_drop = DF.dropout(prev_h1, p, training)
         attn_feat, _ = self.feat_att_layer(prev_h1_drop, feature, output_tilde=False)
         h_1, c_1 = DF.LSTMCellFn.apply(a_emb, attn_feat, prev_h1, c_0, self.lstm.weight_ih, self.lstm.weight_hh,
@@ -132,7 +139,7 @@ class BAttnDecoderLSTM(nn.Module):
         else:
             h_tilde_drop = DF.dropout(h_tilde, p, training)
         if not already_dropfeat:
-            cand_feat = DF.feat_drop(cand_feat, pf, training, angle)
+            cand_feat = self._drop_env_feat(cand_feat, angle)
         logit = self.candidate_att_layer.logits(h_tilde_drop, cand_feat)
         if self.pred_back:
             q = prev_h1 if args.back_input == "pre" else h_tilde_drop

@@ -47,15 +47,16 @@ def init_param_dict(shapes, seed):
             for k in sorted(shapes.keys())}
 
 
-def init_params(module, seed):
-    """Overwrite every parameter/buffer-free state entry of `module` deterministically."""
+def init_params(module, seed, skip_prefix=()):
+    """Overwrite every parameter/buffer-free state entry of `module` deterministically (entries whose
+    key starts with one of `skip_prefix` keep their values and draw nothing from the stream)."""
     import torch
     rng = np.random.default_rng(seed)
     sd = module.state_dict()
     new = {}
     for k in sorted(sd.keys()):
         v = sd[k]
-        if not torch.is_floating_point(v):
+        if not torch.is_floating_point(v) or any(k.startswith(p) for p in skip_prefix):
             new[k] = v
             continue
         arr = param_init_array(k, tuple(v.shape), rng)

@@ -239,13 +239,17 @@ int dasa_gather_rows(const float* ta, const int32_t* ia, int32_t Fa, const float
 int dasa_reverse_valid(const float* x, const int32_t* lengths, float* out, int32_t B, int32_t L,
                        int32_t H, void* stream);
 /* ---- policy head (agent_dg.py:832-886) ------------------------------------------------------- */
-enum dasa_policy_mode { DASA_POLICY_TEACHER = 0, DASA_POLICY_ARGMAX = 1, DASA_POLICY_SAMPLE = 2 };
+enum dasa_policy_mode { DASA_POLICY_TEACHER = 0, DASA_POLICY_ARGMAX = 1, DASA_POLICY_SAMPLE = 2,
+                        DASA_POLICY_FORCED = 3 };
 /* One decision step's loss/action stage on logit [B][C] (row stride ld): candidates c >= cand_len[b]
  * are masked (-inf); logp [B][C] = masked log-softmax (saved for backward); ce_sum[0] = sum over rows
  * with target != ignore_index of -logp[target] (CrossEntropyLoss(reduction='sum')); mode ARGMAX:
  * action = first argmax; mode SAMPLE: action ~ Categorical(softmax) by inverse CDF on the counter RNG
  * (seed, row); ent [B] = entropy, logp_a [B] = logp[action] (each optional). target may be NULL (no
- * CE, ce_sum = 0). C <= 256. ws: B floats of scratch. One launch, deterministic. */
+ * CE, ce_sum = 0). C <= 256. ws: B floats of scratch. One launch, deterministic.
+ * Mode FORCED is mode SAMPLE with the draw replaced by the caller's action[b] (an INPUT, 0 <= action[b]
+ * < cand_len[b]): entropy and logp_a as in SAMPLE. It pins the sampled rollout's loss stage against a
+ * reference run whose Categorical.sample returns the same actions (tests/test_policy_gpu.py). */
 int dasa_policy_head_fwd(const float* logit, int64_t ld, const int32_t* cand_len, const int64_t* target,
                          int32_t B, int32_t C, int32_t mode, int32_t ignore_index, uint64_t seed,
                          float* logp, float* ce_sum, float* ent, float* logp_a, int64_t* action,

@@ -154,12 +154,12 @@ class Recorder:
         agent.decoder.forward = dec_wrap
 
 
-def make_agent(R, env, episode_len):
+def make_agent(R, env, episode_len, tok=None, skip_bert=False):
     import io
     import contextlib
     with contextlib.redirect_stdout(io.StringIO()):
-        agent = R.agent_dg.Seq2SeqAgent(env, "", None, episode_len, "Dic")
-    init_params(agent.encoder, GI.SEED_ENC)
+        agent = R.agent_dg.Seq2SeqAgent(env, "", tok, episode_len, "Dic")
+    init_params(agent.encoder, GI.SEED_ENC, skip_prefix=("bert.",) if skip_bert else ())
     init_params(agent.decoder, GI.SEED_DEC)
     init_params(agent.critic, GI.SEED_CRITIC)
     init_params(agent.adaIn, GI.SEED_ADA)
@@ -238,27 +238,35 @@ def _zero_dropout(agent):
                 sub.p = 0.0
 
 
-def _train_iteration(R, agent, out, prefix):
-    """accumulate_gradient('sample') with argmax 'sampling', then backward; losses + gradients."""
+def _train_iteration(R, agent, out, prefix, sample=None, **kw):
+    """accumulate_gradient('sample') with argmax 'sampling' (or `sample`, a Categorical.sample
+    replacement: GI.reference_forced_sample), then backward; losses, logs + gradients."""
     A = R.args
     A.ml_weight = A.ml_weight_org
     orig_sample = torch.distributions.Categorical.sample
-    torch.distributions.Categorical.sample = lambda self, *a, **k: self.probs.argmax(-1)
+    torch.distributions.Categorical.sample = sample or (lambda self, *a, **k: self.probs.argmax(-1))
     try:
         agent.zero_grad()
-        agent.accumulate_gradient("sample")
+        agent.accumulate_gradient("sample", **kw)
     finally:
         torch.distributions.Categorical.sample = orig_sample
+    _record_losses(agent, out, prefix)
+    agent.loss.backward()
+    for name, mod in (("encoder", agent.encoder), ("decoder", agent.decoder), ("critic", agent.critic),
+                      ("adaIn", agent.adaIn)):
+        grad_record(out, f"{prefix}{name}.", mod.named_parameters())
+
+
+def _record_losses(agent, out, prefix):
     out[prefix + "loss"] = np.array(agent.loss.item())
     out[prefix + "ml_loss_teacher"] = np.array(agent.logs["ml_loss"][0])
     out[prefix + "ml_loss_sample"] = np.array(agent.logs["ml_loss"][1])
     out[prefix + "rl_loss"] = np.array(agent.logs["normalized_rl_loss"][-1])
     out[prefix + "steps_teacher"] = np.array(agent.logs["viewsteps/teacher"][-1])
     out[prefix + "steps_sample"] = np.array(agent.logs["viewsteps/sample"][-1])
-    agent.loss.backward()
-    for name, mod in (("encoder", agent.encoder), ("decoder", agent.decoder), ("critic", agent.critic),
-                      ("adaIn", agent.adaIn)):
-        grad_record(out, f"{prefix}{name}.", mod.named_parameters())
+    for k in ("entropy", "critic_loss", "forth_loss", "total"):
+        if agent.logs.get(k):
+            out[prefix + "logs/" + k] = np.array(agent.logs[k], np.float64)
 
 
 def _eval_rollout(agent, feedback, out, prefix, keep_states=()):
@@ -310,6 +318,189 @@ def cfg2(R):
     agent = make_agent(R, env, cfg["train_max_action"])
     _zero_dropout(agent)
     _train_iteration(R, agent, out, "train/")
+    # the same iteration with the sampled rollout's draws replaced by a seeded action table (valid
+    # candidates only): the product runs its one-kernel policy head (teacher CE, sampled entropy and
+    # log-prob) in both rollouts against it
+    env = SynthR2RBatch(world, cfg["batch"], seed=cfg["train_seed"], mode="goal", instr_len=cfg["instr_len"],
+                        variable_len=True)
+    agent = make_agent(R, env, cfg["train_max_action"])
+    _zero_dropout(agent)
+    sample, _ = GI.reference_forced_sample(GI.forced_table(cfg["train_max_action"], cfg["batch"]))
+    _train_iteration(R, agent, out, "trainf/", sample=sample)
+    return out
+
+
+def aug(R):
+    """The aug half of the auglistener iteration (train.py:237-239): accumulate_gradient('sample',
+    speaker=...) — the speaker back-translates each rollout's teacher path with the shared env-drop
+    noise (speaker.py:293-295), the listener re-tokenises the instructions (agent_dg.py:656-677), both
+    rollouts apply the noise after AdaIN (:780-785) and the A2C bootstrap applies it to the raw
+    features (:946-952), the decoder with already_dropfeat=True (model.py:506-508, 556-557). Dropout 0
+    except the env-drop mask (GI.FixedEnvDrop); sampled draws from the forced table."""
+    import contextlib
+    import importlib
+    import io
+    A = R.args
+    cfg = GI.CFG_AUG
+    if not hasattr(np, "bool"):
+        np.bool = bool
+    A.d_vl_layers, A.batchSize, A.views, A.maxAction = cfg["vl_layers"], cfg["batch"], 36, cfg["max_action"]
+    A.maxDecode = cfg["max_decode"]
+    with contextlib.redirect_stdout(io.StringIO()):
+        stok = R.utils.Tokenizer(vocab=R.utils.read_vocab(os.path.join(ROOT, "tests", "golden", "train_vocab.txt")),
+                                 encoding_length=A.maxInput)
+    world = SynthWorld(n_viewpoints=cfg["viewpoints"], feat_seed=0, graph_seed=cfg["graph_seed"])
+    env = SynthR2RBatch(world, cfg["batch"], seed=cfg["env_seed"], mode="goal", instr_len=80, variable_len=True)
+    agent = make_agent(R, env, cfg["max_action"], tok=GI.WordHashBTokenizer(A.maxInput))
+    _zero_dropout(agent)
+    agent.decoder.drop_env = GI.FixedEnvDrop(GI.env_drop_mask())
+    spk_mod = importlib.import_module("speaker")
+    with contextlib.redirect_stdout(io.StringIO()):
+        spk = spk_mod.Speaker(env, agent, stok)
+    GI.scale_params(init_params(spk.encoder, cfg["seed_enc"]), cfg["spk_scale"])
+    GI.scale_params(init_params(spk.decoder, cfg["seed_dec"]), cfg["spk_scale"])
+    margins = []
+    dec_fwd = spk.decoder.forward
+
+    def dec_rec(*a, **k):      # top-2 logit margin of every decoded word (an argmax flip needs < ~1e-4)
+        r = dec_fwd(*a, **k)
+        lg = r[0].detach().view(r[0].shape[0], -1).clone()
+        lg[:, stok.word_to_index["<UNK>"]] = -float("inf")
+        top = lg.topk(2, dim=1).values
+        margins.append(float((top[:, 0] - top[:, 1]).min()))
+        return r
+    spk.decoder.forward = dec_rec
+    insts = []
+    reset = env.reset
+
+    def reset_rec(batch=None, **k):
+        if batch is not None:
+            insts.append(np.stack([np.asarray(d["instr_encoding"], np.int64) for d in batch]))
+        return reset(batch, **k)
+    env.reset = reset_rec
+    rec = Recorder(agent)
+    out = {}
+    sample, _ = GI.reference_forced_sample(GI.forced_table(cfg["max_action"], cfg["batch"]))
+    _train_iteration(R, agent, out, "aug/", sample=sample, speaker=spk)
+    assert len(insts) == 2, len(insts)       # one back-translation per rollout (teacher, sample)
+    for i, x in enumerate(insts):
+        out[f"aug/instr_encoding/{i}"] = x
+    for t, lg in enumerate(rec.rec["logit"]):
+        out[f"aug/logit/{t}"] = lg
+    out["aug/n_decoder_calls"] = np.array(len(rec.rec["logit"]))
+    out["aug/speaker_min_margin"] = np.array(min(margins))
+    return out
+
+
+def optim(R):
+    """Two training iterations, each zero_grad -> accumulate_gradient('sample') -> optim_step
+    (agent_dg.py:1340-1405: backward, clip_grad_norm 40 on encoder + decoder, RMSprop on all four
+    optimizers, LambdaLR on decoder / critic / adaIn): per iteration the clip norms, every optimizer's
+    learning rate, and per parameter the RMSprop square_avg and the parameter change."""
+    A = R.args
+    cfg = GI.CFG_OPTIM
+    A.d_vl_layers, A.batchSize, A.maxAction, A.views = cfg["vl_layers"], cfg["batch"], cfg["max_action"], 36
+    world = SynthWorld(n_viewpoints=16, feat_seed=0, graph_seed=3)
+    env = SynthR2RBatch(world, cfg["batch"], seed=cfg["env_seed"], mode="goal", instr_len=cfg["instr_len"],
+                        variable_len=True)
+    agent = make_agent(R, env, cfg["max_action"])
+    _zero_dropout(agent)
+    A.ml_weight = A.ml_weight_org
+    mods = (("encoder", agent.encoder, agent.encoder_optimizer), ("decoder", agent.decoder, agent.decoder_optimizer),
+            ("critic", agent.critic, agent.critic_optimizer), ("adaIn", agent.adaIn, agent.adaIn_optimizer))
+    norms = []
+    orig_clip = torch.nn.utils.clip_grad_norm
+    orig_sample = torch.distributions.Categorical.sample
+    out = {}
+    try:
+        torch.nn.utils.clip_grad_norm = lambda params, m, *a, **k: norms.append(float(orig_clip(params, m, *a, **k)))
+        for it in range(cfg["iters"]):
+            sample, _ = GI.reference_forced_sample(GI.forced_table(cfg["max_action"], cfg["batch"],
+                                                                   seed=GI.FORCED_SEED + it))
+            torch.distributions.Categorical.sample = sample
+            before = {name: {k: p.detach().clone() for k, p in m.named_parameters()} for name, m, _ in mods}
+            agent.zero_grad()
+            agent.accumulate_gradient("sample")
+            out[f"opt{it}/loss"] = np.array(agent.loss.item())
+            norms.clear()
+            agent.optim_step()
+            out[f"opt{it}/clip_norms"] = np.array(norms, np.float64)      # encoder, decoder
+            for name, m, opt in mods:
+                out[f"opt{it}/lr/{name}"] = np.array([g["lr"] for g in opt.param_groups], np.float64)
+                for k, p in m.named_parameters():
+                    if p.grad is None:
+                        continue
+                    H.grad_record(out, f"opt{it}/delta/{name}.{k}", p.detach() - before[name][k])
+                    H.grad_record(out, f"opt{it}/sq/{name}.{k}", opt.state[p]["square_avg"])
+    finally:
+        torch.nn.utils.clip_grad_norm = orig_clip
+        torch.distributions.Categorical.sample = orig_sample
+    return out
+
+
+def cfg4_readme(R):
+    """cfg4 at the README finetune configuration (README.md:104-116: --d_update_add_layer True,
+    d_vl_layers 3, batchSize 2): one training iteration at maxAction 6 with dropout 0 and the sampled
+    draws from the forced table, so the LXRT stack (vl=3) and VisionEncoder backward are pinned."""
+    A = R.args
+    cfg = GI.CFG4R
+    A.d_vl_layers, A.batchSize, A.maxAction, A.views = cfg["vl_layers"], cfg["batch"], cfg["max_action"], 36
+    A.d_update_add_layer = True
+    out = {}
+    try:
+        world = SynthWorld(n_viewpoints=16, feat_seed=0, graph_seed=3)
+        env = SynthR2RBatch(world, cfg["batch"], seed=cfg["env_seed"], mode="goal", instr_len=cfg["instr_len"],
+                            variable_len=True)
+        agent = make_agent(R, env, cfg["max_action"])
+        assert agent.encoder.bert.update_add_layer
+        _zero_dropout(agent)
+        sample, _ = GI.reference_forced_sample(GI.forced_table(cfg["max_action"], cfg["batch"]))
+        _train_iteration(R, agent, out, "ft3/", sample=sample)
+    finally:
+        A.d_update_add_layer = False
+    return out
+
+
+def pretrain(R):
+    """--pretrain_model_name (agent_dg.py:165-188, README train flag): a DicAddActionPreTrain checkpoint
+    directory written here (config.json with vl_layers=2 — the command line says 3 — and
+    pytorch_model.bin holding bert.* plus the next_action / mlmhead pretraining heads, bert weights from
+    init_params(seed_bert)), loaded by the reference agent through from_pretrained; the non-bert weights
+    seeded as usual; an argmax eval rollout's logits and critic values. Records the checkpoint's config
+    and key layout so the product test writes the same directory."""
+    import importlib
+    import json
+    import tempfile
+    A = R.args
+    cfg = GI.CFG_PRE
+    A.d_vl_layers, A.batchSize, A.maxAction, A.views = 3, cfg["batch"], cfg["max_action"], 36
+    from pytorch_transformers import BertConfig
+    pc = importlib.import_module("r2rpretrain_class")
+    conf = BertConfig.from_pretrained("bert-base-uncased")
+    conf.img_feature_dim, conf.img_feature_type = 2048 + A.angle_feat_size, ""
+    conf.update_lang_bert = conf.update_add_layer = True
+    conf.vl_layers, conf.la_layers, conf.action_space = cfg["vl_layers_ckpt"], cfg["la_layers"], 36
+    pre = pc.DicAddActionPreTrain(conf)
+    init_params(pre.bert, cfg["seed_bert"])
+    d = tempfile.mkdtemp(prefix="dasa_pre_")
+    with open(os.path.join(d, "config.json"), "w") as f:
+        f.write(conf.to_json_string())
+    sd = pre.state_dict()
+    torch.save(sd, os.path.join(d, "pytorch_model.bin"))
+    out = {"pre/config": np.array(conf.to_json_string()),
+           "pre/head_schema": np.array(json.dumps({k: list(v.shape) for k, v in sd.items()
+                                                   if not k.startswith("bert.")}, sort_keys=True))}
+    A.pretrain_model_name = d
+    try:
+        world = SynthWorld(n_viewpoints=16, feat_seed=0, graph_seed=3)
+        env = SynthR2RBatch(world, cfg["batch"], seed=cfg["env_seed"], mode="goal", instr_len=cfg["instr_len"],
+                            variable_len=True)
+        agent = make_agent(R, env, cfg["max_action"], skip_bert=True)
+    finally:
+        A.pretrain_model_name = None
+    assert len(agent.encoder.bert.addlayer) == cfg["vl_layers_ckpt"]
+    out["pre/vl_layers"] = np.array(len(agent.encoder.bert.addlayer))
+    _eval_rollout(agent, "argmax", out, "pre/", keep_states=(0,))
     return out
 
 
@@ -581,6 +772,10 @@ FIXTURES = {
     "io": io_readers,
     "eval": eval_score,
     "speaker": speaker,
+    "aug": aug,
+    "optim": optim,
+    "cfg4_readme": cfg4_readme,
+    "pretrain": pretrain,
 }
 
 

@@ -6,6 +6,8 @@ standard BERT init (normal(0, initializer_range) for Linear/Embedding, zero bias
 golden generator overwrites every weight with seeded values afterwards anyway.
 """
 import copy
+import json
+import os
 
 import torch
 from torch import nn
@@ -33,6 +35,14 @@ class BertConfig:
     def to_dict(self):
         return copy.deepcopy(self.__dict__)
 
+    def to_json_string(self):
+        return json.dumps(self.to_dict(), indent=2, sort_keys=True) + "\n"
+
+    @classmethod
+    def from_json_file(cls, path):
+        with open(path) as f:
+            return cls(**json.load(f))
+
     def __repr__(self):
         return "BertConfig(%r)" % (self.__dict__,)
 
@@ -57,6 +67,52 @@ class BertPreTrainedModel(nn.Module):
     def init_weights(self):
         self.apply(self._init_weights)
 
+    def _tie_or_clone_weights(self, first_module, second_module):
+        """pytorch_transformers 1.x: the output embedding shares the input embedding's weight."""
+        first_module.weight = second_module.weight
+
     @classmethod
-    def from_pretrained(cls, *a, **k):
-        raise RuntimeError("pretrained checkpoints are unavailable offline")
+    def from_pretrained(cls, path, *a, **k):
+        """pytorch_transformers 1.x PreTrainedModel.from_pretrained restated for a LOCAL directory (the
+        name-based hub download is unavailable offline): config.json -> cls(config) -> non-strict load
+        of pytorch_model.bin (base_model_prefix handling; missing / unexpected keys are reported, not
+        raised) -> tie_weights -> eval()."""
+        if not os.path.isdir(path):
+            raise RuntimeError("pretrained checkpoints are unavailable offline (only a local directory loads)")
+        config = cls.config_class.from_json_file(os.path.join(path, "config.json"))
+        model = cls(config)
+        state_dict = torch.load(os.path.join(path, "pytorch_model.bin"), map_location="cpu", weights_only=True)
+        renames = {}
+        for key in state_dict:      # TF-style LayerNorm names
+            if "gamma" in key:
+                renames[key] = key.replace("gamma", "weight")
+            if "beta" in key:
+                renames[key] = key.replace("beta", "bias")
+        for old, new in renames.items():
+            state_dict[new] = state_dict.pop(old)
+        missing, unexpected, errors = [], [], []
+        metadata = getattr(state_dict, "_metadata", None)
+        state_dict = state_dict.copy()
+        if metadata is not None:
+            state_dict._metadata = metadata
+
+        def load(module, prefix=""):
+            local_metadata = {} if metadata is None else metadata.get(prefix[:-1], {})
+            module._load_from_state_dict(state_dict, prefix, local_metadata, True, missing, unexpected, errors)
+            for name, child in module._modules.items():
+                if child is not None:
+                    load(child, prefix + name + ".")
+        start_prefix = ""
+        model_to_load = model
+        if not hasattr(model, cls.base_model_prefix) and any(s.startswith(cls.base_model_prefix) for s in state_dict):
+            start_prefix = cls.base_model_prefix + "."
+        if hasattr(model, cls.base_model_prefix) and not any(s.startswith(cls.base_model_prefix) for s in state_dict):
+            model_to_load = getattr(model, cls.base_model_prefix)
+        load(model_to_load, prefix=start_prefix)
+        if errors:
+            raise RuntimeError("Error(s) in loading state_dict for %s:\n\t%s" % (cls.__name__, "\n\t".join(errors)))
+        model.load_report = {"missing": missing, "unexpected": unexpected}
+        if hasattr(model, "tie_weights"):
+            model.tie_weights()
+        model.eval()
+        return model

@@ -114,3 +114,102 @@ def io_tables():
 # Speaker back-translation (speaker.py:265-350) at the auglistener batch: B=6 goal episodes (the teacher
 # path ends), weights seeded, eval mode, argmax decoding, maxDecode 12.
 SPEAKER = dict(batch=6, viewpoints=16, graph_seed=3, env_seed=41, max_decode=12, seed_enc=61, seed_dec=62)
+
+
+# ---- forced actions for the sampled rollout (the fused policy head at rollout level) ---------------
+# Categorical.sample is replaced, in the reference run, by a seeded table: at sampled step t row b takes
+# candidate floor(u[t, b] * n_b), n_b = the row's valid candidates (the nonzero probabilities); the
+# product passes the same actions to dasa_policy_head_fwd in mode FORCED (Seq2SeqAgent.force_action_fn).
+FORCED_SEED = 31
+
+
+def forced_table(steps, batch, seed=FORCED_SEED):
+    return np.random.default_rng(seed).random((steps, batch))
+
+
+def forced_actions(table, t, lens):
+    lens = np.asarray(lens, np.int64)
+    return np.minimum((table[t] * lens).astype(np.int64), lens - 1)
+
+
+def reference_forced_sample(table):
+    """A Categorical.sample replacement for the reference run: the t-th call returns the table's step t."""
+    state = {"t": 0}
+
+    def sample(self, *a, **k):
+        lens = (self.probs > 0).sum(-1).numpy()
+        out = torch.from_numpy(forced_actions(table, state["t"], lens))
+        state["t"] += 1
+        return out
+    return sample, state
+
+
+# ---- the aug half of the auglistener iteration (speaker + shared env-drop mask) -------------------
+# accumulate_gradient('sample', speaker=...) at B=4, vl=3: the speaker back-translates each rollout's
+# teacher path, the listener re-tokenises it, and both rollouts run with the shared env-drop noise
+# (agent_dg.py:656-677, 731-736, 780-785, 946-952). Every dropout is p=0 except the env-drop mask,
+# which is a fixed seeded mask (FixedEnvDrop) in both runs.
+# The speaker's seeded weights are scaled by spk_scale: at the 0.02 init every row decodes the same word
+# over and over; x10 gives row-dependent instructions (distinct listener token sequences per row).
+CFG_AUG = dict(batch=4, vl_layers=3, la_layers=9, max_action=4, viewpoints=16, graph_seed=3, env_seed=43,
+               max_decode=12, seed_enc=61, seed_dec=62, mask_seed=44, featdropout=0.4, spk_scale=10.0)
+
+
+def scale_params(module, s):
+    with torch.no_grad():
+        for p in module.parameters():
+            p.mul_(s)
+    return module
+
+
+def env_drop_mask(seed=CFG_AUG["mask_seed"], p=CFG_AUG["featdropout"], n=2048):
+    keep = np.random.default_rng(seed).random(n) >= p
+    return torch.from_numpy((keep / (1.0 - p)).astype(np.float32))
+
+
+class FixedEnvDrop(torch.nn.Module):
+    """decoder.drop_env replaced by a fixed mask: drop_env(ones(2048)) is the shared noise vector."""
+
+    def __init__(self, mask):
+        super().__init__()
+        self.register_buffer("mask", mask.clone())
+
+    def forward(self, x):
+        return x * self.mask.to(x.device)
+
+
+class WordHashBTokenizer:
+    """The listener's tokenizer in the aug loop is utils.BTokenizer (utils.py:581-616, bert-base-uncased
+    WordPiece, a name-based download unavailable offline). This stand-in keeps BTokenizer's contract —
+    [CLS]=101 + one id per word + [SEP]=102, padded with pad_token_id 0 to encoding_length, an over-long
+    encoding cut with [SEP] last — with word ids from a CRC of the word; both runs use it."""
+
+    class _T:
+        pad_token_id = 0
+        sep_token_id = 102
+
+    def __init__(self, encoding_length=80):
+        self.tokenizer = self._T()
+        self.encoding_length = encoding_length
+
+    def encode_sentence(self, sentence, seps=None):
+        import re
+        import zlib
+        words = [w for w in re.split(r"\s+", sentence.strip().lower()) if w]
+        enc = [101] + [1000 + zlib.crc32(w.encode()) % 29000 for w in words] + [102]
+        if len(enc) < self.encoding_length:
+            enc += [0] * (self.encoding_length - len(enc))
+        if len(enc) > self.encoding_length:
+            enc[self.encoding_length - 1] = 102
+        return np.array(enc[:self.encoding_length])
+
+
+# ---- optim_step after a training iteration (clip 40 + RMSprop + LambdaLR, agent_dg.py:1389-1405) ---
+CFG_OPTIM = dict(batch=2, vl_layers=1, la_layers=9, max_action=5, instr_len=80, iters=2, env_seed=8)
+
+# ---- cfg4 at its README configuration (README.md:104-116: vl=3, B=2, maxAction 35 -> 6 steps here) --
+CFG4R = dict(batch=2, vl_layers=3, la_layers=9, max_action=6, instr_len=80, env_seed=10)
+
+# ---- --pretrain_model_name (agent_dg.py:165-188): a DicAddActionPreTrain checkpoint directory -------
+# whose config.json says vl_layers=2 while the command line says d_vl_layers=3 (the checkpoint decides)
+CFG_PRE = dict(batch=2, vl_layers_ckpt=2, la_layers=9, max_action=5, instr_len=80, env_seed=12, seed_bert=71)

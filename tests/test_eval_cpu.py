@@ -25,3 +25,20 @@ def test_evaluation_matches_reference():
     assert set(scores) == set(want_scores)
     for k, v in want_scores.items():
         np.testing.assert_allclose(np.array(scores[k], np.float64), np.array(v), rtol=0, atol=1e-9, err_msg=k)
+
+
+def test_unreachable_viewpoint_raises():
+    """Two components (a-b, c-d): the reference's networkx distance dict has no a->c entry and raises
+    KeyError (eval.py:47-52); the restatement raises too instead of scoring an infinite distance."""
+    import pytest
+    from dasa_amd.r2r.eval import NavGraph
+
+    def vp(name, x, conn):
+        pose = [0.0] * 16
+        pose[3] = x
+        return {"image_id": name, "pose": pose, "included": True, "unobstructed": conn}
+    g = NavGraph([vp("a", 0.0, [False, True, False, False]), vp("b", 1.0, [True, False, False, False]),
+                  vp("c", 5.0, [False, False, False, True]), vp("d", 7.0, [False, False, True, False])])
+    assert g.distance("a", "b") == 1.0 and g.distance("c", "d") == 2.0
+    with pytest.raises(KeyError):
+        g.distance("a", "c")

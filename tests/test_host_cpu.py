@@ -130,6 +130,39 @@ def test_dropin_launcher_binds_reference_module_names(tmp_path, monkeypatch):
     assert r.returncode == 0 and "DROPIN-OK" in r.stdout, r.stderr[-2000:]
 
 
+@pytest.mark.parametrize("mode", ["validspeaker", "speaker"])
+def test_dropin_launcher_speaker_modes_use_reference_speaker(tmp_path, mode):
+    """--train speaker / validspeaker train or validate the speaker (speaker.train / valid,
+    train.py:111,593): the launcher leaves the reference's speaker module and model.Speaker* classes
+    bound there (ours provides infer_batch only), while the policy modules stay ours."""
+    import subprocess
+    import sys
+    (tmp_path / "model.py").write_text("SpeakerEncoder = 'ref-speaker-encoder'\nSpeakerDecoder = 'ref-speaker-decoder'\n")
+    (tmp_path / "speaker.py").write_text(
+        "import model\n"
+        "class Speaker:\n"
+        "    encoder_cls = model.SpeakerEncoder\n"
+        "    def train(self, n):\n        return 'ref-train'\n"
+        "    def valid(self, wrapper=None):\n        return 'ref-valid'\n")
+    (tmp_path / "train.py").write_text(
+        "from param import args\n"
+        "import model, agent_dg, speaker\n"
+        "assert agent_dg.Seq2SeqAgent.__module__.startswith('dasa_amd.r2r')\n"
+        "assert model.BAttnDecoderLSTM.__module__ == 'dasa_amd.r2r.model'\n"
+        "assert model.SpeakerEncoder == 'ref-speaker-encoder', model.SpeakerEncoder\n"
+        "assert model.SpeakerDecoder == 'ref-speaker-decoder'\n"
+        "assert speaker.Speaker.encoder_cls == 'ref-speaker-encoder'\n"
+        "assert speaker.Speaker().valid() == 'ref-valid' and speaker.Speaker().train(1) == 'ref-train'\n"
+        "print('SPEAKER-MODE-OK')\n")
+    from dasa_amd.r2r import param
+    flags = list(param.README_TRAIN_FLAGS)
+    flags[flags.index("--train") + 1] = mode
+    r = subprocess.run([sys.executable, "-m", "dasa_amd.launch", str(tmp_path / "train.py")] + flags,
+                       cwd=str(tmp_path), capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, PYTHONPATH=ROOT))
+    assert r.returncode == 0 and "SPEAKER-MODE-OK" in r.stdout, r.stderr[-2000:]
+
+
 @pytest.mark.parametrize("mode,seed", [("goal", 8), ("wander", 1000)])
 def test_teacher_plan_matches_stepwise_oracle(mode, seed):
     """Seq2SeqAgent._teacher_plan (env stepped through a whole teacher-forced episode before the

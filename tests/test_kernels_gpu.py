@@ -427,6 +427,69 @@ def test_policy_head(dev):
     freq = torch.bincount(acts, minlength=11).double() / N
     assert (freq - p).abs().max() < 0.03
     assert (lps.cpu().double() - torch.log(p)[acts]).abs().max() < 1e-5
+    # forced mode: the caller's actions, entropy / log-prob / gradients as for a sampled draw
+    a_f = torch.stack([torch.randint(0, int(n), (1,), generator=g)[0] for n in lens])
+    x2 = logit.double().requires_grad_(True)
+    z2 = x2.masked_fill(mask, -float("inf"))
+    cat2 = torch.distributions.Categorical(torch.softmax(z2, 1), validate_args=False)
+    ent2, lp2 = cat2.entropy(), cat2.log_prob(a_f)
+    ce2 = torch.nn.CrossEntropyLoss(ignore_index=-100, reduction="sum")(z2, target)
+    (ce2 * 0.3 + (ent2 * w_ent.double()).sum() + (lp2 * w_lp.double()).sum()).backward()
+    xf = logit.to(dev).requires_grad_(True)
+    ce_f, ent_f, lp_f, a_out = DF.policy_head(xf, lens32, target.to(dev), "forced", forced=a_f.to(dev))
+    (ce_f * 0.3 + (ent_f * w_ent.to(dev)).sum() + (lp_f * w_lp.to(dev)).sum()).backward()
+    assert torch.equal(a_out.cpu(), a_f)
+    assert abs(ce_f.item() - ce2.item()) < 1e-4 * max(1.0, abs(ce2.item()))
+    assert (ent_f.cpu().double() - ent2).abs().max() < 1e-5
+    assert (lp_f.cpu().double() - lp2).abs().max() < 1e-5
+    assert (xf.grad.cpu().double() - x2.grad).abs().max() < 1e-5
+
+
+def test_x6_weight_planes_first_use_on_two_streams(dev):
+    """ops._x6_weight caches the bf16 planes of a weight per version; the LXRT layer uses one weight
+    from its side stream and the main stream (vilmodel.py:309-316). A FRESH weight whose planes are
+    built on the side stream and first used on the main stream must wait for the split kernel."""
+    from dasa_amd import ops
+    g = torch.Generator().manual_seed(3)
+    M, N, K = 2048, 1024, 768          # 128 output tiles: the bf16x6 path
+    x = torch.randn(M, K, generator=g).to(dev)
+    ref = None
+    side = torch.cuda.Stream(device=dev)
+    for trial in range(3):
+        W = (torch.randn(N, K, generator=g) * 0.05).to(dev)
+        assert ops._emu_ok(M, N, K, K, x)
+        main = torch.cuda.current_stream(dev)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            if hasattr(torch.cuda, "_sleep"):
+                torch.cuda._sleep(2_000_000)         # keep the side stream busy: the split lags
+            y_side = ops.linear(x, W)                # builds the planes on the side stream
+        y_main = ops.linear(x, W)                    # first use on the main stream
+        main.wait_stream(side)
+        ref = (x.double() @ W.double().t())
+        for y in (y_side, y_main):
+            assert (y.double() - ref).abs().max().item() < 1e-4, trial
+        assert torch.equal(y_side, y_main)
+
+
+def test_adain_musigma_grad_with_aliased_out(dev):
+    """adain_musigma(c, s, out=c) on the autograd path (the agent's in-place
+    f_t[..., :F] = adain(f_t[..., :F], d_t[..., :F])): the saved content is private, so backward works
+    and matches the out-of-place gradient."""
+    from dasa_amd import functional as DF
+    g = torch.Generator().manual_seed(9)
+    c0 = torch.rand(6, 2176, generator=g).to(dev)
+    s0 = torch.rand(6, 2176, generator=g).to(dev)
+    w = torch.randn(6, 2176, generator=g).to(dev)
+    a = c0.clone().requires_grad_(True)
+    f = a * 1.0
+    DF.adain_musigma(f[:, :2048], s0[:, :2048], out=f[:, :2048])
+    (f * w).sum().backward()
+    b = c0.clone().requires_grad_(True)
+    y = DF.adain_musigma(b[:, :2048], s0[:, :2048])
+    ((y * w[:, :2048]).sum() + (b[:, 2048:] * w[:, 2048:]).sum()).backward()
+    assert torch.allclose(f[:, :2048], y, atol=1e-6)
+    assert (a.grad - b.grad).abs().max().item() < 1e-5
 
 
 def test_f32_to_bf16_matches_torch_rounding(dev):
