@@ -58,6 +58,7 @@ SIGNATURES = {
                            vp]),
     "dasa_softdot_fwd": (i32, [vp, vp, i64, vp, vp, vp, vp, i32, i32, i32, vp, vp]),
     "dasa_attn_workspace": (i64, [i32, i32, i32]),
+    "dasa_attn_set_mode": (i32, [i32]),
     "dasa_softdot_bwd": (i32, [vp, vp, i64, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp, vp]),
     "dasa_shift_attn_fwd": (i32, [vp, vp, i64, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp]),
     "dasa_shift_attn_bwd": (i32, [vp, vp, i64, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp, vp]),
@@ -78,7 +79,7 @@ SIGNATURES = {
     "dasa_dropout_fwd": (i32, [vp, i64, vp, i64, i32, i32, f32, u64, vp]),
     "dasa_set_seed_source": (i32, [vp]),
     "dasa_policy_head_fwd": (i32, [vp, i64, vp, vp, i32, i32, i32, i32, u64, vp, vp, vp, vp, vp, vp, vp]),
-    "dasa_policy_head_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, vp]),
+    "dasa_policy_head_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, i32, vp]),
     "dasa_seed_bump": (i32, [vp, vp]),
     "dasa_ada_gate_fwd": (i32, [vp, i64, vp, i64, vp, vp, i64, i32, i32, vp]),
     "dasa_ada_gate_bwd": (i32, [vp, i64, vp, i64, vp, i64, vp, vp, i64, i32, i32, vp]),

@@ -19,6 +19,8 @@
 //             partial dq per row block; the last arriver sums the dq partials.
 // Workspace: dasa_attn_workspace(); its first 2 x 32768 words are arrival counters that must be zero
 // on entry and are left zero.
+#include <stdlib.h>
+
 #include "common.h"
 #include "../../include/dasa_hip.h"
 
@@ -252,7 +254,13 @@ __global__ __launch_bounds__(1024) void attn_fwd_kernel(FwdArgs a) {
   if (a.wctx && t < D4) {
     const int pb = a.o_part + (b * nblk * a.D + 4 * t) * 4;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int i = 0; i < nblk; ++i) fma4(ssc[i], get4(wr, pb + i * a.D * 4), acc);
+    for (int i0 = 0; i0 < nblk; i0 += 8) {   // 8 partial loads in flight (clamped, unconditional)
+      float4 pv[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) pv[k] = get4(wr, pb + min(i0 + k, nblk - 1) * a.D * 4);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) fma4(i0 + k < nblk ? ssc[i0 + k] : 0.f, pv[k], acc);
+    }
     reinterpret_cast<float4*>(a.wctx + (long)b * a.D)[t] = acc;
   }
 }
@@ -276,7 +284,7 @@ struct BwdArgs {
 template <int RB>
 __global__ __launch_bounds__(1024) void attn_bwd_dp_kernel(BwdArgs a) {
   __shared__ float red[kMaxW][16];
-  __shared__ float sdp[kMaxN], sda[kMaxN];
+  __shared__ float sdp[kMaxN], sda[kMaxN], sp[kMaxN], swt[kMaxK + 1];
   __shared__ int s_flag;
   const int j = blockIdx.x, b = blockIdx.y, t = threadIdx.x, lane = t & 63;
   const int N = a.N, D4 = a.D >> 2, r0 = j * RB, nr = min(RB, N - r0);
@@ -287,13 +295,19 @@ __global__ __launch_bounds__(1024) void attn_bwd_dp_kernel(BwdArgs a) {
   if (t < 64 && lane < nr) pub1(wr, a.o_dp + (b * N + r0 + lane) * 4, s);
   if (!last_arriver(a.cnt1 + b, a.nblk, &s_flag)) return;
   if (t >= 64) return;
-  const float* p = a.probs + (long)b * N;
-  for (int n = lane; n < N; n += 64) sdp[n] = get1(wr, a.o_dp + (b * N + n) * 4);
+  // stage dp, the softmax and the taps in LDS (every load issued before any is used: the loops below
+  // would otherwise wait out one global round trip per element)
+  for (int n = lane; n < N; n += 64) {
+    sdp[n] = get1(wr, a.o_dp + (b * N + n) * 4);
+    sp[n] = a.probs[(long)b * N + n];
+  }
+  if (a.wsm && lane < a.K) swt[lane] = a.wsm[(long)b * a.K + lane];
   lds_wave_sync();
+  const float* p = sp;
   if (a.wsm) {
     // da[v] = sum_k w_k dp'[r][(i - k + P) mod 12] (transpose of the forward correlation);
     // dw[k] = sum_v dp'[v] a[r][(j + k - P) mod 12]; softmax backward over the K taps.
-    const float* w = a.wsm + (long)b * a.K;
+    const float* w = swt;
     const int P = a.K / 2;
     for (int v = lane; v < N; v += 64) {
       const int r = v / 12, i = v % 12;
@@ -394,12 +408,340 @@ __global__ __launch_bounds__(1024) void attn_bwd_apply_kernel(BwdArgs a) {
   if (t < D4) {
     const int pb = a.o_part + (b * nblk * a.D + 4 * t) * 4;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int i = 0; i < nblk; ++i) {
-      const float4 p = get4(wr, pb + i * a.D * 4);
-      acc.x += p.x; acc.y += p.y; acc.z += p.z; acc.w += p.w;
+    for (int i0 = 0; i0 < nblk; i0 += 8) {   // 8 partial loads in flight (clamped, unconditional)
+      float4 pv[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) pv[k] = get4(wr, pb + min(i0 + k, nblk - 1) * a.D * 4);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) fma4(i0 + k < nblk ? 1.f : 0.f, pv[k], acc);
     }
     reinterpret_cast<float4*>(a.dq + (long)b * a.D)[t] = acc;
   }
+}
+
+// ---- D-split forms (small batches: the decision step at B = 20) -----------------------------------
+// The row-split kernels above give a batch row ceil(N / RB) workgroups (60 / 100 / 20 at B = 20 for
+// the panorama / instruction / candidates), each streaming up to 12-16 rows x 8.7 KB through one CU:
+// per-CU bandwidth and the merge tail bound them, not HBM. Here a batch row gets G = D / 128
+// workgroups instead (17 for D = 2176, 16 for 2048: 340 / 320 / 340 at B = 20), each owning a 128-float
+// column chunk of ALL N rows (N <= 80): thread (row lane rl = t / 32, column t % 32) holds rows
+// rl, rl + 8, ... of its float4 column in registers for both passes.
+//   forward   partial row dots over the chunk -> published write-through; the G workgroups of the batch
+//             row meet at a group barrier (bounded spin on an agent-scope counter); every workgroup then
+//             sums the G partials in the same order (identical scores everywhere), forms the softmax (and
+//             the K-tap shift) and writes ITS chunk of the weighted context from the rows in registers. No
+//             merge pass: each output column is produced once. Scores-only calls (the candidate logits)
+//             need no barrier: the last workgroup to arrive sums the partials.
+//   backward  one launch (the row-split form takes two): partial dp = ctx . dwctx -> group barrier ->
+//             every workgroup forms ds / the shift backward for the N rows, then writes its chunk of dctx
+//             and of dq directly (no dq partial merge). Without dwctx (candidate logits) no barrier.
+// Co-residency: the spin forms are used only while B x G <= kSplitMaxWG (4 small workgroups per CU);
+// workgroups are dispatched in order, so a group whose first member runs is completed by workgroups
+// that are either running or next in line. A wait that exceeds kAttnSpinTicks anyway NaN-poisons the
+// workgroup's outputs and sets bit 4 of the library error word (raised by ops.check_device_errors).
+constexpr int kCW = 32;                          // float4 columns per workgroup
+constexpr int kSplitMaxN = 80;
+constexpr long kSplitMaxWG = 1024;
+constexpr long long kAttnSpinTicks = 20000000;   // 200 ms of the 100 MHz wall clock
+constexpr unsigned kErrAttnBarrier = 4u;
+
+struct SplitArgs {
+  const float* q; const float* ctx; long ldn;
+  const uint8_t* mask;                            // fwd [B][N] or NULL
+  const float* shift_logits; int K;               // fwd, shift attention
+  float* scores; float* probs; float* shifted; float* wsm; float* wctx;   // fwd outputs (each optional)
+  const float* a_probs; const float* a_shifted; const float* a_wsm;       // bwd: saved forward values
+  const float* dwctx; const float* dscores;       // bwd inputs (either may be NULL, not both)
+  float* dq; float* dctx; int accumulate; float* dshift;                  // bwd outputs
+  int N, D, G;
+  unsigned* cnt; unsigned* bar; float* ws; int o_part;   // workspace: last-arriver / barrier counters, partials
+  unsigned* err; int force;
+};
+
+// The G workgroups of batch row b meet on a monotonic counter (one per (G, b), never reset): every
+// launch adds exactly G arrivals, so an arrival's ticket tk says which launch it belongs to and the
+// wait ends at (tk / G + 1) * G. One atomic round trip plus the poll; no departure count, and a
+// timed-out workgroup still arrives, so the counters stay consistent. False on timeout (error word).
+__device__ bool group_barrier(unsigned* cnt, int G, unsigned* err, int force, int* s_ok) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave: its write-through stores landed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned tk = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned target = (tk / (unsigned)G + 1u) * (unsigned)G;
+    int ok = force ? 0 : 1;
+    const long long t0 = wall_clock64();
+    while (ok && (int)(__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
+      __builtin_amdgcn_s_sleep(1);
+      if (wall_clock64() - t0 > kAttnSpinTicks) ok = 0;
+    }
+    if (!ok && err) __hip_atomic_fetch_or(err, kErrAttnBarrier, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *s_ok = ok;
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler-only: keep the sc1 loads below
+  return *s_ok != 0;
+}
+
+// Row dots of the thread's RPT rows with vec over its float4 column, summed over the 32 columns of the
+// half-wave: lane col == 0 ends with the chunk's partial dot of row rl + 8 i in v[i].
+template <int RPT>
+__device__ __forceinline__ void chunk_row_dots(const float4 (&x)[RPT], float4 vec, float (&v)[RPT]) {
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) v[i] = dot4(x[i], vec);
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1)
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) v[i] += __shfl_xor(v[i], o, 64);
+}
+
+// The G x N published partials of a batch row into LDS spart[g * N + n]: every load is issued before
+// the first is used (clamped, unconditional addresses: a guarded load would make the compiler wait for
+// each one in turn — a dependent round trip per partial), then the caller sums them in LDS.
+constexpr int kMaxPartPerThread = 10;   // G * N <= 32 * 80 over 256 threads
+__device__ __forceinline__ void gather_partials(__amdgpu_buffer_rsrc_t wr, int pbase, int GN, float* spart) {
+  const int t = threadIdx.x;
+  float tmp[kMaxPartPerThread];
+#pragma unroll
+  for (int k = 0; k < kMaxPartPerThread; ++k) tmp[k] = get1(wr, pbase + min(t + 256 * k, GN - 1) * 4);
+#pragma unroll
+  for (int k = 0; k < kMaxPartPerThread; ++k)
+    if (t + 256 * k < GN) spart[t + 256 * k] = tmp[k];
+  __syncthreads();
+}
+
+// Sum over the 8 row lanes of the per-thread float4 (LDS), returned on threads t < 32 (column t).
+__device__ __forceinline__ float4 rowlane_sum(float4 acc, float4 (*red4)[kCW]) {
+  const int t = threadIdx.x;
+  red4[t >> 5][t & 31] = acc;
+  __syncthreads();
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (t < kCW) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float4 p = red4[i][t];
+      s.x += p.x; s.y += p.y; s.z += p.z; s.w += p.w;
+    }
+  }
+  return s;
+}
+
+template <int RPT>
+__global__ __launch_bounds__(256) void attn_split_fwd_kernel(SplitArgs a) {
+  __shared__ float4 red4[8][kCW];
+  __shared__ float spart[256 * kMaxPartPerThread];
+  __shared__ float sc[kSplitMaxN], wv[kSplitMaxN], sw[kMaxK + 1];
+  __shared__ int s_flag;
+  const int g = blockIdx.x, b = blockIdx.y, t = threadIdx.x, lane = t & 63, col = t & 31, rl = t >> 5;
+  const int N = a.N, G = a.G, c = g * kCW + col;
+  const bool shift = a.shift_logits != nullptr;
+  const float* base = a.ctx + (long)b * N * a.ldn;
+  float4 x[RPT];
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) x[i] = reinterpret_cast<const float4*>(base + (long)min(rl + 8 * i, N - 1) * a.ldn)[c];
+  const float4 qv = reinterpret_cast<const float4*>(a.q + (long)b * a.D)[c];
+  float v[RPT];
+  chunk_row_dots<RPT>(x, qv, v);
+  const __amdgpu_buffer_rsrc_t wr = ws_rsrc(a.ws);
+  const int pbase = a.o_part + (int)((long)b * G * N) * 4;
+  if (col == 0) {
+#pragma unroll
+    for (int i = 0; i < RPT; ++i)
+      if (rl + 8 * i < N) pub1(wr, pbase + (g * N + rl + 8 * i) * 4, v[i]);
+  }
+  const bool combine = a.wctx || a.probs || a.shifted;
+  if (!combine) {   // scores only: the last workgroup of the row sums the partials
+    if (!last_arriver(a.cnt + b, G, &s_flag)) return;
+    gather_partials(wr, pbase, G * N, spart);
+    if (t < N && a.scores) {
+      float s = 0.f;
+      for (int gg = 0; gg < G; ++gg) s += spart[gg * N + t];
+      a.scores[(long)b * N + t] = s;
+    }
+    return;
+  }
+  if (!group_barrier(a.bar + b, G, a.err, a.force, &s_flag)) {
+    const float qnan = __builtin_nanf("");
+    if (t < kCW && a.wctx) reinterpret_cast<float4*>(a.wctx + (long)b * a.D)[g * kCW + t] = make_float4(qnan, qnan, qnan, qnan);
+    if (g == 0)
+      for (int n = t; n < N; n += blockDim.x) {
+        if (a.probs) a.probs[(long)b * N + n] = qnan;
+        if (a.shifted) a.shifted[(long)b * N + n] = qnan;
+      }
+    return;
+  }
+  gather_partials(wr, pbase, G * N, spart);
+  if (t < N) {   // identical sums (same order) in every workgroup of the row
+    float s = 0.f;
+    for (int gg = 0; gg < G; ++gg) s += spart[gg * N + t];
+    sc[t] = s;
+    if (g == 0 && a.scores) a.scores[(long)b * N + t] = s;
+  }
+  __syncthreads();
+  if (t < 64) {
+    float s0 = -INFINITY, s1 = -INFINITY;
+    if (lane < N) s0 = (a.mask && a.mask[(long)b * N + lane]) ? -INFINITY : sc[lane];
+    if (lane + 64 < N) s1 = (a.mask && a.mask[(long)b * N + lane + 64]) ? -INFINITY : sc[lane + 64];
+    const float m = wave_max(fmaxf(s0, s1));
+    const float e0 = s0 == -INFINITY ? 0.f : __expf(s0 - m), e1 = s1 == -INFINITY ? 0.f : __expf(s1 - m);
+    const float inv = 1.f / wave_sum(e0 + e1);
+    const float p0 = e0 * inv, p1 = e1 * inv;
+    if (shift) shift_taps(a.shift_logits + (long)b * a.K, a.K, sw, lane);
+    lds_wave_sync();
+    if (lane < N) sc[lane] = p0;            // sc: the softmax now
+    if (lane + 64 < N) sc[lane + 64] = p1;
+    lds_wave_sync();
+    float w0 = p0, w1 = p1;
+    if (shift && lane < N) {   // N = 36: three elevation rings of 12 headings (model.py:337-344)
+      const int P = a.K / 2, r = lane / 12, j = lane % 12;
+      w0 = 0.f;
+      for (int k = 0; k < a.K; ++k) {
+        int jj = j + k - P;
+        jj = ((jj % 12) + 12) % 12;
+        w0 = fmaf(sw[k], sc[r * 12 + jj], w0);
+      }
+    }
+    if (lane < N) wv[lane] = w0;
+    if (lane + 64 < N) wv[lane + 64] = w1;
+    if (g == 0) {
+      if (lane < N) {
+        if (a.probs) a.probs[(long)b * N + lane] = p0;
+        if (a.shifted) a.shifted[(long)b * N + lane] = w0;
+      }
+      if (lane + 64 < N) {
+        if (a.probs) a.probs[(long)b * N + lane + 64] = p1;
+        if (a.shifted) a.shifted[(long)b * N + lane + 64] = w1;
+      }
+      if (shift && a.wsm && lane < a.K) a.wsm[(long)b * a.K + lane] = sw[lane];
+    }
+  }
+  __syncthreads();
+  if (!a.wctx) return;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const int r = rl + 8 * i;
+    fma4(r < N ? wv[r] : 0.f, x[i], acc);
+  }
+  const float4 o = rowlane_sum(acc, red4);
+  if (t < kCW) reinterpret_cast<float4*>(a.wctx + (long)b * a.D)[g * kCW + t] = o;
+}
+
+template <int RPT>
+__global__ __launch_bounds__(256) void attn_split_bwd_kernel(SplitArgs a) {
+  __shared__ float4 red4[8][kCW];
+  __shared__ float spart[256 * kMaxPartPerThread];
+  __shared__ float sdp[kSplitMaxN], sds[kSplitMaxN], spw[kSplitMaxN], sp[kSplitMaxN], swk[kMaxK + 1];
+  __shared__ int s_flag;
+  const int g = blockIdx.x, b = blockIdx.y, t = threadIdx.x, lane = t & 63, col = t & 31, rl = t >> 5;
+  const int N = a.N, G = a.G, c = g * kCW + col;
+  const float* base = a.ctx + (long)b * N * a.ldn;
+  float4 x[RPT];
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) x[i] = reinterpret_cast<const float4*>(base + (long)min(rl + 8 * i, N - 1) * a.ldn)[c];
+  const float4 qv = reinterpret_cast<const float4*>(a.q + (long)b * a.D)[c];
+  const bool gdw = a.dwctx != nullptr;
+  const float4 gv = gdw ? reinterpret_cast<const float4*>(a.dwctx + (long)b * a.D)[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+  if (gdw) {
+    float v[RPT];
+    chunk_row_dots<RPT>(x, gv, v);
+    const __amdgpu_buffer_rsrc_t wr = ws_rsrc(a.ws);
+    const int pbase = a.o_part + (int)((long)b * G * N) * 4;
+    if (col == 0) {
+#pragma unroll
+      for (int i = 0; i < RPT; ++i)
+        if (rl + 8 * i < N) pub1(wr, pbase + (g * N + rl + 8 * i) * 4, v[i]);
+    }
+    if (!group_barrier(a.bar + b, G, a.err, a.force, &s_flag)) {
+      const float qnan = __builtin_nanf("");
+      const float4 q4 = make_float4(qnan, qnan, qnan, qnan);
+      if (t < kCW && a.dq) reinterpret_cast<float4*>(a.dq + (long)b * a.D)[g * kCW + t] = q4;
+      if (a.dctx)
+#pragma unroll
+        for (int i = 0; i < RPT; ++i)
+          if (rl + 8 * i < N) reinterpret_cast<float4*>(a.dctx + ((long)b * N + rl + 8 * i) * a.ldn)[c] = q4;
+      return;
+    }
+    gather_partials(wr, pbase, G * N, spart);
+    if (t < N) {
+      float s = 0.f;
+      for (int gg = 0; gg < G; ++gg) s += spart[gg * N + t];
+      sdp[t] = s;
+      sp[t] = a.a_probs[(long)b * N + t];
+      if (a.a_shifted) spw[t] = a.a_shifted[(long)b * N + t];
+    }
+    if (a.a_wsm && t < a.K) swk[t] = a.a_wsm[(long)b * a.K + t];
+    __syncthreads();
+    if (t < 64) {
+      const float* p = sp;
+      float da0 = 0.f, da1 = 0.f;
+      if (a.a_wsm) {   // shift backward (transpose of the forward correlation; softmax over the taps)
+        const float* w = swk;
+        const int P = a.K / 2;
+        if (lane < N) {
+          const int r = lane / 12, i = lane % 12;
+          for (int k = 0; k < a.K; ++k) {
+            int jj = i - k + P;
+            jj = ((jj % 12) + 12) % 12;
+            da0 = fmaf(w[k], sdp[r * 12 + jj], da0);
+          }
+        }
+        float dwk = 0.f;
+        if (lane < a.K) {
+          for (int vv = 0; vv < N; ++vv) {
+            const int r = vv / 12, jx = vv % 12;
+            int jj = jx + lane - P;
+            jj = ((jj % 12) + 12) % 12;
+            dwk = fmaf(sdp[vv], p[r * 12 + jj], dwk);
+          }
+        }
+        const float wk = lane < a.K ? w[lane] : 0.f;
+        const float dot = wave_sum(wk * dwk);
+        if (g == 0 && lane < a.K && a.dshift) a.dshift[(long)b * a.K + lane] = wk * (dwk - dot);
+      } else {
+        if (lane < N) { da0 = sdp[lane]; spw[lane] = p[lane]; }
+        if (lane + 64 < N) { da1 = sdp[lane + 64]; spw[lane + 64] = p[lane + 64]; }
+      }
+      const float p0 = lane < N ? p[lane] : 0.f, p1 = lane + 64 < N ? p[lane + 64] : 0.f;
+      const float dot = wave_sum(p0 * da0 + p1 * da1);
+      if (lane < N) sds[lane] = p0 * (da0 - dot) + (a.dscores ? a.dscores[(long)b * N + lane] : 0.f);
+      if (lane + 64 < N) sds[lane + 64] = p1 * (da1 - dot) + (a.dscores ? a.dscores[(long)b * N + lane + 64] : 0.f);
+    }
+  } else {
+    if (t < N) {
+      sds[t] = a.dscores[(long)b * N + t];
+      spw[t] = 0.f;
+    }
+  }
+  __syncthreads();
+  if (a.dctx) {
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int r = rl + 8 * i;
+      if (r < N) {
+        float4* d4 = reinterpret_cast<float4*>(a.dctx + ((long)b * N + r) * a.ldn) + c;
+        const float pw = spw[r], ds = sds[r];
+        float4 o;
+        o.x = fmaf(pw, gv.x, ds * qv.x);
+        o.y = fmaf(pw, gv.y, ds * qv.y);
+        o.z = fmaf(pw, gv.z, ds * qv.z);
+        o.w = fmaf(pw, gv.w, ds * qv.w);
+        if (a.accumulate) {
+          const float4 old = *d4;
+          o.x += old.x; o.y += old.y; o.z += old.z; o.w += old.w;
+        }
+        *d4 = o;
+      }
+    }
+  }
+  if (!a.dq) return;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const int r = rl + 8 * i;
+    fma4(r < N ? sds[r] : 0.f, x[i], acc);
+  }
+  const float4 o = rowlane_sum(acc, red4);
+  if (t < kCW) reinterpret_cast<float4*>(a.dq + (long)b * a.D)[g * kCW + t] = o;
 }
 
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
@@ -413,11 +755,13 @@ inline int block_threads(int D) {
 inline int rows_per_block(int N, bool shift) { return shift ? 12 : 16; }
 
 // Workspace layout (32-bit words): [cnt1 kMaxB][cnt2 kMaxB] at fixed offsets (so the zero-on-entry
-// counters never overlap another call's data, whatever its shape), then [dp B*N][ds B*N][pw B*N]
-// [ml B*nblk*2][ee B*N*2][part B*nblk*D], the partial blocks 16-B aligned.
+// counters never overlap another call's data, whatever its shape), the D-split group-barrier counters
+// [kBarSlots][kSplitMaxWG] (monotonic, slot = G), then [dp B*N][ds B*N][pw B*N][ml B*nblk*2]
+// [ee B*N*2][part B*nblk*D], the partial blocks 16-B aligned.
 constexpr long kMaxB = 32768;
+constexpr long kBarSlots = 33;   // G = D / 128 <= 32
 struct WsLayout {
-  unsigned* cnt1; unsigned* cnt2; float* ds; float* pw;
+  unsigned* cnt1; unsigned* cnt2; unsigned* bar; float* ds; float* pw;
   int o_dp, o_ml, o_ee, o_part;   // byte offsets from the workspace base
   int64_t bytes;
 };
@@ -426,11 +770,12 @@ inline WsLayout ws_layout(void* ws, int B, int N, int D) {
   const long nblk = (N + 11) / 12;   // the larger block count of the two row splits
   long off = 0;
   auto take = [&](long n) { long o = off; off += (n + 3) & ~3L; return o; };
-  const long o1 = take(kMaxB), o2 = take(kMaxB), o3 = take((long)B * N), o4 = take((long)B * N), o5 = take((long)B * N),
-             o6 = take((long)B * nblk * 2), o7 = take((long)B * N * 2), o8 = take((long)B * nblk * D);
+  const long o1 = take(kMaxB), o2 = take(kMaxB), ob = take(kBarSlots * kSplitMaxWG), o3 = take((long)B * N),
+             o4 = take((long)B * N), o5 = take((long)B * N), o6 = take((long)B * nblk * 2), o7 = take((long)B * N * 2),
+             o8 = take((long)B * nblk * D);
   float* f = (float*)ws;
-  WsLayout L{(unsigned*)(f + o1), (unsigned*)(f + o2), f + o4, f + o5, (int)(o3 * 4), (int)(o6 * 4), (int)(o7 * 4),
-             (int)(o8 * 4), (int64_t)off * 4};
+  WsLayout L{(unsigned*)(f + o1), (unsigned*)(f + o2), (unsigned*)(f + ob), f + o4, f + o5, (int)(o3 * 4),
+             (int)(o6 * 4), (int)(o7 * 4), (int)(o8 * 4), (int64_t)off * 4};
   return L;
 }
 
@@ -460,12 +805,53 @@ int launch_bwd(BwdArgs a, int B, void* ws, hipStream_t st) {
   return 0;
 }
 
+// D-split eligibility (0 = use the row-split kernels): rows per thread for N <= 80, D a multiple of 128,
+// and B x G within kSplitMaxWG when the call needs the group barrier. DASA_ATTN_SPLIT=0 disables it.
+int g_attn_mode = -1;   // dasa_attn_set_mode: 0 automatic, 1 row-split only; -1 = not read from the env yet
+
+int split_rpt(int B, int N, int D, bool spin) {
+  if (g_attn_mode < 0) {
+    const char* e = getenv("DASA_ATTN_SPLIT");
+    g_attn_mode = (e && e[0] == '0') ? 1 : 0;
+  }
+  if (g_attn_mode == 1 || N < 1 || N > kSplitMaxN || D % (4 * kCW) != 0) return 0;
+  if (spin && (long)B * (D / (4 * kCW)) > kSplitMaxWG) return 0;
+  return N <= 16 ? 2 : (N <= 40 ? 5 : 10);
+}
+
+template <int RPT, bool FWD>
+void split_launch(const SplitArgs& a, int B, hipStream_t st) {
+  if (FWD) hipLaunchKernelGGL(attn_split_fwd_kernel<RPT>, dim3(a.G, B), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(attn_split_bwd_kernel<RPT>, dim3(a.G, B), dim3(256), 0, st, a);
+}
+
+template <bool FWD>
+int launch_split(SplitArgs a, int rpt, int B, void* ws, hipStream_t st) {
+  WsLayout L = ws_layout(ws, B, a.N, a.D);
+  a.G = a.D / (4 * kCW);
+  a.cnt = L.cnt1; a.bar = L.bar + (long)a.G * kSplitMaxWG; a.ws = (float*)ws; a.o_part = L.o_part;
+  a.err = dasa_err_word_host(); a.force = dasa_force_timeout_host();
+  switch (rpt) {
+    case 2: split_launch<2, FWD>(a, B, st); break;
+    case 5: split_launch<5, FWD>(a, B, st); break;
+    default: split_launch<10, FWD>(a, B, st); break;
+  }
+  DASA_CHECK_LAUNCH();
+  return 0;
+}
+
 bool bad_common(const float* q, const float* ctx, int64_t ldn, int B, int N, int D, const void* ws) {
   return N > kMaxN || D > 4096 || B > kMaxB || ws_layout(nullptr, B, N, D).bytes >= (1L << 31) || (D & 3) || (ldn & 3) || ldn < D || !aligned16(q) || !aligned16(ctx) || !ws ||
          !aligned16(ws);
 }
 
 }  // namespace
+
+extern "C" int dasa_attn_set_mode(int32_t mode) {
+  if (mode != 0 && mode != 1) return (int)hipErrorInvalidValue;
+  g_attn_mode = mode;
+  return 0;
+}
 
 extern "C" int64_t dasa_attn_workspace(int32_t B, int32_t N, int32_t D) {
   if (B <= 0 || N <= 0 || D <= 0) return 16;
@@ -477,6 +863,13 @@ extern "C" int dasa_softdot_fwd(const float* q, const float* ctx, int64_t ldn, c
                                 int32_t B, int32_t N, int32_t D, float* ws, void* stream) {
   if (B <= 0 || N <= 0) return 0;
   if (bad_common(q, ctx, ldn, B, N, D, ws) || (wctx && !aligned16(wctx))) return (int)hipErrorInvalidValue;
+  const int rpt = split_rpt(B, N, D, probs || wctx);
+  if (rpt) {
+    SplitArgs sa{};
+    sa.q = q; sa.ctx = ctx; sa.ldn = ldn; sa.mask = mask; sa.scores = scores; sa.probs = probs; sa.wctx = wctx;
+    sa.N = N; sa.D = D;
+    return launch_split<true>(sa, rpt, B, ws, (hipStream_t)stream);
+  }
   FwdArgs a{q, ctx, (long)ldn, mask, nullptr, 0, scores, probs, nullptr, nullptr, wctx, N, D};
   return launch_fwd<16>(a, B, ws, (hipStream_t)stream);
 }
@@ -489,6 +882,13 @@ extern "C" int dasa_softdot_bwd(const float* q, const float* ctx, int64_t ldn, c
   if (bad_common(q, ctx, ldn, B, N, D, ws) || !probs || (!dwctx && !dscores) || (dwctx && !aligned16(dwctx)) ||
       (dq && !aligned16(dq)) || (dctx && !aligned16(dctx)))
     return (int)hipErrorInvalidValue;
+  const int rpt = split_rpt(B, N, D, dwctx != nullptr);
+  if (rpt) {
+    SplitArgs sa{};
+    sa.q = q; sa.ctx = ctx; sa.ldn = ldn; sa.a_probs = probs; sa.dwctx = dwctx; sa.dscores = dscores;
+    sa.dq = dq; sa.dctx = dctx; sa.accumulate = accumulate; sa.N = N; sa.D = D;
+    return launch_split<false>(sa, rpt, B, ws, (hipStream_t)stream);
+  }
   BwdArgs a{q, ctx, (long)ldn, probs, nullptr, nullptr, 0, dwctx, dscores, dq, dctx, accumulate, nullptr, N, D};
   return launch_bwd<16>(a, B, ws, (hipStream_t)stream);
 }
@@ -500,6 +900,13 @@ extern "C" int dasa_shift_attn_fwd(const float* q, const float* ctx, int64_t ldn
   if (B <= 0) return 0;
   if (K < 1 || K > kMaxK || bad_common(q, ctx, ldn, B, N, D, ws) || !shift_logits || !wctx || !aligned16(wctx))
     return (int)hipErrorInvalidValue;
+  const int rpt = split_rpt(B, N, D, true);
+  if (rpt) {
+    SplitArgs sa{};
+    sa.q = q; sa.ctx = ctx; sa.ldn = ldn; sa.shift_logits = shift_logits; sa.K = K; sa.probs = attn;
+    sa.shifted = shifted; sa.wsm = wsm; sa.wctx = wctx; sa.N = N; sa.D = D;
+    return launch_split<true>(sa, rpt, B, ws, (hipStream_t)stream);
+  }
   FwdArgs a{q, ctx, (long)ldn, nullptr, shift_logits, K, nullptr, attn, shifted, wsm, wctx, N, D};
   return launch_fwd<12>(a, B, ws, (hipStream_t)stream);
 }
@@ -513,6 +920,14 @@ extern "C" int dasa_shift_attn_bwd(const float* q, const float* ctx, int64_t ldn
   if (K < 1 || K > kMaxK || bad_common(q, ctx, ldn, B, N, D, ws) || !attn || !shifted || !wsm || !dwctx ||
       !dshift_logits || !aligned16(dwctx) || (dq && !aligned16(dq)) || (dctx && !aligned16(dctx)))
     return (int)hipErrorInvalidValue;
+  const int rpt = split_rpt(B, N, D, true);
+  if (rpt) {
+    SplitArgs sa{};
+    sa.q = q; sa.ctx = ctx; sa.ldn = ldn; sa.K = K; sa.a_probs = attn; sa.a_shifted = shifted; sa.a_wsm = wsm;
+    sa.dwctx = dwctx; sa.dq = dq; sa.dctx = dctx; sa.accumulate = accumulate; sa.dshift = dshift_logits;
+    sa.N = N; sa.D = D;
+    return launch_split<false>(sa, rpt, B, ws, (hipStream_t)stream);
+  }
   BwdArgs a{q, ctx, (long)ldn, attn, shifted, wsm, K, dwctx, nullptr, dq, dctx, accumulate,
             dshift_logits, N, D};
   return launch_bwd<12>(a, B, ws, (hipStream_t)stream);

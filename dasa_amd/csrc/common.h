@@ -68,6 +68,10 @@ __device__ __forceinline__ uint64_t eff_seed(uint64_t seed, const uint64_t* src)
 }
 // Host side: the seed source recorded into dropout launches (nullptr = plain host seeds).
 __attribute__((visibility("hidden"))) const uint64_t* dasa_seed_src_host();
+// Host side: the library's device error word (dasa_set_error_word; bits: 1 bi-LSTM forward, 2 bi-LSTM
+// BPTT, 4 attention group barrier) and the forced-timeout test hook (dasa_persist_force_timeout).
+__attribute__((visibility("hidden"))) unsigned* dasa_err_word_host();
+__attribute__((visibility("hidden"))) int dasa_force_timeout_host();
 
 __device__ __forceinline__ float dasa_dropout_scale(float p, uint64_t seed, uint64_t idx) {
   if (p <= 0.f) return 1.f;

@@ -1084,7 +1084,9 @@ struct X6Split { unsigned* cnt; float* slab; int splitk, kchunk; };
 
 // (at most 2 waves per SIMD fit the LDS of the 128-row forms anyway: telling the register allocator so
 // lets it use 256 VGPRs instead of spilling to reach an occupancy the LDS forbids)
-template <int BM, int BN, int WAVES_M, int WAVES_N, bool SEP, int PF = 1, bool SPL = false>
+// PRIO (A/B forms 10-13): 1 = s_setprio(1) around every MFMA cluster (cdna_hip_programming.md T5),
+// 2 = one static s_setprio(1) for the second half of the workgroup's waves (T5 static form).
+template <int BM, int BN, int WAVES_M, int WAVES_N, bool SEP, int PF = 1, bool SPL = false, int PRIO = 0>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) __attribute__((amdgpu_waves_per_eu(1, 2)))
 void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
   constexpr int NT = 64 * WAVES_M * WAVES_N;
@@ -1096,6 +1098,7 @@ void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
   __shared__ uint4 smem[2 * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (PRIO == 2 && __builtin_amdgcn_readfirstlane(tid) >= NT / 2) __builtin_amdgcn_s_setprio(1);
   const int wm = (wave / WAVES_N) * WM, wn = (wave % WAVES_N) * WN;
   const int wgid = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
   int m0, n0;
@@ -1176,6 +1179,7 @@ void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
 
   auto compute = [&](const uint4* S) {
     const int q = lane >> 4;
+    if (PRIO == 1) __builtin_amdgcn_s_setprio(1);
     bf16x8_t bf[3][TN];
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl)
@@ -1199,6 +1203,7 @@ void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
         big[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[0][j], big[i][j], 0, 0, 0);
       }
     }
+    if (PRIO == 1) __builtin_amdgcn_s_setprio(0);
   };
 
   const int nk = (SPL ? min(xs.kchunk, p.K - kb) : p.K) / 32;
@@ -2017,7 +2022,8 @@ static X6Plan x6_plan(const dasa_gemm_desc* d) {
     pl.cfg = (g_force_cfg - kX6Force) % 16;
     fsplit = ((g_force_cfg - kX6Force) / 16) % 64;
   }
-  pl.bm = (pl.cfg == 1 || pl.cfg == 3 || pl.cfg == 6 || pl.cfg == 7) ? 256 : (pl.cfg == 4 || pl.cfg == 5) ? 64 : 128;
+  pl.bm = (pl.cfg == 1 || pl.cfg == 3 || pl.cfg == 6 || pl.cfg == 7 || pl.cfg == 12 || pl.cfg == 13) ? 256
+          : (pl.cfg == 4 || pl.cfg == 5) ? 64 : 128;
   pl.bn = pl.cfg == 5 ? 64 : 128;
   const long tiles = (long)cdiv(M, pl.bm) * cdiv(N, pl.bn) * batch;
   // split count (profiles/r02/gemm_x6_splitk.txt): the most splits that keep tiles x splits <= 256
@@ -2093,6 +2099,10 @@ extern "C" int dasa_gemm_f32x6_ws(const dasa_gemm_desc* d, int64_t plane, void* 
     case 6: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<256, 128, 4, 2, false, 2>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
     case 7: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<256, 128, 4, 2, true, 2>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
     case 8: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true, 2>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
+    case 10: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true, 2, false, 1>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
+    case 11: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true, 2, false, 2>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
+    case 12: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<256, 128, 4, 2, true, 2, false, 1>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
+    case 13: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<256, 128, 4, 2, true, 2, false, 2>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
     case 9: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true, 3>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
     default: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
   }

@@ -394,6 +394,9 @@ extern "C" int dasa_persist_force_timeout(int32_t on) {
   g_force_tmo = on ? 1 : 0;
   return 0;
 }
+// shared with the other kernels that wait on a bounded inter-workgroup barrier (attn.hip)
+unsigned* dasa_err_word_host() { return g_err_word; }
+int dasa_force_timeout_host() { return g_force_tmo; }
 
 // Residency check done once per kernel: the grid (one 1024-thread workgroup per CU) must fit the
 // device in one wave of workgroups. Launched as plain kernels: a cooperative launch adds only this

@@ -9,12 +9,22 @@
 // one workgroup; the CE row terms are summed in row order by wave 0 at the end (deterministic).
 // Sampling is inverse-CDF on the counter RNG (dasa_uniform(seed, row)): the same distribution as
 // torch.multinomial, another random stream.
+// The sampled rollout's entropy and log-probability follow torch.distributions.Categorical(probs)
+// exactly (agent_dg.py:874-880): its log-pmf is log(clamp(p, eps, 1 - eps)) with eps = FLT_EPSILON
+// (probs_to_logits), so log_prob(a) and entropy = -sum p * log(clamp(p)) use the clamped logs and their
+// gradients vanish where the clamp is active; argmax mode keeps the exact log_softmax
+// (F.log_softmax(logit).gather, agent_dg.py:866-869).
 #include "common.h"
 #include "../../include/dasa_hip.h"
 
 namespace {
 
 constexpr int kVpl = 4;   // candidates per lane (C <= 256)
+constexpr float kPEps = 1.1920928955078125e-07f;   // torch.finfo(float32).eps (clamp_probs)
+
+__device__ __forceinline__ float clamped_log(float p) {   // log(clamp(p, eps, 1 - eps))
+  return __logf(fminf(fmaxf(p, kPEps), 1.f - kPEps));
+}
 
 struct PolicyFwd {
   const float* logit; long ld;
@@ -48,12 +58,14 @@ __global__ __launch_bounds__(1024) void policy_head_fwd_kernel(PolicyFwd a) {
     for (int k = 0; k < kVpl; ++k) s += (z[k] == -INFINITY) ? 0.f : __expf(z[k] - m);
     s = wave_sum(s);
     const float lse = m + __logf(s);
-    float lp[kVpl], h = 0.f;
+    const bool cat = a.mode == DASA_POLICY_SAMPLE || a.mode == DASA_POLICY_FORCED;   // Categorical semantics
+    float lp[kVpl], lc[kVpl], h = 0.f;
 #pragma unroll
     for (int k = 0; k < kVpl; ++k) {
       const int c = lane + 64 * k;
       lp[k] = z[k] == -INFINITY ? -INFINITY : z[k] - lse;
-      if (z[k] != -INFINITY) h -= __expf(lp[k]) * lp[k];
+      lc[k] = (cat && z[k] != -INFINITY) ? clamped_log(__expf(lp[k])) : lp[k];
+      if (z[k] != -INFINITY) h -= __expf(lp[k]) * lc[k];
       if (c < a.C) a.logp[(long)b * a.C + c] = lp[k];
     }
     h = wave_sum(h);
@@ -123,7 +135,7 @@ __global__ __launch_bounds__(1024) void policy_head_fwd_kernel(PolicyFwd a) {
     if (a.logp_a && act >= 0) {
 #pragma unroll
       for (int k = 0; k < kVpl; ++k)
-        if (lane + 64 * k == act) a.logp_a[b] = lp[k];
+        if (lane + 64 * k == act) a.logp_a[b] = lc[k];
     }
   }
   __syncthreads();
@@ -135,34 +147,65 @@ __global__ __launch_bounds__(1024) void policy_head_fwd_kernel(PolicyFwd a) {
 }
 
 struct PolicyBwd {
-  const float* logp;        // [B][C] saved
+  const float* logp;        // [B][C] saved (exact log-softmax, -inf where masked)
   const int32_t* len;
   const int64_t* target;    // or NULL
   const int64_t* action;    // or NULL
-  const float* ent;         // [B] saved entropy (needed with d_ent)
+  const float* ent;         // [B] saved entropy (unused: the row sums are recomputed)
   const float* d_ce;        // [1] or NULL
   const float* d_logp_a;    // [B] or NULL
   const float* d_ent;       // [B] or NULL
   float* dlogit; long ldd;
-  int B, C, ignore;
+  int B, C, ignore, mode;
 };
 
-__global__ __launch_bounds__(256) void policy_head_bwd_kernel(PolicyBwd a) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (long)a.B * a.C) return;
-  const int b = (int)(idx / a.C), c = (int)(idx % a.C);
-  float g = 0.f;
-  if (c < a.len[b]) {
-    const float lp = a.logp[idx];
-    const float p = __expf(lp);
-    if (a.d_ce && a.target) {
-      const long t = a.target[b];
-      if (t != a.ignore) g += a.d_ce[0] * (p - (c == t ? 1.f : 0.f));
+// One wave per row. With Categorical semantics (sample / forced): l_c = log(clamp(p_c)), u_c = 1 where
+// the clamp is inactive; d log_prob(a) / dz_j = u_a (onehot_a - p_j); dH / dz_j = p_j (g_j - sum_c p_c g_c)
+// with g_c = dH / dp_c = -(l_c + u_c). Argmax / teacher: u = 1 and l = log p (the exact log-softmax).
+__global__ __launch_bounds__(1024) void policy_head_bwd_kernel(PolicyBwd a) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const bool cat = a.mode == DASA_POLICY_SAMPLE || a.mode == DASA_POLICY_FORCED;
+  for (int b = blockIdx.x * nw + w; b < a.B; b += gridDim.x * nw) {
+    const int L = a.len[b];
+    float p[kVpl], gh[kVpl];
+    float S = 0.f;
+#pragma unroll
+    for (int k = 0; k < kVpl; ++k) {
+      const int c = lane + 64 * k;
+      const bool v = c < a.C && c < L;
+      p[k] = v ? __expf(a.logp[(long)b * a.C + c]) : 0.f;
+      float l = 0.f, u = 1.f;
+      if (v) {
+        l = cat ? clamped_log(p[k]) : a.logp[(long)b * a.C + c];
+        u = (!cat || (p[k] > kPEps && p[k] < 1.f - kPEps)) ? 1.f : 0.f;
+      }
+      gh[k] = -(l + u);
+      S += p[k] * gh[k];
     }
-    if (a.d_logp_a && a.action) g += a.d_logp_a[b] * ((c == a.action[b] ? 1.f : 0.f) - p);
-    if (a.d_ent) g += a.d_ent[b] * (p > 0.f ? -p * (lp + a.ent[b]) : 0.f);
+    if (a.d_ent) S = wave_sum(S);
+    const long t = (a.d_ce && a.target) ? a.target[b] : (long)a.ignore;
+    const long act = (a.d_logp_a && a.action) ? a.action[b] : -1;
+    float pa = 0.f;
+    if (act >= 0 && cat) {
+#pragma unroll
+      for (int k = 0; k < kVpl; ++k)
+        if (lane + 64 * k == act) pa = p[k];
+      pa = wave_max(pa);
+    }
+    const float ua = (!cat || (pa > kPEps && pa < 1.f - kPEps)) ? 1.f : 0.f;
+#pragma unroll
+    for (int k = 0; k < kVpl; ++k) {
+      const int c = lane + 64 * k;
+      if (c >= a.C) continue;
+      float g = 0.f;
+      if (c < L) {
+        if (t != a.ignore) g += a.d_ce[0] * (p[k] - (c == t ? 1.f : 0.f));
+        if (act >= 0) g += a.d_logp_a[b] * ua * ((c == act ? 1.f : 0.f) - p[k]);
+        if (a.d_ent) g += a.d_ent[b] * p[k] * (gh[k] - S);
+      }
+      a.dlogit[(long)b * a.ldd + c] = g;
+    }
   }
-  a.dlogit[(long)b * a.ldd + c] = g;
 }
 
 }  // namespace
@@ -189,12 +232,16 @@ extern "C" int dasa_policy_head_fwd(const float* logit, int64_t ld, const int32_
 extern "C" int dasa_policy_head_bwd(const float* logp, const int32_t* cand_len, const int64_t* target,
                                     const int64_t* action, const float* ent, const float* d_ce,
                                     const float* d_logp_a, const float* d_ent, float* dlogit, int64_t ldd,
-                                    int32_t B, int32_t C, int32_t ignore_index, void* stream) {
+                                    int32_t B, int32_t C, int32_t mode, int32_t ignore_index, void* stream) {
   if (B <= 0 || C <= 0) return 0;
-  if (ldd < C || !logp || !cand_len || !dlogit || (d_ent && !ent)) return (int)hipErrorInvalidValue;
-  PolicyBwd a{logp, cand_len, target, action, ent, d_ce, d_logp_a, d_ent, dlogit, (long)ldd, B, C, ignore_index};
-  const long n = (long)B * C;
-  hipLaunchKernelGGL(policy_head_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a);
+  if (C > 64 * kVpl || ldd < C || !logp || !cand_len || !dlogit || (d_ent && !ent)) return (int)hipErrorInvalidValue;
+  if (mode < DASA_POLICY_TEACHER || mode > DASA_POLICY_FORCED) return (int)hipErrorInvalidValue;
+  PolicyBwd a{logp, cand_len, target, action, ent, d_ce, d_logp_a, d_ent, dlogit, (long)ldd, B, C, ignore_index,
+              mode};
+  const int waves = B < 16 ? B : 16;
+  const int blocks = (B + waves - 1) / waves;
+  hipLaunchKernelGGL(policy_head_bwd_kernel, dim3(blocks < 1024 ? blocks : 1024), dim3(64 * waves), 0,
+                     (hipStream_t)stream, a);
   DASA_CHECK_LAUNCH();
   return 0;
 }

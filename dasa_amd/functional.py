@@ -406,14 +406,15 @@ class CandLogitFn(torch.autograd.Function):
 class PolicyHeadFn(torch.autograd.Function):
     """agent_dg.py:832-880 in one kernel: logit.masked_fill(cand_mask, -inf) -> CrossEntropyLoss(sum,
     ignore_index) against the teacher target, and the action (argmax, or a Categorical draw) with its
-    entropy and log-probability. Returns (ce_sum, entropy [B], logp_action [B], action [B] int64)."""
+    entropy and log-probability (Categorical(probs)'s clamped log-pmf in sample / forced mode, the
+    exact log_softmax in argmax mode). Returns (ce_sum, entropy [B], logp_action [B], action [B] int64)."""
 
     @staticmethod
     def forward(ctx, logit, cand_len_i32, target, mode, seed, ignore_index, forced=None):
         ce, ent, lpa, action, logp = ops.policy_head_fwd(logit, cand_len_i32, target, mode, seed, ignore_index,
                                                          forced)
         ctx.save_for_backward(logp, cand_len_i32, target, action, ent)
-        ctx.ignore = ignore_index
+        ctx.ignore, ctx.mode = ignore_index, mode
         if action is None:   # teacher mode: no action drawn
             action = torch.empty(0, dtype=torch.int64, device=logit.device)
         ctx.mark_non_differentiable(action)
@@ -427,7 +428,7 @@ class PolicyHeadFn(torch.autograd.Function):
         dlogit = ops.policy_head_bwd(logp, lens, target, action, ent,
                                      d_ce.reshape(1).contiguous() if d_ce is not None else None,
                                      d_lpa.contiguous() if d_lpa is not None else None,
-                                     d_ent.contiguous() if d_ent is not None else None, ctx.ignore)
+                                     d_ent.contiguous() if d_ent is not None else None, ctx.mode, ctx.ignore)
         return dlogit, None, None, None, None, None, None
 
 

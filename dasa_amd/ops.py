@@ -552,12 +552,12 @@ def policy_head_fwd(logit, cand_len_i32, target, mode, seed, ignore_index=-100, 
     return ce, ent, logp_a, action, logp
 
 
-def policy_head_bwd(logp, cand_len_i32, target, action, ent, d_ce, d_logp_a, d_ent, ignore_index=-100):
+def policy_head_bwd(logp, cand_len_i32, target, action, ent, d_ce, d_logp_a, d_ent, mode, ignore_index=-100):
     B, C = logp.shape
     dlogit = torch.empty(B, C, dtype=torch.float32, device=logp.device)
     _call("dasa_policy_head_bwd", "policy_head", _lib.lib().dasa_policy_head_bwd, _p(logp), _p(cand_len_i32),
           _p(target), _p(action), _p(ent), _p(d_ce), _p(d_logp_a), _p(d_ent), _p(dlogit), C, B, C,
-          int(ignore_index), _stream(), nbytes=4.0 * B * 3 * C)
+          POLICY_MODES[mode], int(ignore_index), _stream(), nbytes=4.0 * B * 3 * C)
     return dlogit
 
 
@@ -565,10 +565,17 @@ def policy_head_bwd(logp, cand_len_i32, target, action, ent, d_ce, d_logp_a, d_e
 _AWS = {}
 
 
+def attn_set_mode(mode):
+    """Attention implementation (include/dasa_hip.h dasa_attn_set_mode): 0 automatic, 1 row-split only."""
+    _lib.check(_lib.lib().dasa_attn_set_mode(int(mode)), "dasa_attn_set_mode")
+
+
 def _attn_ws(device, B, N, D):
     """Attention workspace (include/dasa_hip.h dasa_attn_workspace): one zero-initialised buffer per
     (device, stream), grown on demand. Its leading arrival counters are left zero by every call, so
-    the buffer is zeroed only when (re)allocated; calls on one stream never overlap."""
+    the buffer is zeroed only when (re)allocated; calls on one stream never overlap. The D-split form
+    polls them with a bounded wait, so every call also joins the error-word registry."""
+    _error_word(device)
     need = int(_lib.lib().dasa_attn_workspace(int(B), int(N), int(D)))
     key = (device.index, _stream())
     buf = _AWS.get(key)
@@ -684,7 +691,8 @@ def _error_word(dev):
 
 
 _ERR_BITS = {1: "persistent bi-LSTM forward: inter-workgroup barrier timed out (outputs poisoned with NaN)",
-             2: "persistent bi-LSTM BPTT: inter-workgroup barrier timed out (gate gradients poisoned with NaN)"}
+             2: "persistent bi-LSTM BPTT: inter-workgroup barrier timed out (gate gradients poisoned with NaN)",
+             4: "D-split attention: group barrier timed out (outputs poisoned with NaN)"}
 
 
 def check_device_errors():
@@ -694,6 +702,10 @@ def check_device_errors():
         v = int(w.item())
         if v:
             w.zero_()
+            # a timed-out barrier may leave the inter-workgroup counters of the workspaces non-zero:
+            # drop the cached workspaces (re-allocated zeroed on next use)
+            _WS_OLD.extend(_AWS.values())     # captured graphs may still point at them
+            _AWS.clear()
             msgs = [m for bit, m in _ERR_BITS.items() if v & bit] or [f"error word 0x{v:x}"]
             raise _lib.DasaError(f"device-side failure on cuda:{idx}: " + "; ".join(msgs))
 

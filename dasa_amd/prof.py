@@ -22,12 +22,12 @@ FAMILIES = {
     "gemm_x6": ("mfma", "gemm_f32x6_nt_kernel"),
     "bilstm": ("mfma", "bilstm_step_fused_kernel"),
     "bilstm_bptt": ("mfma", "bilstm_bptt_step_kernel"),
-    "shift_attn": ("hbm", "attn_fwd_kernel<12>"),
-    "shift_attn_bwd": ("hbm", "attn_bwd_dp_kernel<12>+attn_bwd_apply_kernel<12>"),
-    "softdot": ("hbm", "attn_fwd_kernel<16>"),
-    "softdot_bwd": ("hbm", "attn_bwd_dp_kernel<16>+attn_bwd_apply_kernel<16>"),
-    "cand_logit": ("hbm", "attn_fwd_kernel<16>"),
-    "cand_logit_bwd": ("hbm", "attn_bwd_apply_kernel<16>"),
+    "shift_attn": ("hbm", "attn_split_fwd_kernel<5> (B*17 <= 1024) / attn_fwd_kernel<12>"),
+    "shift_attn_bwd": ("hbm", "attn_split_bwd_kernel<5> / attn_bwd_dp_kernel<12>+attn_bwd_apply_kernel<12>"),
+    "softdot": ("hbm", "attn_split_fwd_kernel<10> / attn_fwd_kernel<16>"),
+    "softdot_bwd": ("hbm", "attn_split_bwd_kernel<10> / attn_bwd_dp_kernel<16>+attn_bwd_apply_kernel<16>"),
+    "cand_logit": ("hbm", "attn_split_fwd_kernel<2> / attn_fwd_kernel<16>"),
+    "cand_logit_bwd": ("hbm", "attn_split_bwd_kernel<2> / attn_bwd_apply_kernel<16>"),
     "mha": ("mfma", "mha_fwd_kernel"),
     "layernorm": ("hbm", "ln_fwd_kernel"),
     "embed": ("hbm", "embed_kernel"),

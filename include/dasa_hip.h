@@ -130,8 +130,16 @@ int dasa_mha_bwd(const float* Q, int64_t ldq, const float* K, int64_t ldk, const
  * (raw logits, output_prob=False), probs [B][N], wctx [B][D].
  * ws: dasa_attn_workspace(B, N, D) bytes, 16-B aligned, shared by the four calls below (B <= 32768);
  * its first 65536 32-bit words are arrival counters that must be ZERO on entry (calls leave them
- * zero), so a caller zeroes the buffer once and reuses it on one stream for calls of any shape.  */
+ * zero) and the next 33 x 1024 are monotonic group-barrier counters (zero once), so a caller zeroes
+ * the buffer once and reuses it on one stream for calls of any shape.
+ * Two implementations, same results to fp32 rounding: row-split (a batch row's rows over workgroups,
+ * online-softmax merge by the last workgroup) and, for N <= 80, D % 128 == 0 and B * D/128 <= 1024
+ * (the decision step's B = 20), D-split (a batch row's 128-float column chunks over D/128 workgroups
+ * that meet at a bounded group barrier; a timeout NaN-poisons the outputs and ORs 4 into the error
+ * word, dasa_set_error_word). dasa_attn_set_mode: 0 = automatic (the default; DASA_ATTN_SPLIT=0 in
+ * the environment starts in mode 1), 1 = row-split only. Host-only setting.                        */
 int64_t dasa_attn_workspace(int32_t B, int32_t N, int32_t D);
+int dasa_attn_set_mode(int32_t mode);
 int dasa_softdot_fwd(const float* q, const float* ctx, int64_t ldn, const uint8_t* mask,
                      float* scores, float* probs, float* wctx,
                      int32_t B, int32_t N, int32_t D, float* ws, void* stream);
@@ -186,9 +194,10 @@ int dasa_bilstm_bwd(const float* whh_fwd, const float* whh_bwd, const int32_t* l
 int dasa_bilstm_set_mode(int mode);
 /* Error word for failures that a kernel can only detect on the device (no host sync inside a call):
  * a persistent bi-LSTM launch whose inter-workgroup barrier times out (a workgroup was not
- * co-resident) ORs 1 (forward) / 2 (BPTT) into *dev_word and fills its outputs with NaN. The host
- * reads the word at its own sync points. NULL disables the report (the NaN poisoning stays).
- * Host-only setting. dasa_persist_force_timeout(1) is a test hook: every barrier times out. */
+ * co-resident) ORs 1 (forward) / 2 (BPTT) into *dev_word and fills its outputs with NaN; a D-split
+ * attention group barrier (dasa_softdot_*, dasa_shift_attn_*) ORs 4. The host reads the word at its
+ * own sync points. NULL disables the report (the NaN poisoning stays). Host-only setting.
+ * dasa_persist_force_timeout(1) is a test hook: every such barrier times out. */
 int dasa_set_error_word(uint32_t* dev_word);
 int dasa_persist_force_timeout(int32_t on);
 /* Diagnostic: buf (device, >= 8 * L uint64 words) != NULL makes workgroup 0 of every persistent bi-LSTM
@@ -254,12 +263,17 @@ int dasa_policy_head_fwd(const float* logit, int64_t ld, const int32_t* cand_len
                          int32_t B, int32_t C, int32_t mode, int32_t ignore_index, uint64_t seed,
                          float* logp, float* ce_sum, float* ent, float* logp_a, int64_t* action,
                          float* ws, void* stream);
-/* dlogit[b][c] (row stride ldd) = d_ce * (p - onehot(target)) + d_logp_a[b] * (onehot(action) - p)
- *   + d_ent[b] * (-p * (logp + ent[b])) over unmasked c, 0 where masked; each d_* may be NULL. */
+/* In modes SAMPLE / FORCED, ent and logp_a follow torch.distributions.Categorical(probs): the log-pmf
+ * is l = log(clamp(p, FLT_EPSILON, 1 - FLT_EPSILON)), ent = -sum p l, logp_a = l[action]; in mode
+ * ARGMAX logp_a is the exact log-softmax (F.log_softmax(...).gather).
+ * Backward, `mode` as in the forward: dlogit[b][c] (row stride ldd) = d_ce * (p - onehot(target))
+ *   + d_logp_a[b] * u_a * (onehot(action) - p) + d_ent[b] * p_c * (g_c - sum_j p_j g_j),
+ *   g = -(l + u), u = 1 where the clamp is inactive (always in ARGMAX / TEACHER), over unmasked c, 0
+ *   where masked; each d_* may be NULL. */
 int dasa_policy_head_bwd(const float* logp, const int32_t* cand_len, const int64_t* target,
                          const int64_t* action, const float* ent, const float* d_ce,
                          const float* d_logp_a, const float* d_ent, float* dlogit, int64_t ldd,
-                         int32_t B, int32_t C, int32_t ignore_index, void* stream);
+                         int32_t B, int32_t C, int32_t mode, int32_t ignore_index, void* stream);
 
 /* Device seed source for hipGraph capture. While a counter is set (dev_counter != NULL), every
  * forward dropout launch (layernorm, embeddings, attention probabilities, dropout) records it, and

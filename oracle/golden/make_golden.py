@@ -238,18 +238,26 @@ def _zero_dropout(agent):
                 sub.p = 0.0
 
 
-def _train_iteration(R, agent, out, prefix, sample=None, **kw):
-    """accumulate_gradient('sample') with argmax 'sampling' (or `sample`, a Categorical.sample
-    replacement: GI.reference_forced_sample), then backward; losses, logs + gradients."""
+def _train_iteration(R, agent, out, prefix, forced=None, **kw):
+    """accumulate_gradient('sample') with argmax 'sampling' (or, given `forced`, the seeded action table
+    of GI.reference_forced_sample), then backward; losses, logs + gradients."""
     A = R.args
     A.ml_weight = A.ml_weight_org
     orig_sample = torch.distributions.Categorical.sample
-    torch.distributions.Categorical.sample = sample or (lambda self, *a, **k: self.probs.argmax(-1))
+    uninstall = None
+    if forced is not None:
+        sample, install, uninstall = GI.reference_forced_sample(forced, R.utils)
+        install()
+    else:
+        sample = lambda self, *a, **k: self.probs.argmax(-1)   # noqa: E731
+    torch.distributions.Categorical.sample = sample
     try:
         agent.zero_grad()
         agent.accumulate_gradient("sample", **kw)
     finally:
         torch.distributions.Categorical.sample = orig_sample
+        if uninstall:
+            uninstall()
     _record_losses(agent, out, prefix)
     agent.loss.backward()
     for name, mod in (("encoder", agent.encoder), ("decoder", agent.decoder), ("critic", agent.critic),
@@ -325,8 +333,7 @@ def cfg2(R):
                         variable_len=True)
     agent = make_agent(R, env, cfg["train_max_action"])
     _zero_dropout(agent)
-    sample, _ = GI.reference_forced_sample(GI.forced_table(cfg["train_max_action"], cfg["batch"]))
-    _train_iteration(R, agent, out, "trainf/", sample=sample)
+    _train_iteration(R, agent, out, "trainf/", forced=GI.forced_table(cfg["train_max_action"], cfg["batch"]))
     return out
 
 
@@ -380,8 +387,7 @@ def aug(R):
     env.reset = reset_rec
     rec = Recorder(agent)
     out = {}
-    sample, _ = GI.reference_forced_sample(GI.forced_table(cfg["max_action"], cfg["batch"]))
-    _train_iteration(R, agent, out, "aug/", sample=sample, speaker=spk)
+    _train_iteration(R, agent, out, "aug/", forced=GI.forced_table(cfg["max_action"], cfg["batch"]), speaker=spk)
     assert len(insts) == 2, len(insts)       # one back-translation per rollout (teacher, sample)
     for i, x in enumerate(insts):
         out[f"aug/instr_encoding/{i}"] = x
@@ -395,8 +401,10 @@ def aug(R):
 def optim(R):
     """Two training iterations, each zero_grad -> accumulate_gradient('sample') -> optim_step
     (agent_dg.py:1340-1405: backward, clip_grad_norm 40 on encoder + decoder, RMSprop on all four
-    optimizers, LambdaLR on decoder / critic / adaIn): per iteration the clip norms, every optimizer's
-    learning rate, and per parameter the RMSprop square_avg and the parameter change."""
+    optimizers, LambdaLR on decoder / critic / adaIn): per iteration the loss, the clip norms, every
+    optimizer's learning rate, and per parameter the RMSprop square_avg and the parameter change. (The
+    second iteration's policy is sharp after RMSprop's ~10 lr sign(g) first step: some candidate
+    probabilities underflow, which is why the forced draws count candidates from length2mask.)"""
     A = R.args
     cfg = GI.CFG_OPTIM
     A.d_vl_layers, A.batchSize, A.maxAction, A.views = cfg["vl_layers"], cfg["batch"], cfg["max_action"], 36
@@ -415,15 +423,17 @@ def optim(R):
     try:
         torch.nn.utils.clip_grad_norm = lambda params, m, *a, **k: norms.append(float(orig_clip(params, m, *a, **k)))
         for it in range(cfg["iters"]):
-            sample, _ = GI.reference_forced_sample(GI.forced_table(cfg["max_action"], cfg["batch"],
-                                                                   seed=GI.FORCED_SEED + it))
+            sample, install, uninstall = GI.reference_forced_sample(
+                GI.forced_table(cfg["max_action"], cfg["batch"], seed=GI.FORCED_SEED + it), R.utils)
+            install()
             torch.distributions.Categorical.sample = sample
             before = {name: {k: p.detach().clone() for k, p in m.named_parameters()} for name, m, _ in mods}
             agent.zero_grad()
             agent.accumulate_gradient("sample")
-            out[f"opt{it}/loss"] = np.array(agent.loss.item())
             norms.clear()
+            loss = agent.loss.item()
             agent.optim_step()
+            out[f"opt{it}/loss"] = np.array(loss)
             out[f"opt{it}/clip_norms"] = np.array(norms, np.float64)      # encoder, decoder
             for name, m, opt in mods:
                 out[f"opt{it}/lr/{name}"] = np.array([g["lr"] for g in opt.param_groups], np.float64)
@@ -432,6 +442,7 @@ def optim(R):
                         continue
                     H.grad_record(out, f"opt{it}/delta/{name}.{k}", p.detach() - before[name][k])
                     H.grad_record(out, f"opt{it}/sq/{name}.{k}", opt.state[p]["square_avg"])
+            uninstall()
     finally:
         torch.nn.utils.clip_grad_norm = orig_clip
         torch.distributions.Categorical.sample = orig_sample
@@ -454,8 +465,7 @@ def cfg4_readme(R):
         agent = make_agent(R, env, cfg["max_action"])
         assert agent.encoder.bert.update_add_layer
         _zero_dropout(agent)
-        sample, _ = GI.reference_forced_sample(GI.forced_table(cfg["max_action"], cfg["batch"]))
-        _train_iteration(R, agent, out, "ft3/", sample=sample)
+        _train_iteration(R, agent, out, "ft3/", forced=GI.forced_table(cfg["max_action"], cfg["batch"]))
     finally:
         A.d_update_add_layer = False
     return out

@@ -132,16 +132,29 @@ def forced_actions(table, t, lens):
     return np.minimum((table[t] * lens).astype(np.int64), lens - 1)
 
 
-def reference_forced_sample(table):
-    """A Categorical.sample replacement for the reference run: the t-th call returns the table's step t."""
-    state = {"t": 0}
+def reference_forced_sample(table, utils_mod):
+    """A Categorical.sample replacement for the reference run: the t-th call returns the table's step t,
+    over the candidate counts the step passed to utils.length2mask (agent_dg.py:834, right before the
+    draw; counting probs > 0 instead would miss candidates whose probability underflows). Returns
+    (sample, install, uninstall): install() also wraps utils_mod.length2mask to record the counts."""
+    state = {"t": 0, "lens": None}
+    orig = utils_mod.length2mask
+
+    def length2mask(length, size=None):
+        state["lens"] = [int(x) for x in length]
+        return orig(length, size) if size is not None else orig(length)
 
     def sample(self, *a, **k):
-        lens = (self.probs > 0).sum(-1).numpy()
-        out = torch.from_numpy(forced_actions(table, state["t"], lens))
+        out = torch.from_numpy(forced_actions(table, state["t"], state["lens"]))
         state["t"] += 1
         return out
-    return sample, state
+
+    def install():
+        utils_mod.length2mask = length2mask
+
+    def uninstall():
+        utils_mod.length2mask = orig
+    return sample, install, uninstall
 
 
 # ---- the aug half of the auglistener iteration (speaker + shared env-drop mask) -------------------

@@ -16,7 +16,8 @@ FAMILY_PREFIX = [
     ("mha", ("mha_fwd_kernel", "mha_bwd_kernel")),
     ("layernorm", ("ln_fwd_kernel", "ln_bwd_kernel")),
     ("softdot/shift/cand", ("scores_kernel", "apply_fwd_kernel", "apply_bwd_kernel", "attn_fwd_kernel",
-                            "attn_bwd_apply_kernel", "attn_bwd_scores_kernel")),
+                            "attn_bwd_apply_kernel", "attn_bwd_scores_kernel", "attn_bwd_dp_kernel",
+                            "attn_split_fwd_kernel", "attn_split_bwd_kernel")),
     ("ada_gate", ("AdaFwdOp", "AdaBwdOp")),
     ("adain_musigma", ("adain_musigma",)),
     ("policy_head", ("policy_head_fwd_kernel", "policy_head_bwd_kernel")),
