@@ -55,6 +55,9 @@ def parse():
     p.add_argument("--no-host-input", action="store_true", help="skip the host-input (PCIe-inclusive) leg")
     p.add_argument("--no-hoist", action="store_true", help="skip the --hoist_language (non-default mode) leg")
     p.add_argument("--cfg5-only", action="store_true", help="run only the configs[4] leg (tuning)")
+    p.add_argument("--only", choices=("cfg4", "cfg5"), default=None,
+                   help="run only that leg and print it (the per-workload rocprofv3 --pmc passes)")
+    p.add_argument("--no-cfg4", action="store_true", help="skip the configs[3] (finetune, B=2, vl=3) leg")
     p.add_argument("--cfg5-steps", type=int, default=6, help="decision steps per configs[4] rollout")
     p.add_argument("--backend", default="nccl", help="nccl (= RCCL on ROCm) | gloo (rehearsal only)")
     p.add_argument("--same-device", action="store_true",
@@ -79,9 +82,10 @@ def setup_dist(a):
     return rank, world
 
 
-def build_agent(a, rank, world):
+def build_agent(a, rank, world, finetune=False):
     from dasa_amd.r2r import param
-    param.readme_train(["--d_vl_layers", str(a.vl), "--batchSize", str(a.batch), "--maxAction", str(a.max_action)])
+    flags = ["--d_vl_layers", str(a.vl), "--batchSize", str(a.batch), "--maxAction", str(a.max_action)]
+    (param.readme_finetune if finetune else param.readme_train)(flags)
     param.args.ml_weight = param.args.ml_weight_org     # train.py:233 (GT env)
     from dasa_amd import dp
     from dasa_amd.r2r.agent_dg import Seq2SeqAgent
@@ -209,6 +213,35 @@ def host_input_leg(a, steps=2):
             "note": "cfg2 training iteration with host-built observation features copied H2D (pinned) each step"}
 
 
+def cfg4_leg(a, steps=3):
+    """BASELINE configs[3] per rank: the README finetune iteration (README.md:104-116:
+    --d_update_add_layer True, so the LXRT layers and the VisionEncoder train; d_vl_layers 3, batchSize 2,
+    maxAction 35, lr 2e-6, no LR scheduler), teacher + sampled rollout, backward, RMSprop, on one GPU
+    (the 8-rank DP form is the driver's scaling run). Kernel table + roofline of the dominant family
+    from an extra HIP-event iteration, PMC values only from this workload's own rocprofv3 passes."""
+    from types import SimpleNamespace
+    from dasa_amd import prof
+    c = SimpleNamespace(**vars(a))
+    c.batch, c.vl = 2, 3
+    agent, _ = build_agent(c, 0, 1, finetune=True)
+    assert agent.encoder.bert.update_add_layer
+    train_step(agent)
+    u, dt = timed(lambda: train_step(agent), steps, 0, 1)
+    res = {"workload": "configs[3] per rank: README finetune iteration (d_update_add_layer, vl=3, B=2, "
+                       f"maxAction {c.max_action}, teacher + sample rollout, backward, RMSprop)",
+           "value": round(u / dt, 2), "unit": "agent-decisions/s", "ms_per_step": round(1000 * dt / steps, 2)}
+    with prof.collect(a.shapes) as rec:
+        train_step(agent)
+    summ = rec.summary(pmc_workload="cfg4")
+    res["roofline"] = summ["roofline"]
+    res["kernels"] = dict(list(summ["kernels"].items())[:8])
+    if "shapes" in summ:
+        res["shapes"] = summ["shapes"]
+    del agent
+    torch.cuda.empty_cache()
+    return res
+
+
 def cfg5_leg(a):
     """BASELINE configs[4]: B=256, d_vl_layers=6, 36x2048 synthetic feats, forward (eval/argmax rollout)
     with bf16 GEMM operands and fp32 accumulation (ops.bf16_matmul); the same rollout in fp32 beside it.
@@ -231,7 +264,7 @@ def cfg5_leg(a):
         ent = {"value": round(u / dt, 2), "ms_per_step": round(1000 * dt * c.batch / u, 2)}
         with prof.collect() as rec:
             run()
-        summ = rec.summary()
+        summ = rec.summary(pmc_workload="cfg5")
         ent["kernels"] = {k: v for k, v in summ["kernels"].items() if k in ("gemm", "gemm_x6", "gemm_bf16", "mha",
                                                                               "bilstm", "layernorm", "elementwise")}
         fam = "gemm_bf16" if mode == "bf16" else ("gemm_x6" if "gemm_x6" in summ["kernels"] else "gemm")
@@ -239,6 +272,10 @@ def cfg5_leg(a):
             k = summ["kernels"][fam]
             ent["roofline"] = {"kernel": fam, "bound": "mfma", "achieved": k["achieved"], "peak": k["peak"],
                                "unit": "TFLOP/s", "frac": k["frac"]}
+            if summ["roofline"]["kernel"] == fam and summ["roofline"].get("traffic") is not None:
+                for key in ("traffic", "mfma_busy", "traffic_source"):
+                    if key in summ["roofline"]:
+                        ent["roofline"][key] = summ["roofline"][key]
         res[mode] = ent
     res["dtype_note"] = ("bf16: nn.Linear operands rounded to bf16 (weights once, activations on load), fp32 "
                          "accumulation and epilogue; attention cores, LayerNorm, softmax, LSTM recurrences fp32")
@@ -253,8 +290,11 @@ def main():
     torch.manual_seed(1 + rank)
     from dasa_amd import functional as DF
     DF.reseed(1234 + rank)
-    if a.cfg5_only:
+    if a.cfg5_only or a.only == "cfg5":
         print(json.dumps({"cfg5": cfg5_leg(a)}), flush=True)
+        return
+    if a.only == "cfg4":
+        print(json.dumps({"cfg4": cfg4_leg(a)}), flush=True)
         return
     agent, env = build_agent(a, rank, world)
     for _ in range(a.warmup):
@@ -303,6 +343,8 @@ def main():
         out["hoist_language"] = hoist_leg(agent)
     if rank == 0 and world == 1 and not a.no_host_input:
         out["host_input"] = host_input_leg(a)
+    if rank == 0 and world == 1 and not a.no_cfg4:
+        out["cfg4"] = cfg4_leg(a)
     if rank == 0 and world == 1 and not a.no_cfg5:
         out["cfg5"] = cfg5_leg(a)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

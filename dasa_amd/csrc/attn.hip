@@ -265,6 +265,123 @@ __global__ __launch_bounds__(1024) void attn_fwd_kernel(FwdArgs a) {
   }
 }
 
+// ---- whole-row form: one workgroup per batch row, rows streamed ring by ring -----------------------
+// No cross-workgroup hand-off at all (each costs several microseconds on MI355X: MI355X_MICROARCH.md
+// "handoff-flag", "barrier-counter"): thread t owns float4 column t of every row. The rows come in
+// slices of 12 (for the panorama: the three elevation rings), two slices in registers at a time: a
+// slice's row dots are reduce-scattered over the wave and meet in LDS, wave 0 turns them into
+// exp(s - m) weights against the running max m (and shifts them within the ring: the K-tap
+// correlation is linear and never leaves a ring, model.py:337-344), and every thread folds the slice
+// into its running context column (online softmax: earlier slices rescaled when m grows). At the end
+// the exact softmax / shifted weights are written from the saved scores, and wctx = acc / Z. A
+// workgroup streams its 313 KB panorama through one CU: at B = 20 that beats the row-split kernel's
+// launch + merge latency, and at B = 256 its 256 workgroups stream at HBM rate.
+template <int NS>
+__global__ __launch_bounds__(576) void attn_rows_fwd_kernel(FwdArgs a) {
+  __shared__ float red[kMaxW][16];
+  __shared__ float ssc[12 * NS], swt[12], sw[kMaxK + 1], sscale;
+  const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6, W = blockDim.x >> 6;
+  const int N = a.N, D4 = a.D >> 2;
+  const bool shift = a.shift_logits != nullptr, col = t < D4;
+  const float* rows = a.ctx + (long)b * N * a.ldn;
+  float4 xa[12], xb[12];
+  float4 qv = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto load = [&](float4 (&x)[12], int s0) {
+    if (col) {
+#pragma unroll
+      for (int i = 0; i < 12; ++i) x[i] = reinterpret_cast<const float4*>(rows + (long)min(s0 + i, N - 1) * a.ldn)[t];
+    }
+  };
+  load(xa, 0);
+  if (NS > 1) load(xb, 12);
+  if (col) qv = reinterpret_cast<const float4*>(a.q + (long)b * a.D)[t];
+  if (shift && t < 64) shift_taps(a.shift_logits + (long)b * a.K, a.K, sw, lane);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  float m_run = -INFINITY, z_run = 0.f;   // wave 0's running max / sum (lane-uniform)
+  auto slice = [&](const float4 (&x)[12], int s0) {
+    float v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = (i < 12 && col) ? dot4(x[i], qv) : 0.f;
+    const float sum = reduce_scatter16(v, lane);
+    const int r = (lane >> 2) & 15;
+    if ((lane & 3) == 0 && r < 12) red[w][r] = sum;
+    __syncthreads();
+    if (t < 64) {
+      float sv = -INFINITY;
+      if (lane < 12 && s0 + lane < N) {
+        float tot = 0.f;
+        for (int i = 0; i < W; ++i) tot += red[i][lane];
+        ssc[s0 + lane] = tot;
+        sv = (a.mask && a.mask[(long)b * N + s0 + lane]) ? -INFINITY : tot;
+      }
+      const float m_new = fmaxf(m_run, wave_max(sv));
+      const float e = sv == -INFINITY ? 0.f : __expf(sv - m_new);
+      const float sc = m_run == -INFINITY ? 0.f : __expf(m_run - m_new);
+      z_run = z_run * sc + wave_sum(e);
+      m_run = m_new;
+      float we = e;
+      if (shift) {   // the ring's shifted weights, exp(s - m_new) scale
+        if (lane < 12) swt[lane] = e;
+        lds_wave_sync();
+        const int P = a.K / 2;
+        we = 0.f;
+        if (lane < 12)
+          for (int k = 0; k < a.K; ++k) {
+            int jj = lane + k - P;
+            jj = ((jj % 12) + 12) % 12;
+            we = fmaf(sw[k], swt[jj], we);
+          }
+        lds_wave_sync();
+      }
+      if (lane < 12) swt[lane] = we;
+      if (lane == 0) sscale = sc;
+    }
+    __syncthreads();
+    if (col) {
+      const float sc = sscale;
+      acc.x *= sc; acc.y *= sc; acc.z *= sc; acc.w *= sc;
+#pragma unroll
+      for (int i = 0; i < 12; ++i) fma4(swt[i], x[i], acc);
+    }
+    __syncthreads();   // red / swt are rewritten by the next slice
+  };
+  slice(xa, 0);
+  if (NS > 2) load(xa, 24);
+  if (NS > 1) slice(xb, 12);
+  if (NS > 2) slice(xa, 24);
+  if (t < 64) {   // the exact softmax / shifted weights from the saved scores
+    const float M = m_run, inv = 1.f / z_run;
+    if (lane == 0) sscale = inv;
+    for (int n = lane; n < N; n += 64) {
+      const bool masked = a.mask && a.mask[(long)b * N + n];
+      const float p = masked ? 0.f : __expf(ssc[n] - M) * inv;
+      if (a.scores) a.scores[(long)b * N + n] = ssc[n];
+      if (a.probs) a.probs[(long)b * N + n] = p;
+      ssc[n] = p;
+    }
+    lds_wave_sync();
+    if (shift) {
+      const int P = a.K / 2;
+      for (int n = lane; n < N; n += 64) {
+        const int r = n / 12, j = n % 12;
+        float wgt = 0.f;
+        for (int k = 0; k < a.K; ++k) {
+          int jj = j + k - P;
+          jj = ((jj % 12) + 12) % 12;
+          wgt = fmaf(sw[k], ssc[r * 12 + jj], wgt);
+        }
+        if (a.shifted) a.shifted[(long)b * N + n] = wgt;
+      }
+      if (a.wsm && lane < a.K) a.wsm[(long)b * a.K + lane] = sw[lane];
+    }
+  }
+  __syncthreads();
+  if (a.wctx && col) {
+    const float inv = sscale;
+    reinterpret_cast<float4*>(a.wctx + (long)b * a.D)[t] = make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
+  }
+}
+
 struct BwdArgs {
   const float* q; const float* ctx; long ldn;
   const float* probs;     // softmax a [B][N]
@@ -419,23 +536,17 @@ __global__ __launch_bounds__(1024) void attn_bwd_apply_kernel(BwdArgs a) {
   }
 }
 
-// ---- D-split forms (small batches: the decision step at B = 20) -----------------------------------
-// The row-split kernels above give a batch row ceil(N / RB) workgroups (60 / 100 / 20 at B = 20 for
-// the panorama / instruction / candidates), each streaming up to 12-16 rows x 8.7 KB through one CU:
-// per-CU bandwidth and the merge tail bound them, not HBM. Here a batch row gets G = D / 128
-// workgroups instead (17 for D = 2176, 16 for 2048: 340 / 320 / 340 at B = 20), each owning a 128-float
-// column chunk of ALL N rows (N <= 80): thread (row lane rl = t / 32, column t % 32) holds rows
-// rl, rl + 8, ... of its float4 column in registers for both passes.
-//   forward   partial row dots over the chunk -> published write-through; the G workgroups of the batch
-//             row meet at a group barrier (bounded spin on an agent-scope counter); every workgroup then
-//             sums the G partials in the same order (identical scores everywhere), forms the softmax (and
-//             the K-tap shift) and writes ITS chunk of the weighted context from the rows in registers. No
-//             merge pass: each output column is produced once. Scores-only calls (the candidate logits)
-//             need no barrier: the last workgroup to arrive sums the partials.
-//   backward  one launch (the row-split form takes two): partial dp = ctx . dwctx -> group barrier ->
-//             every workgroup forms ds / the shift backward for the N rows, then writes its chunk of dctx
-//             and of dq directly (no dq partial merge). Without dwctx (candidate logits) no barrier.
-// Co-residency: the spin forms are used only while B x G <= kSplitMaxWG (4 small workgroups per CU);
+// ---- D-split backward (small batches: the decision step at B = 20) --------------------------------
+// The row-split backward gives a batch row ceil(N / RB) workgroups (60 / 100 / 20 at B = 20) and two
+// launches. Here a batch row gets G = D / 128 workgroups instead (17 for D = 2176, 16 for 2048), each
+// owning a 128-float column chunk of ALL N rows (N <= 80): thread (row lane rl = t / 32, column t % 32)
+// holds rows rl, rl + 8, ... of its float4 column in registers. One launch: partial dp = ctx . dwctx
+// over the chunk, published write-through; the G workgroups meet at a group barrier (bounded spin on an
+// agent-scope counter); every workgroup sums the G partials in the same order, forms ds / the shift
+// backward for the N rows, then writes its chunk of dctx and of dq directly (no dq partial merge).
+// Without dwctx (candidate logits) there is no barrier. (The forward takes the whole-row form above:
+// a cross-workgroup hand-off costs more than streaming the whole row through one CU.)
+// Co-residency: the spin form is used only while B x G <= kSplitMaxWG (4 small workgroups per CU);
 // workgroups are dispatched in order, so a group whose first member runs is completed by workgroups
 // that are either running or next in line. A wait that exceeds kAttnSpinTicks anyway NaN-poisons the
 // workgroup's outputs and sets bit 4 of the library error word (raised by ops.check_device_errors).
@@ -523,107 +634,6 @@ __device__ __forceinline__ float4 rowlane_sum(float4 acc, float4 (*red4)[kCW]) {
     }
   }
   return s;
-}
-
-template <int RPT>
-__global__ __launch_bounds__(256) void attn_split_fwd_kernel(SplitArgs a) {
-  __shared__ float4 red4[8][kCW];
-  __shared__ float spart[256 * kMaxPartPerThread];
-  __shared__ float sc[kSplitMaxN], wv[kSplitMaxN], sw[kMaxK + 1];
-  __shared__ int s_flag;
-  const int g = blockIdx.x, b = blockIdx.y, t = threadIdx.x, lane = t & 63, col = t & 31, rl = t >> 5;
-  const int N = a.N, G = a.G, c = g * kCW + col;
-  const bool shift = a.shift_logits != nullptr;
-  const float* base = a.ctx + (long)b * N * a.ldn;
-  float4 x[RPT];
-#pragma unroll
-  for (int i = 0; i < RPT; ++i) x[i] = reinterpret_cast<const float4*>(base + (long)min(rl + 8 * i, N - 1) * a.ldn)[c];
-  const float4 qv = reinterpret_cast<const float4*>(a.q + (long)b * a.D)[c];
-  float v[RPT];
-  chunk_row_dots<RPT>(x, qv, v);
-  const __amdgpu_buffer_rsrc_t wr = ws_rsrc(a.ws);
-  const int pbase = a.o_part + (int)((long)b * G * N) * 4;
-  if (col == 0) {
-#pragma unroll
-    for (int i = 0; i < RPT; ++i)
-      if (rl + 8 * i < N) pub1(wr, pbase + (g * N + rl + 8 * i) * 4, v[i]);
-  }
-  const bool combine = a.wctx || a.probs || a.shifted;
-  if (!combine) {   // scores only: the last workgroup of the row sums the partials
-    if (!last_arriver(a.cnt + b, G, &s_flag)) return;
-    gather_partials(wr, pbase, G * N, spart);
-    if (t < N && a.scores) {
-      float s = 0.f;
-      for (int gg = 0; gg < G; ++gg) s += spart[gg * N + t];
-      a.scores[(long)b * N + t] = s;
-    }
-    return;
-  }
-  if (!group_barrier(a.bar + b, G, a.err, a.force, &s_flag)) {
-    const float qnan = __builtin_nanf("");
-    if (t < kCW && a.wctx) reinterpret_cast<float4*>(a.wctx + (long)b * a.D)[g * kCW + t] = make_float4(qnan, qnan, qnan, qnan);
-    if (g == 0)
-      for (int n = t; n < N; n += blockDim.x) {
-        if (a.probs) a.probs[(long)b * N + n] = qnan;
-        if (a.shifted) a.shifted[(long)b * N + n] = qnan;
-      }
-    return;
-  }
-  gather_partials(wr, pbase, G * N, spart);
-  if (t < N) {   // identical sums (same order) in every workgroup of the row
-    float s = 0.f;
-    for (int gg = 0; gg < G; ++gg) s += spart[gg * N + t];
-    sc[t] = s;
-    if (g == 0 && a.scores) a.scores[(long)b * N + t] = s;
-  }
-  __syncthreads();
-  if (t < 64) {
-    float s0 = -INFINITY, s1 = -INFINITY;
-    if (lane < N) s0 = (a.mask && a.mask[(long)b * N + lane]) ? -INFINITY : sc[lane];
-    if (lane + 64 < N) s1 = (a.mask && a.mask[(long)b * N + lane + 64]) ? -INFINITY : sc[lane + 64];
-    const float m = wave_max(fmaxf(s0, s1));
-    const float e0 = s0 == -INFINITY ? 0.f : __expf(s0 - m), e1 = s1 == -INFINITY ? 0.f : __expf(s1 - m);
-    const float inv = 1.f / wave_sum(e0 + e1);
-    const float p0 = e0 * inv, p1 = e1 * inv;
-    if (shift) shift_taps(a.shift_logits + (long)b * a.K, a.K, sw, lane);
-    lds_wave_sync();
-    if (lane < N) sc[lane] = p0;            // sc: the softmax now
-    if (lane + 64 < N) sc[lane + 64] = p1;
-    lds_wave_sync();
-    float w0 = p0, w1 = p1;
-    if (shift && lane < N) {   // N = 36: three elevation rings of 12 headings (model.py:337-344)
-      const int P = a.K / 2, r = lane / 12, j = lane % 12;
-      w0 = 0.f;
-      for (int k = 0; k < a.K; ++k) {
-        int jj = j + k - P;
-        jj = ((jj % 12) + 12) % 12;
-        w0 = fmaf(sw[k], sc[r * 12 + jj], w0);
-      }
-    }
-    if (lane < N) wv[lane] = w0;
-    if (lane + 64 < N) wv[lane + 64] = w1;
-    if (g == 0) {
-      if (lane < N) {
-        if (a.probs) a.probs[(long)b * N + lane] = p0;
-        if (a.shifted) a.shifted[(long)b * N + lane] = w0;
-      }
-      if (lane + 64 < N) {
-        if (a.probs) a.probs[(long)b * N + lane + 64] = p1;
-        if (a.shifted) a.shifted[(long)b * N + lane + 64] = w1;
-      }
-      if (shift && a.wsm && lane < a.K) a.wsm[(long)b * a.K + lane] = sw[lane];
-    }
-  }
-  __syncthreads();
-  if (!a.wctx) return;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-  for (int i = 0; i < RPT; ++i) {
-    const int r = rl + 8 * i;
-    fma4(r < N ? wv[r] : 0.f, x[i], acc);
-  }
-  const float4 o = rowlane_sum(acc, red4);
-  if (t < kCW) reinterpret_cast<float4*>(a.wctx + (long)b * a.D)[g * kCW + t] = o;
 }
 
 template <int RPT>
@@ -819,22 +829,42 @@ int split_rpt(int B, int N, int D, bool spin) {
   return N <= 16 ? 2 : (N <= 40 ? 5 : 10);
 }
 
-template <int RPT, bool FWD>
+template <int RPT>
 void split_launch(const SplitArgs& a, int B, hipStream_t st) {
-  if (FWD) hipLaunchKernelGGL(attn_split_fwd_kernel<RPT>, dim3(a.G, B), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(attn_split_bwd_kernel<RPT>, dim3(a.G, B), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(attn_split_bwd_kernel<RPT>, dim3(a.G, B), dim3(256), 0, st, a);
 }
 
-template <bool FWD>
-int launch_split(SplitArgs a, int rpt, int B, void* ws, hipStream_t st) {
+// Whole-row forward: N <= 36 rows, D4 = D / 4 <= 576 columns (one per thread), mode 0, and at least
+// 128 batch rows. One CU streams a row at ~35-40 GB/s (the loads one CU keeps in flight), so the form
+// pays at large B — B = 256: shift 0.44 -> 0.57 of HBM peak — and loses at B = 20, where the row-split
+// kernel's 60 workgroups win despite their merge (9.2 vs 10.6 us; profiles/r03/attn_forms.txt).
+constexpr int kRowsMinB = 128;
+bool rows_ok(int B, int N, int D) {
+  if (g_attn_mode < 0) split_rpt(1, 1, 128, false);   // reads DASA_ATTN_SPLIT once
+  return g_attn_mode == 0 && B >= kRowsMinB && N >= 1 && N <= 36 && D <= 4 * 576;
+}
+
+int launch_rows(const FwdArgs& a, int B, hipStream_t st) {
+  const int ns = (a.N + 11) / 12;
+  const dim3 grid(B), block(block_threads(a.D));
+  switch (ns) {
+    case 1: hipLaunchKernelGGL(attn_rows_fwd_kernel<1>, grid, block, 0, st, a); break;
+    case 2: hipLaunchKernelGGL(attn_rows_fwd_kernel<2>, grid, block, 0, st, a); break;
+    default: hipLaunchKernelGGL(attn_rows_fwd_kernel<3>, grid, block, 0, st, a); break;
+  }
+  DASA_CHECK_LAUNCH();
+  return 0;
+}
+
+int launch_split_bwd(SplitArgs a, int rpt, int B, void* ws, hipStream_t st) {
   WsLayout L = ws_layout(ws, B, a.N, a.D);
   a.G = a.D / (4 * kCW);
   a.cnt = L.cnt1; a.bar = L.bar + (long)a.G * kSplitMaxWG; a.ws = (float*)ws; a.o_part = L.o_part;
   a.err = dasa_err_word_host(); a.force = dasa_force_timeout_host();
   switch (rpt) {
-    case 2: split_launch<2, FWD>(a, B, st); break;
-    case 5: split_launch<5, FWD>(a, B, st); break;
-    default: split_launch<10, FWD>(a, B, st); break;
+    case 2: split_launch<2>(a, B, st); break;
+    case 5: split_launch<5>(a, B, st); break;
+    default: split_launch<10>(a, B, st); break;
   }
   DASA_CHECK_LAUNCH();
   return 0;
@@ -863,14 +893,8 @@ extern "C" int dasa_softdot_fwd(const float* q, const float* ctx, int64_t ldn, c
                                 int32_t B, int32_t N, int32_t D, float* ws, void* stream) {
   if (B <= 0 || N <= 0) return 0;
   if (bad_common(q, ctx, ldn, B, N, D, ws) || (wctx && !aligned16(wctx))) return (int)hipErrorInvalidValue;
-  const int rpt = split_rpt(B, N, D, probs || wctx);
-  if (rpt) {
-    SplitArgs sa{};
-    sa.q = q; sa.ctx = ctx; sa.ldn = ldn; sa.mask = mask; sa.scores = scores; sa.probs = probs; sa.wctx = wctx;
-    sa.N = N; sa.D = D;
-    return launch_split<true>(sa, rpt, B, ws, (hipStream_t)stream);
-  }
   FwdArgs a{q, ctx, (long)ldn, mask, nullptr, 0, scores, probs, nullptr, nullptr, wctx, N, D};
+  if ((probs || wctx) && rows_ok(B, N, D)) return launch_rows(a, B, (hipStream_t)stream);
   return launch_fwd<16>(a, B, ws, (hipStream_t)stream);
 }
 
@@ -887,7 +911,7 @@ extern "C" int dasa_softdot_bwd(const float* q, const float* ctx, int64_t ldn, c
     SplitArgs sa{};
     sa.q = q; sa.ctx = ctx; sa.ldn = ldn; sa.a_probs = probs; sa.dwctx = dwctx; sa.dscores = dscores;
     sa.dq = dq; sa.dctx = dctx; sa.accumulate = accumulate; sa.N = N; sa.D = D;
-    return launch_split<false>(sa, rpt, B, ws, (hipStream_t)stream);
+    return launch_split_bwd(sa, rpt, B, ws, (hipStream_t)stream);
   }
   BwdArgs a{q, ctx, (long)ldn, probs, nullptr, nullptr, 0, dwctx, dscores, dq, dctx, accumulate, nullptr, N, D};
   return launch_bwd<16>(a, B, ws, (hipStream_t)stream);
@@ -900,14 +924,8 @@ extern "C" int dasa_shift_attn_fwd(const float* q, const float* ctx, int64_t ldn
   if (B <= 0) return 0;
   if (K < 1 || K > kMaxK || bad_common(q, ctx, ldn, B, N, D, ws) || !shift_logits || !wctx || !aligned16(wctx))
     return (int)hipErrorInvalidValue;
-  const int rpt = split_rpt(B, N, D, true);
-  if (rpt) {
-    SplitArgs sa{};
-    sa.q = q; sa.ctx = ctx; sa.ldn = ldn; sa.shift_logits = shift_logits; sa.K = K; sa.probs = attn;
-    sa.shifted = shifted; sa.wsm = wsm; sa.wctx = wctx; sa.N = N; sa.D = D;
-    return launch_split<true>(sa, rpt, B, ws, (hipStream_t)stream);
-  }
   FwdArgs a{q, ctx, (long)ldn, nullptr, shift_logits, K, nullptr, attn, shifted, wsm, wctx, N, D};
+  if (rows_ok(B, N, D)) return launch_rows(a, B, (hipStream_t)stream);
   return launch_fwd<12>(a, B, ws, (hipStream_t)stream);
 }
 
@@ -926,7 +944,7 @@ extern "C" int dasa_shift_attn_bwd(const float* q, const float* ctx, int64_t ldn
     sa.q = q; sa.ctx = ctx; sa.ldn = ldn; sa.K = K; sa.a_probs = attn; sa.a_shifted = shifted; sa.a_wsm = wsm;
     sa.dwctx = dwctx; sa.dq = dq; sa.dctx = dctx; sa.accumulate = accumulate; sa.dshift = dshift_logits;
     sa.N = N; sa.D = D;
-    return launch_split<false>(sa, rpt, B, ws, (hipStream_t)stream);
+    return launch_split_bwd(sa, rpt, B, ws, (hipStream_t)stream);
   }
   BwdArgs a{q, ctx, (long)ldn, attn, shifted, wsm, K, dwctx, nullptr, dq, dctx, accumulate,
             dshift_logits, N, D};

@@ -103,17 +103,70 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
   }
 }
 
-// dx = rstd * (g*dy - mean(g*dy) - xhat * mean(g*dy*xhat)); dgamma += dy*xhat; dbeta += dy.
+// dx = rstd * (g*dy - mean(g*dy) - xhat * mean(g*dy*xhat)); dgamma += sum_rows dy*xhat; dbeta += sum_rows dy.
+// One launch, two kinds of 1024-thread block: the first ceil(M/16) blocks take one row per wave (dx); the last
+// ceil(N/256) take 64 float4 columns each and reduce dgamma / dbeta over ALL rows (16 waves stride the rows, then a
+// fixed-order LDS reduction), so the parameter gradients are deterministic and need no atomics (the previous
+// per-element global atomics serialised on the same N addresses from every row block: 45 us per launch at the
+// finetune shapes).
+constexpr int kLnBwdWaves = 16;
 template <int VPL>
-__global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ xsum,
-                                                     const float* __restrict__ gamma, const float* __restrict__ mean_in,
-                                                     const float* __restrict__ rstd_in, float* __restrict__ dx,
-                                                     float* __restrict__ dgamma, float* __restrict__ dbeta, int M,
-                                                     int N) {
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+__global__ __launch_bounds__(1024) void ln_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ xsum,
+                                                      const float* __restrict__ gamma, const float* __restrict__ mean_in,
+                                                      const float* __restrict__ rstd_in, float* __restrict__ dx,
+                                                      float* __restrict__ dgamma, float* __restrict__ dbeta, int M,
+                                                      int N) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int rowBlocks = (M + kLnBwdWaves - 1) / kLnBwdWaves;
+  const int N4 = N >> 2;
+  if ((int)blockIdx.x >= rowBlocks) {
+    __shared__ float4 red[2][kLnBwdWaves][64];
+    const int c = ((int)blockIdx.x - rowBlocks) * 64 + lane;
+    const bool cok = c < N4;
+    const int cc = cok ? c : 0;
+    float4 sg = make_float4(0.f, 0.f, 0.f, 0.f), sb = sg;
+    for (int r0 = wave; r0 < M; r0 += 4 * kLnBwdWaves) {
+      float4 xs[4], d[4];
+      float mu[4], rs[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {        // all loads first (clamped rows), then the arithmetic
+        const int r = r0 + u * kLnBwdWaves, rr = r < M ? r : M - 1;
+        xs[u] = reinterpret_cast<const float4*>(xsum + (long)rr * N)[cc];
+        d[u] = reinterpret_cast<const float4*>(dy + (long)rr * N)[cc];
+        mu[u] = mean_in[rr];
+        rs[u] = r < M ? rstd_in[rr] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (r0 + u * kLnBwdWaves >= M) break;
+        sg.x = fmaf(d[u].x, (xs[u].x - mu[u]) * rs[u], sg.x);
+        sg.y = fmaf(d[u].y, (xs[u].y - mu[u]) * rs[u], sg.y);
+        sg.z = fmaf(d[u].z, (xs[u].z - mu[u]) * rs[u], sg.z);
+        sg.w = fmaf(d[u].w, (xs[u].w - mu[u]) * rs[u], sg.w);
+        sb.x += d[u].x; sb.y += d[u].y; sb.z += d[u].z; sb.w += d[u].w;
+      }
+    }
+    red[0][wave][lane] = sg;
+    red[1][wave][lane] = sb;
+    __syncthreads();
+    if (wave < 2 && cok) {
+      float* dst = wave == 0 ? dgamma : dbeta;
+      if (dst) {
+        float4 acc = red[wave][0][lane];
+        for (int w = 1; w < kLnBwdWaves; ++w) {
+          const float4 v = red[wave][w][lane];
+          acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        }
+        float4* o = reinterpret_cast<float4*>(dst) + c;
+        const float4 prev = *o;
+        *o = make_float4(prev.x + acc.x, prev.y + acc.y, prev.z + acc.z, prev.w + acc.w);
+      }
+    }
+    return;
+  }
+  const int row = blockIdx.x * kLnBwdWaves + wave;
   if (row >= M) return;
   const float mean = mean_in[row], rstd = rstd_in[row];
-  const int N4 = N >> 2;
   float4 xh[VPL], gd[VPL];
   float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -127,18 +180,6 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
       gd[i] = make_float4(d.x * g.x, d.y * g.y, d.z * g.z, d.w * g.w);
       s1 += gd[i].x + gd[i].y + gd[i].z + gd[i].w;
       s2 += gd[i].x * xh[i].x + gd[i].y * xh[i].y + gd[i].z * xh[i].z + gd[i].w * xh[i].w;
-      if (dgamma) {
-        atomicAdd(dgamma + 4 * c + 0, d.x * xh[i].x);
-        atomicAdd(dgamma + 4 * c + 1, d.y * xh[i].y);
-        atomicAdd(dgamma + 4 * c + 2, d.z * xh[i].z);
-        atomicAdd(dgamma + 4 * c + 3, d.w * xh[i].w);
-      }
-      if (dbeta) {
-        atomicAdd(dbeta + 4 * c + 0, d.x);
-        atomicAdd(dbeta + 4 * c + 1, d.y);
-        atomicAdd(dbeta + 4 * c + 2, d.z);
-        atomicAdd(dbeta + 4 * c + 3, d.w);
-      }
     }
   }
   const float m1 = wave_sum(s1) / N, m2 = wave_sum(s2) / N;
@@ -426,6 +467,140 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(MhaArgs a, const float* dO
   }
 }
 
+// Backward for Lq, Lk <= 80 (the language / LXRT shapes): one workgroup per (b, h), every operand staged
+// in LDS once (K-major copies where a product needs them: dO^T, V^T, dS^T), and the four products
+//   dP = dO V^T (x the dropout scale),  dV = P_dropped^T dO,  dQ = dS K,  dK = dS^T Q,
+//   dS = P (dP - rowsum(P dP)) * scale
+// as register-blocked 4x4 outer products over LDS rows (two float4 reads per 16 FMAs). No atomics: the
+// previous form accumulated dK / dV with per-element LDS atomics row by row (0.64 ms per launch at the
+// finetune shapes, B = 2; bench.py cfg4 leg).
+constexpr int kBwdMaxL = 80;
+constexpr int kBwdLd = kBwdMaxL + 4;   // row stride of [.][Lq] / [.][Lk] tiles
+constexpr int kBwdLdD = kDh + 4;       // row stride of [.][64] tiles
+constexpr int kBwdBufA = (kDh * kBwdLd > kBwdMaxL * kBwdLdD) ? kDh * kBwdLd : kBwdMaxL * kBwdLdD;
+constexpr int kBwdBufL = kBwdMaxL * kBwdLd;
+
+// C[m][n] = sum_k A[k][m] B[k][n] over 4x4 register blocks (A, B row-major in LDS, m / n multiples of 4).
+template <typename Epi>
+__device__ __forceinline__ void lds_tn_blocks(const float* A, int lda, const float* B, int ldb, int K, int MB, int NB,
+                                              Epi epi) {
+  for (int blk = threadIdx.x; blk < MB * NB; blk += blockDim.x) {
+    const int m0 = (blk / NB) * 4, n0 = (blk % NB) * 4;
+    float acc[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[r][c] = 0.f;
+    for (int k = 0; k < K; ++k) {
+      const float4 av = *reinterpret_cast<const float4*>(A + k * lda + m0);
+      const float4 bv = *reinterpret_cast<const float4*>(B + k * ldb + n0);
+      const float am[4] = {av.x, av.y, av.z, av.w}, bn[4] = {bv.x, bv.y, bv.z, bv.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[r][c] = fmaf(am[r], bn[c], acc[r][c]);
+    }
+    epi(m0, n0, acc);
+  }
+}
+
+__global__ __launch_bounds__(256) void mha_bwd_lds_kernel(MhaArgs a, const float* dO, long lddo, float* dQ, float* dK,
+                                                          float* dV) {
+  __shared__ float bufA[kBwdBufA];   // dO^T [64][Lq]; then Q [Lq][64]
+  __shared__ float bufB[kBwdBufA];   // V^T [64][Lk]; then K [Lk][64]
+  __shared__ float sP[kBwdBufL];     // P [Lq][Lk]; then P_dropped
+  __shared__ float sdO[kBwdMaxL * kBwdLdD];   // dO [Lq][64]
+  __shared__ float sdS[kBwdBufL];    // dP, then dS [Lq][Lk]
+  __shared__ float sdST[kBwdBufL];   // dS^T [Lk][Lq]
+  __shared__ float rowdot[kBwdMaxL];
+  const int bh = blockIdx.x, b = bh / a.heads, h = bh % a.heads, t = threadIdx.x;
+  const int Lq = a.Lq, Lk = a.Lk, Lq4 = (Lq + 3) & ~3, Lk4 = (Lk + 3) & ~3;
+  const long pbase = ((long)b * a.heads + h) * Lq * Lk;
+  const bool drop = a.p > 0.f;
+  for (int idx = t; idx < Lq4 * kDh; idx += blockDim.x) {
+    const int i = idx / kDh, d = idx % kDh;
+    const float v = i < Lq ? dO[((long)b * Lq + i) * lddo + h * kDh + d] : 0.f;
+    sdO[i * kBwdLdD + d] = v;
+    bufA[d * kBwdLd + i] = v;
+  }
+  for (int idx = t; idx < Lk4 * kDh; idx += blockDim.x) {
+    const int j = idx / kDh, d = idx % kDh;
+    bufB[d * kBwdLd + j] = j < Lk ? a.V[((long)b * Lk + j) * a.ldv + h * kDh + d] : 0.f;
+  }
+  for (int idx = t; idx < Lq4 * Lk4; idx += blockDim.x) {
+    const int i = idx / Lk4, j = idx % Lk4;
+    sP[i * kBwdLd + j] = (i < Lq && j < Lk) ? a.probs[pbase + (long)i * Lk + j] : 0.f;
+  }
+  __syncthreads();
+  // dP (masked by the forward's dropout scale) into sdS
+  lds_tn_blocks(bufA, kBwdLd, bufB, kBwdLd, kDh, Lq4 / 4, Lk4 / 4, [&](int m0, int n0, float (&acc)[4][4]) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int i = m0 + r, j = n0 + c;
+        float v = 0.f;
+        if (i < Lq && j < Lk)
+          v = drop ? acc[r][c] * dasa_dropout_scale(a.p, a.seed, (uint64_t)(pbase + (long)i * Lk + j)) : acc[r][c];
+        sdS[i * kBwdLd + j] = v;
+      }
+  });
+  __syncthreads();
+  for (int i = t; i < Lq; i += blockDim.x) {
+    float s = 0.f;
+    for (int j = 0; j < Lk; ++j) s = fmaf(sP[i * kBwdLd + j], sdS[i * kBwdLd + j], s);
+    rowdot[i] = s;
+  }
+  __syncthreads();
+  for (int idx = t; idx < Lq4 * Lk4; idx += blockDim.x) {
+    const int i = idx / Lk4, j = idx % Lk4;
+    float g = 0.f;
+    if (i < Lq && j < Lk) g = sP[i * kBwdLd + j] * (sdS[i * kBwdLd + j] - rowdot[i]) * a.scale;
+    sdS[i * kBwdLd + j] = g;
+    sdST[j * kBwdLd + i] = g;
+  }
+  __syncthreads();
+  // the dropped probabilities feed dV; Q and K replace dO^T / V^T
+  if (drop)
+    for (int idx = t; idx < Lq * Lk; idx += blockDim.x) {
+      const int i = idx / Lk, j = idx % Lk;
+      sP[i * kBwdLd + j] *= dasa_dropout_scale(a.p, a.seed, (uint64_t)(pbase + idx));
+    }
+  for (int idx = t; idx < Lq4 * kDh; idx += blockDim.x) {
+    const int i = idx / kDh, d = idx % kDh;
+    bufA[i * kBwdLdD + d] = i < Lq ? a.Q[((long)b * Lq + i) * a.ldq + h * kDh + d] : 0.f;
+  }
+  for (int idx = t; idx < Lk4 * kDh; idx += blockDim.x) {
+    const int j = idx / kDh, d = idx % kDh;
+    bufB[j * kBwdLdD + d] = j < Lk ? a.K[((long)b * Lk + j) * a.ldk + h * kDh + d] : 0.f;
+  }
+  __syncthreads();
+  // dV[j][d] = sum_i Pd[i][j] dO[i][d]
+  lds_tn_blocks(sP, kBwdLd, sdO, kBwdLdD, Lq, Lk4 / 4, kDh / 4, [&](int m0, int n0, float (&acc)[4][4]) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (m0 + r < Lk)
+        *reinterpret_cast<float4*>(dV + ((long)b * Lk + m0 + r) * a.ldv + h * kDh + n0) =
+            make_float4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
+  });
+  // dQ[i][d] = sum_j dS[i][j] K[j][d]
+  lds_tn_blocks(sdST, kBwdLd, bufB, kBwdLdD, Lk, Lq4 / 4, kDh / 4, [&](int m0, int n0, float (&acc)[4][4]) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (m0 + r < Lq)
+        *reinterpret_cast<float4*>(dQ + ((long)b * Lq + m0 + r) * a.ldq + h * kDh + n0) =
+            make_float4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
+  });
+  // dK[j][d] = sum_i dS[i][j] Q[i][d]
+  lds_tn_blocks(sdS, kBwdLd, bufA, kBwdLdD, Lq, Lk4 / 4, kDh / 4, [&](int m0, int n0, float (&acc)[4][4]) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (m0 + r < Lk)
+        *reinterpret_cast<float4*>(dK + ((long)b * Lk + m0 + r) * a.ldk + h * kDh + n0) =
+            make_float4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
+  });
+}
+
 // ------------------------------------------------------------------ misc
 __global__ void reverse_valid_kernel(const float* __restrict__ x, const int* __restrict__ len, float* __restrict__ out,
                                      int B, int L, int H) {
@@ -572,19 +747,20 @@ __global__ __launch_bounds__(256) void adain_musigma_bwd_kernel(const float* __r
 extern "C" int dasa_version(void) { return 2; }
 extern "C" const char* dasa_build_info(void) { return "libdasa_hip gfx950 (CDNA4) fp32-MFMA v1"; }
 
-#define DASA_VPL_DISPATCH(N, KERNEL, GRID, ...)                                        \
-  do {                                                                                 \
-    const int vpl = ((N) / 4 + 63) / 64;                                               \
-    switch (vpl) {                                                                     \
-      case 1: hipLaunchKernelGGL(KERNEL<1>, GRID, dim3(256), 0, st, __VA_ARGS__); break; \
-      case 2: hipLaunchKernelGGL(KERNEL<2>, GRID, dim3(256), 0, st, __VA_ARGS__); break; \
-      case 3: hipLaunchKernelGGL(KERNEL<3>, GRID, dim3(256), 0, st, __VA_ARGS__); break; \
-      case 4: hipLaunchKernelGGL(KERNEL<4>, GRID, dim3(256), 0, st, __VA_ARGS__); break; \
-      case 8: case 5: case 6: case 7:                                                  \
-        hipLaunchKernelGGL(KERNEL<8>, GRID, dim3(256), 0, st, __VA_ARGS__); break;       \
-      default: return (int)hipErrorInvalidValue;                                       \
-    }                                                                                  \
+#define DASA_VPL_DISPATCH_B(N, KERNEL, GRID, BLOCK, ...)                                    \
+  do {                                                                                     \
+    const int vpl = ((N) / 4 + 63) / 64;                                                   \
+    switch (vpl) {                                                                         \
+      case 1: hipLaunchKernelGGL(KERNEL<1>, GRID, dim3(BLOCK), 0, st, __VA_ARGS__); break; \
+      case 2: hipLaunchKernelGGL(KERNEL<2>, GRID, dim3(BLOCK), 0, st, __VA_ARGS__); break; \
+      case 3: hipLaunchKernelGGL(KERNEL<3>, GRID, dim3(BLOCK), 0, st, __VA_ARGS__); break; \
+      case 4: hipLaunchKernelGGL(KERNEL<4>, GRID, dim3(BLOCK), 0, st, __VA_ARGS__); break; \
+      case 8: case 5: case 6: case 7:                                                      \
+        hipLaunchKernelGGL(KERNEL<8>, GRID, dim3(BLOCK), 0, st, __VA_ARGS__); break;       \
+      default: return (int)hipErrorInvalidValue;                                           \
+    }                                                                                      \
   } while (0)
+#define DASA_VPL_DISPATCH(N, KERNEL, GRID, ...) DASA_VPL_DISPATCH_B(N, KERNEL, GRID, 256, __VA_ARGS__)
 
 extern "C" int dasa_layernorm_fwd(const float* x, const float* res, const float* gamma, const float* beta, float* y,
                                   float* mean, float* rstd, float* xsum, int32_t M, int32_t N, float eps,
@@ -604,7 +780,9 @@ extern "C" int dasa_layernorm_bwd(const float* dy, const float* xsum, const floa
   if (M <= 0) return 0;
   if ((N & 3) || N > 8192) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
-  DASA_VPL_DISPATCH(N, ln_bwd_kernel, dim3(cdivi(M, 4)), dy, xsum, gamma, mean, rstd, dx, dgamma, dbeta, M, N);
+  const int colBlocks = (dgamma || dbeta) ? cdivi(N >> 2, 64) : 0;
+  DASA_VPL_DISPATCH_B(N, ln_bwd_kernel, dim3(cdivi(M, kLnBwdWaves) + colBlocks), 64 * kLnBwdWaves, dy, xsum, gamma,
+                      mean, rstd, dx, dgamma, dbeta, M, N);
   DASA_CHECK_LAUNCH();
   return 0;
 }
@@ -654,8 +832,13 @@ extern "C" int dasa_mha_bwd(const float* Q, int64_t ldq, const float* K, int64_t
   if (dh != kDh || Lk <= 0 || Lk > kMaxLk || !probs) return (int)hipErrorInvalidValue;
   MhaArgs a{Q, ldq, K, ldk, V, ldv, nullptr, nullptr, 0, const_cast<float*>(probs), B, heads, Lq, Lk, scale, drop_p,
             seed, nullptr};
-  hipLaunchKernelGGL(mha_bwd_kernel, dim3(B * heads), dim3(256), 0, (hipStream_t)stream, a, dout, (long)lddo, dQ, dK,
-                     dV);
+  const bool vec = ((ldq | ldk | ldv) & 3) == 0 && (((uintptr_t)dQ | (uintptr_t)dK | (uintptr_t)dV) & 15) == 0;
+  if (Lq <= kBwdMaxL && Lk <= kBwdMaxL && vec)
+    hipLaunchKernelGGL(mha_bwd_lds_kernel, dim3(B * heads), dim3(256), 0, (hipStream_t)stream, a, dout, (long)lddo, dQ,
+                       dK, dV);
+  else
+    hipLaunchKernelGGL(mha_bwd_kernel, dim3(B * heads), dim3(256), 0, (hipStream_t)stream, a, dout, (long)lddo, dQ, dK,
+                       dV);
   DASA_CHECK_LAUNCH();
   return 0;
 }

@@ -478,8 +478,8 @@ def layernorm_bwd(dy, saved, gamma, dgamma, dbeta):
     M, _ = _rows(xsum)
     N = xsum.shape[-1]
     dx = torch.empty_like(xsum)
-    _call("dasa_layernorm_bwd", "elementwise", _lib.lib().dasa_layernorm_bwd, _p(dy.contiguous()), _p(xsum), _p(gamma), _p(mean), _p(rstd), _p(dx),
-                                        _p(dgamma), _p(dbeta), M, N, _stream())
+    _call("dasa_layernorm_bwd", "layernorm_bwd", _lib.lib().dasa_layernorm_bwd, _p(dy.contiguous()), _p(xsum), _p(gamma), _p(mean), _p(rstd), _p(dx),
+                                        _p(dgamma), _p(dbeta), M, N, _stream(), nbytes=12.0 * M * N)
     return dx
 
 
@@ -515,9 +515,9 @@ def mha_bwd(Q, K, V, probs, dout, heads, scale, drop_p=0.0, seed=0):
     Lk = K.shape[1]
     Q, K, V, dout = Q.contiguous(), K.contiguous(), V.contiguous(), dout.contiguous()
     dQ, dK, dV = torch.empty_like(Q), torch.empty_like(K), torch.empty_like(V)
-    _call("dasa_mha_bwd", "elementwise", _lib.lib().dasa_mha_bwd, _p(Q), Hd, _p(K), Hd, _p(V), Hd, _p(probs), _p(dout), Hd, _p(dQ), _p(dK), _p(dV),
+    _call("dasa_mha_bwd", "mha_bwd", _lib.lib().dasa_mha_bwd, _p(Q), Hd, _p(K), Hd, _p(V), Hd, _p(probs), _p(dout), Hd, _p(dQ), _p(dK), _p(dV),
                                   B, heads, Lq, Lk, Hd // heads, float(scale), float(drop_p), int(seed) & (2**64 - 1),
-                                  _stream())
+                                  _stream(), flops=8.0 * B * Lq * Lk * Hd, nbytes=4.0 * B * (4 * Lq + 4 * Lk) * Hd)
     return dQ, dK, dV
 
 
@@ -788,14 +788,16 @@ def bilstm_bwd(whh_f, whh_b, lengths_i32, saved, dout, dh_n, dc_n, H):
 def bilstm_hprev(out, H):
     B, L, _ = out.shape
     hprev = torch.empty(2, B, L, H, dtype=torch.float32, device=out.device)
-    _call("dasa_bilstm_hprev", "elementwise", _lib.lib().dasa_bilstm_hprev, _p(out.contiguous()), _p(hprev), B, L, H, _stream())
+    _call("dasa_bilstm_hprev", "elementwise", _lib.lib().dasa_bilstm_hprev, _p(out.contiguous()), _p(hprev), B, L, H, _stream(),
+          nbytes=16.0 * B * L * H)
     return hprev
 
 
 def reverse_valid(x, lengths_i32):
     B, L, H = x.shape
     out = torch.empty_like(x)
-    _call("dasa_reverse_valid", "elementwise", _lib.lib().dasa_reverse_valid, _p(x.contiguous()), _p(lengths_i32), _p(out), B, L, H, _stream())
+    _call("dasa_reverse_valid", "elementwise", _lib.lib().dasa_reverse_valid, _p(x.contiguous()), _p(lengths_i32), _p(out), B, L, H, _stream(),
+          nbytes=8.0 * B * L * H)
     return out
 
 
@@ -807,8 +809,8 @@ def adain_musigma(content, style, out=None, eps=1e-5):
     if out is None:
         out = torch.empty(content.shape, dtype=torch.float32, device=content.device)
     _, ldo = _rows(out)
-    _call("dasa_adain_musigma_fwd", "elementwise", _lib.lib().dasa_adain_musigma_fwd, _p(content), ldc, _p(style), lds, _p(out), ldo, None, M, N, float(eps),
-                                            _stream())
+    _call("dasa_adain_musigma_fwd", "adain_musigma", _lib.lib().dasa_adain_musigma_fwd, _p(content), ldc, _p(style), lds, _p(out), ldo, None, M, N, float(eps),
+                                            _stream(), nbytes=12.0 * M * N)
     return out
 
 
@@ -820,7 +822,7 @@ def adain_musigma_bwd(content, style, dout, want_dcontent=True, want_dstyle=True
     N = content.shape[-1]
     dc = torch.empty(content.shape, dtype=torch.float32, device=content.device) if want_dcontent else None
     ds = torch.empty(style.shape, dtype=torch.float32, device=style.device) if want_dstyle else None
-    _call("dasa_adain_musigma_bwd", "elementwise", _lib.lib().dasa_adain_musigma_bwd, _p(content), ldc, _p(style),
+    _call("dasa_adain_musigma_bwd", "adain_musigma", _lib.lib().dasa_adain_musigma_bwd, _p(content), ldc, _p(style),
           lds, _p(dout), ldg, _p(dc), N, _p(ds), N, M, N, float(eps), _stream(), nbytes=4.0 * M * N * 5)
     return dc, ds
 

@@ -29,7 +29,9 @@ FAMILIES = {
     "cand_logit": ("hbm", "attn_split_fwd_kernel<2> / attn_fwd_kernel<16>"),
     "cand_logit_bwd": ("hbm", "attn_split_bwd_kernel<2> / attn_bwd_apply_kernel<16>"),
     "mha": ("mfma", "mha_fwd_kernel"),
+    "mha_bwd": ("mfma", "mha_bwd_kernel"),
     "layernorm": ("hbm", "ln_fwd_kernel"),
+    "layernorm_bwd": ("hbm", "ln_bwd_kernel"),
     "embed": ("hbm", "embed_kernel"),
     "ada_gate": ("hbm", "ada_gate_*_kernel"),
     "gather": ("hbm", "gather_rows_kernel"),
@@ -43,7 +45,9 @@ class _Recorder:
         self.items = []
         self.want_shapes = want_shapes
 
-    def summary(self, peak_tf=157.3, peak_gbs=8000.0):
+    def summary(self, peak_tf=157.3, peak_gbs=8000.0, pmc_workload="cfg2"):
+        """Per-family table + the dominant kernel's roofline. PMC values (HBM bytes, MFMA busy) are
+        attached only from the committed rocprofv3 --pmc summary of THIS workload (PMC_FILES)."""
         torch.cuda.synchronize()
         fam = defaultdict(lambda: {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0})
         shapes = defaultdict(lambda: [0, 0.0, 0.0])
@@ -87,13 +91,14 @@ class _Recorder:
             roof["frac_vs_fp32_peak"] = round(d["achieved"] / peak_tf, 4)
             roof["peak_note"] = ("fp32 GEMM as six exact bf16 products (bf16x6): peak = 2500 / 6 TFLOP/s "
                                  "fp32-equivalent; native fp32 MFMA peak 157.3")
-        pmc = _pmc_traffic()
+        pmc = _pmc_traffic(pmc_workload)
         if pmc is not None and dom_name in pmc["families"]:
             pf = pmc["families"][dom_name]
             roof["traffic"] = pf.get("hbm_bytes", pf.get("hbm_bytes_per_launch"))
             if pf.get("mfma_busy") is not None:
                 roof["mfma_busy"] = round(pf["mfma_busy"], 4)
-            roof["traffic_source"] = pmc["file"] + ": " + pmc["source"]
+            roof["traffic_source"] = (pmc["file"] + ": " + pmc["source"] + " (a separate rocprofv3 --pmc run of the "
+                                      "same workload; counters cannot be collected in the timed run)")
         for name, ent in kernels.items():          # PMC MFMA-busy / HBM bytes per family where measured
             pf = (pmc or {}).get("families", {}).get(name)
             if pf:
@@ -111,12 +116,14 @@ class _Recorder:
         return out
 
 
-def _pmc_traffic():
-    """Per-launch HBM bytes per kernel family from the committed rocprofv3 PMC passes
-    (tools/pmc_traffic.py -> profiles/pmc_traffic.json), or None."""
+def _pmc_traffic(workload):
+    """Per-launch HBM bytes / MFMA busy per kernel family from the committed rocprofv3 PMC passes of
+    `workload` (tools/pmc_summary.py -> PMC_FILES[workload]), or None when none was measured."""
     import json
     import os
-    rel = PMC_FILE
+    rel = PMC_FILES.get(workload)
+    if rel is None:
+        return None
     path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), rel)
     if not os.path.exists(path):
         return None
@@ -126,8 +133,10 @@ def _pmc_traffic():
     return d
 
 
-# the committed PMC summary the roofline's `traffic` / `mfma_busy` come from (tools/pmc_summary.py)
-PMC_FILE = "profiles/r02/prof_f/pmc.json"
+# the committed PMC summaries per workload the roofline's `traffic` / `mfma_busy` come from
+# (tools/prof_round.sh -> tools/pmc_summary.py); a workload without one reports no PMC values
+PMC_FILES = {"cfg2": "profiles/r03/pmc_cfg2.json", "cfg5": "profiles/r03/pmc_cfg5.json",
+             "cfg4": "profiles/r03/pmc_cfg4.json"}
 
 
 def active():

@@ -87,6 +87,14 @@ README_TRAIN_FLAGS = [
 ]
 
 
+# README "finetune" command line (README.md:104-116) without data / speaker / load paths: the train
+# flags with --d_update_add_layer True, lr 2e-6, batch 2 and no --use_lr_scheduler
+README_FINETUNE_FLAGS = [f for f in README_TRAIN_FLAGS if f != "--use_lr_scheduler"]
+for _flag, _val in (("--lr", "0.000002"), ("--batchSize", "2"), ("--iters", "30000"), ("--val_every", "1000")):
+    README_FINETUNE_FLAGS[README_FINETUNE_FLAGS.index(_flag) + 1] = _val
+README_FINETUNE_FLAGS += ["--d_update_add_layer", "True"]
+
+
 def make_parser():
     p = argparse.ArgumentParser(description="DASA agent_dg (MI355X build)")
     for flag, dest, typ, default in _FLAGS:
@@ -133,3 +141,8 @@ def parse(argv, make_dirs=False):
 def readme_train(extra=()):
     """args for the README training configuration (optionally overridden by `extra` flags)."""
     return parse(README_TRAIN_FLAGS + list(extra))
+
+
+def readme_finetune(extra=()):
+    """args for the README finetune configuration (configs[3] per rank)."""
+    return parse(README_FINETUNE_FLAGS + list(extra))

@@ -98,7 +98,8 @@ int dasa_f32_split3_bf16(const float* x, int64_t ldx, uint16_t* y, int32_t rows,
 int dasa_layernorm_fwd(const float* x, const float* res, const float* gamma, const float* beta,
                        float* y, float* mean, float* rstd, float* xsum, int32_t M, int32_t N, float eps,
                        float drop_p, uint64_t seed, void* stream);
-/* dx = dLN/d(xsum) (= grad of both x-after-dropout and res); dgamma/dbeta accumulated (+=). */
+/* dx = dLN/d(xsum) (= grad of both x-after-dropout and res); dgamma/dbeta accumulated (+=) by a
+ * fixed-order column reduction in the same launch (deterministic, no atomics). */
 int dasa_layernorm_bwd(const float* dy, const float* xsum, const float* gamma, const float* mean,
                        const float* rstd, float* dx, float* dgamma, float* dbeta,
                        int32_t M, int32_t N, void* stream);
@@ -118,7 +119,8 @@ int dasa_mha_fwd(const float* Q, int64_t ldq, const float* K, int64_t ldk, const
                  int32_t B, int32_t heads, int32_t Lq, int32_t Lk, int32_t dh, float scale,
                  float drop_p, uint64_t seed, void* stream);
 /* Backward; probs are the forward's saved pre-dropout softmax [B][heads][Lq][Lk], the dropout mask
- * is regenerated from (drop_p, seed). dQ/dK/dV are written with the ld of Q/K/V. */
+ * is regenerated from (drop_p, seed). dQ/dK/dV are written with the ld of Q/K/V. Lq, Lk <= 80 with
+ * 16-B aligned dQ/dK/dV take the LDS-staged form (no atomics); larger shapes the row-streaming one. */
 int dasa_mha_bwd(const float* Q, int64_t ldq, const float* K, int64_t ldk, const float* V, int64_t ldv,
                  const float* probs, const float* dout, int64_t lddo,
                  float* dQ, float* dK, float* dV, int32_t B, int32_t heads, int32_t Lq, int32_t Lk,
@@ -132,12 +134,13 @@ int dasa_mha_bwd(const float* Q, int64_t ldq, const float* K, int64_t ldk, const
  * its first 65536 32-bit words are arrival counters that must be ZERO on entry (calls leave them
  * zero) and the next 33 x 1024 are monotonic group-barrier counters (zero once), so a caller zeroes
  * the buffer once and reuses it on one stream for calls of any shape.
- * Two implementations, same results to fp32 rounding: row-split (a batch row's rows over workgroups,
- * online-softmax merge by the last workgroup) and, for N <= 80, D % 128 == 0 and B * D/128 <= 1024
- * (the decision step's B = 20), D-split (a batch row's 128-float column chunks over D/128 workgroups
- * that meet at a bounded group barrier; a timeout NaN-poisons the outputs and ORs 4 into the error
- * word, dasa_set_error_word). dasa_attn_set_mode: 0 = automatic (the default; DASA_ATTN_SPLIT=0 in
- * the environment starts in mode 1), 1 = row-split only. Host-only setting.                        */
+ * Implementations, same results to fp32 rounding: row-split (a batch row's rows over workgroups,
+ * online-softmax merge by the last workgroup); forward with N <= 36 and B >= 128, whole-row (one
+ * workgroup streams a batch row); backward with N <= 80, D % 128 == 0 and B * D/128 <= 1024 (the
+ * decision step's B = 20), D-split (a batch row's 128-float column chunks over D/128 workgroups that
+ * meet at a bounded group barrier; a timeout NaN-poisons the outputs and ORs 4 into the error word,
+ * dasa_set_error_word). dasa_attn_set_mode: 0 = automatic (the default; DASA_ATTN_SPLIT=0 in the
+ * environment starts in mode 1), 1 = row-split only. Host-only setting.                            */
 int64_t dasa_attn_workspace(int32_t B, int32_t N, int32_t D);
 int dasa_attn_set_mode(int32_t mode);
 int dasa_softdot_fwd(const float* q, const float* ctx, int64_t ldn, const uint8_t* mask,

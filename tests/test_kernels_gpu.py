@@ -129,6 +129,73 @@ def test_mha(dev, Lq, Lk):
     assert (out - ref).abs().max() < 1e-5
 
 
+@pytest.mark.parametrize("M,N", [(123, 768), (1, 768), (1700, 768), (37, 2048), (9, 12)])
+def test_layernorm_bwd_vs_autograd(dev, M, N):
+    """dx / dgamma / dbeta of dasa_layernorm_bwd vs torch autograd (fp32); dgamma / dbeta accumulate into what
+    the caller passes and are bit-identical run to run (fixed-order column reduction, no atomics)."""
+    from dasa_amd import ops
+    g = torch.Generator().manual_seed(M + N)
+    x, dy = _rand(M, N, g=g), _rand(M, N, g=g)
+    gm, bt = _rand(N, g=g), _rand(N, g=g)
+    xr, gr, br = x.clone().requires_grad_(), gm.clone().requires_grad_(), bt.clone().requires_grad_()
+    torch.nn.functional.layer_norm(xr, (N,), gr, br, 1e-12).backward(dy)
+    y, saved = ops.layernorm(x.to(dev), gm.to(dev), bt.to(dev), 1e-12, save=True)
+    outs = []
+    for _ in range(2):
+        dg0, db0 = torch.full((N,), 0.5, device=dev), torch.full((N,), -0.25, device=dev)
+        dx = ops.layernorm_bwd(dy.to(dev), saved, gm.to(dev), dg0, db0)
+        outs.append((dx.cpu(), dg0.cpu() - 0.5, db0.cpu() + 0.25))
+    dx, dg, db = outs[0]
+    tol = 2e-4 * max(1.0, M / 64)
+    assert (dx - xr.grad).abs().max() < 1e-3
+    assert (dg - gr.grad).abs().max() < tol
+    assert (db - br.grad).abs().max() < tol
+    assert all(torch.equal(a, b) for a, b in zip(outs[0], outs[1]))
+
+
+def _mha_ref(Q, K, V, m, h, scale, dscale=None):
+    B, Lq, Hd = Q.shape
+    Lk = K.shape[1]
+    q4 = Q.view(B, Lq, h, 64).permute(0, 2, 1, 3)
+    k4 = K.view(B, Lk, h, 64).permute(0, 2, 1, 3)
+    v4 = V.view(B, Lk, h, 64).permute(0, 2, 1, 3)
+    p = torch.softmax(q4 @ k4.transpose(-1, -2) * scale + m[:, None, None, :], -1)
+    if dscale is not None:
+        p = p * dscale
+    return (p @ v4).permute(0, 2, 1, 3).reshape(B, Lq, Hd)
+
+
+@pytest.mark.parametrize("Lq,Lk,p", [(80, 80, 0.0), (80, 36, 0.0), (36, 80, 0.0), (7, 13, 0.0), (5, 100, 0.0),
+                                     (80, 36, 0.1), (13, 7, 0.1)])
+def test_mha_bwd_vs_autograd(dev, Lq, Lk, p):
+    """dasa_mha_bwd (LDS-staged form for Lq, Lk <= 80; the row-streaming form above) vs torch autograd in
+    fp32. With dropout the forward's per-element scale is read back through an identity V (Lk <= 64):
+    out[b, i, h*64 + j] = P_dropped[b, h, i, j]."""
+    from dasa_amd import ops
+    g = torch.Generator().manual_seed(3 * Lq + Lk)
+    B, h, scale, seed = 2, 12, 1 / 8.0, 1234
+    Q, K, V = _rand(B, Lq, 768, g=g), _rand(B, Lk, 768, g=g), _rand(B, Lk, 768, g=g)
+    dO = _rand(B, Lq, 768, g=g)
+    m = torch.zeros(B, Lk)
+    m[1, Lk // 2:] = -10000.0
+    dscale = None
+    _, probs = ops.mha(Q.to(dev), K.to(dev), V.to(dev), m.to(dev), h, scale, p, seed, save_probs=True)
+    if p > 0:
+        eye = torch.zeros(B, Lk, 768)
+        for hh in range(h):
+            eye[:, torch.arange(Lk), hh * 64 + torch.arange(Lk)] = 1.0
+        pd = ops.mha(Q.to(dev), K.to(dev), eye.to(dev), m.to(dev), h, scale, p, seed).cpu()
+        pd = pd.view(B, Lq, h, 64)[..., :Lk].permute(0, 2, 1, 3)
+        pr = probs.cpu()
+        dscale = torch.where(pd != 0, torch.full_like(pd, 1 / (1 - p)), torch.zeros_like(pd))
+        assert (pd - pr * dscale).abs().max() < 1e-5          # the read-back mask is the forward's
+    qr, kr, vr = (t.clone().requires_grad_() for t in (Q, K, V))
+    _mha_ref(qr, kr, vr, m, h, scale, dscale).backward(dO)
+    dQ, dK, dV = (t.cpu() for t in ops.mha_bwd(Q.to(dev), K.to(dev), V.to(dev), probs, dO.to(dev), h, scale, p, seed))
+    for got, ref in ((dQ, qr.grad), (dK, kr.grad), (dV, vr.grad)):
+        assert (got - ref).abs().max() < 1e-4 * max(1.0, ref.abs().max().item())
+
+
 @pytest.fixture(params=["split", "rowsplit"])
 def attn_mode(request, dev):
     """Both attention implementations (include/dasa_hip.h dasa_attn_set_mode): the D-split form the
@@ -238,6 +305,43 @@ def test_softdot_fused_shapes(dev, B, N, D, ldn, attn_mode):
     assert (sc2.cpu().double() - s.detach()).abs().max() < 1e-4
 
 
+@pytest.mark.parametrize("N,D,ldn", [(36, 2176, 2176), (20, 2048, 2176), (7, 2176, 2176)])
+def test_attention_whole_row_forward(dev, N, D, ldn):
+    """The whole-row forward (B >= 128: one workgroup per batch row, rows streamed 12 at a time with an
+    online softmax) against fp64 host math: SoftDot with a mask at N = 36 / 20 / 7 (strided rows), and
+    the K=5 shift attention over the 36-view panorama."""
+    from dasa_amd import ops
+    ops.attn_set_mode(0)
+    g = torch.Generator().manual_seed(N + D)
+    B = 130
+    q = _rand(B, D, g=g, scale=0.05).double()
+    full = torch.rand(B, N, ldn, generator=g).double()
+    ctx = full[:, :, :D]
+    mask = torch.rand(B, N, generator=g) < 0.3
+    mask[:, 0] = False
+    s = torch.einsum("bnd,bd->bn", ctx, q)
+    p = torch.softmax(s.masked_fill(mask, -float("inf")), 1)
+    w = torch.einsum("bn,bnd->bd", p, ctx)
+    cd = full.float().to(dev)[:, :, :D]
+    sc, pr, wc = ops.softdot_fwd(q.float().to(dev), cd, mask.to(dev))
+    assert (sc.cpu().double() - s).abs().max() < 1e-4
+    assert (pr.cpu().double() - p).abs().max() < 1e-5
+    assert (wc.cpu().double() - w).abs().max() < 1e-4
+    if N != 36:
+        return
+    z = _rand(B, 5, g=g).double()
+    a = torch.softmax(s, 1)
+    a3 = a.view(B, 3, 12)
+    kern = torch.softmax(z, -1).unsqueeze(1)
+    a3 = torch.cat([a3[:, :, -2:], a3, a3[:, :, :2]], -1).transpose(0, 1)
+    a3 = torch.nn.functional.conv1d(a3, kern, groups=B).transpose(0, 1).reshape(B, 1, -1)
+    wref = torch.bmm(a3, ctx).squeeze(1)
+    wctx, attn, shifted, wsm = ops.shift_attn_fwd(q.float().to(dev), cd, z.float().to(dev))
+    assert (attn.cpu().double() - a).abs().max() < 1e-5
+    assert (shifted.cpu().double() - a3.squeeze(1)).abs().max() < 1e-5
+    assert (wctx.cpu().double() - wref).abs().max() < 1e-4
+
+
 def test_lstm_cell(dev):
     from dasa_amd import ops
     g = torch.Generator().manual_seed(17)
@@ -314,29 +418,32 @@ def _check_bilstm(dev, B, L):
 
 
 def test_attention_group_barrier_timeout_raises(dev):
-    """The D-split attention's group barrier is bounded like the persistent kernels': a timed-out wait
-    NaN-poisons the outputs and raises DasaError at the host's next check (bit 4 of the error word)."""
+    """The D-split attention backward's group barrier is bounded like the persistent kernels': a
+    timed-out wait NaN-poisons dq / dctx and raises DasaError at the host's next check (bit 4 of the
+    error word); the next call runs normally."""
     from dasa_amd import _lib, ops
     g = torch.Generator().manual_seed(5)
     B, D = 6, 2176
     q = (torch.randn(B, D, generator=g) * 0.05).to(dev)
     ctx = torch.rand(B, 36, D, generator=g).to(dev)
     z = torch.randn(B, 5, generator=g).to(dev)
+    gw = torch.randn(B, D, generator=g).to(dev)
     ops.attn_set_mode(0)
     ops.check_device_errors()
-    w0, *_ = ops.shift_attn_fwd(q, ctx, z)
-    assert torch.isfinite(w0).all()
+    _, attn, shifted, wsm = ops.shift_attn_fwd(q, ctx, z)
+    dq0, dc0, dz0 = ops.shift_attn_bwd(q, ctx, attn, shifted, wsm, gw)
+    assert torch.isfinite(dq0).all() and torch.isfinite(dc0).all()
     ops.force_persist_timeout(True)
     try:
-        w1, *_ = ops.shift_attn_fwd(q, ctx, z)
+        dq1, dc1, _ = ops.shift_attn_bwd(q, ctx, attn, shifted, wsm, gw)
         torch.cuda.synchronize()
     finally:
         ops.force_persist_timeout(False)
-    assert torch.isnan(w1).all()
+    assert torch.isnan(dq1).all() and torch.isnan(dc1).all()
     with pytest.raises(_lib.DasaError, match="attention: group barrier timed out"):
         ops.check_device_errors()
-    w2, *_ = ops.shift_attn_fwd(q, ctx, z)        # fresh workspace: back to normal
-    assert torch.equal(w2, w0)
+    dq2, dc2, dz2 = ops.shift_attn_bwd(q, ctx, attn, shifted, wsm, gw)
+    assert torch.equal(dq2, dq0) and torch.equal(dc2, dc0) and torch.equal(dz2, dz0)
     ops.check_device_errors()
 
 

@@ -4,9 +4,13 @@ One CSV per pass (gfx950 cannot collect FETCH_SIZE and WRITE_SIZE, or many SQ co
 Per family it reports the dispatch count, the mean of every counter per dispatch, and derived values:
   * hbm_read_bytes  = 2 x FETCH_SIZE x 1024 (MI355X_MICROARCH.md "HBM": FETCH_SIZE reads exactly half
                       the bytes of a wide coalesced stream on gfx950, in KB), hbm_write_bytes = WRITE_SIZE x 1024;
-  * mfma_busy       = SQ_VALU_MFMA_BUSY_CYCLES / (SIMDs x kernel cycles), kernel cycles = GRBM_GUI_ACTIVE / XCDs
-                      (rocprofv3 sums GRBM_GUI_ACTIVE over the 8 XCDs), SIMDs = 4 x 256 CUs;
-  * clock_ghz       = GRBM_GUI_ACTIVE / XCDs / dispatch duration (the DVFS-effective clock).
+  * per dispatch, from the counters and the duration of THAT dispatch in the same pass: kernel cycles
+    = GRBM_GUI_ACTIVE / XCDs (rocprofv3 sums it over the 8 XCDs) and clock = kernel cycles / duration.
+    For short dispatches the counter window outlasts the kernel (clock > F_MAX = 2.4 GHz, impossible on
+    MI355X): there the kernel's cycles are taken as duration x F_MAX, and the dispatch is left out of
+    the clock estimate (`window_inflated` = the fraction of such dispatches);
+  * mfma_busy       = sum SQ_VALU_MFMA_BUSY_CYCLES / (SIMDs x sum kernel cycles), SIMDs = 4 x 256 CUs;
+  * clock_ghz       = the duration-weighted mean clock of the dispatches whose window is not inflated.
 
     python tools/pmc_summary.py out.json pass1_counter_collection.csv [pass2 ...]
 """
@@ -20,6 +24,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from tools.prof_compare import family  # noqa: E402
 
 XCDS, SIMDS = 8, 1024
+F_MAX = 2.4   # GHz: MI355X peak engine clock (MI355X_MICROARCH.md)
 
 
 def _f(r, *names):
@@ -48,14 +53,29 @@ def load(paths):
 
 
 def summarise(disp):
-    fam = defaultdict(lambda: {"dispatches": defaultdict(int), "sums": defaultdict(float), "ns": []})
+    fam = defaultdict(lambda: {"dispatches": defaultdict(int), "sums": defaultdict(float), "ns": [],
+                               "busy": 0.0, "cyc": 0.0, "clk_w": 0.0, "clk_ns": 0.0, "clk_n": 0, "inflated": 0})
     for e in disp.values():
         f = fam[e["family"]]
-        for c, v in e["counters"].items():
-            f["sums"][c] += v
-            f["dispatches"][c] += 1
+        c = e["counters"]
+        for k, v in c.items():
+            f["sums"][k] += v
+            f["dispatches"][k] += 1
         if e["ns"]:
             f["ns"].append(e["ns"])
+        if "GRBM_GUI_ACTIVE" in c and e["ns"]:
+            cyc = c["GRBM_GUI_ACTIVE"] / XCDS
+            clk = cyc / e["ns"]
+            f["clk_n"] += 1
+            if clk > F_MAX:                     # the counter window outlasts the dispatch
+                f["inflated"] += 1
+                cyc = e["ns"] * F_MAX
+            else:
+                f["clk_w"] += clk * e["ns"]
+                f["clk_ns"] += e["ns"]
+            if "SQ_VALU_MFMA_BUSY_CYCLES" in c:
+                f["busy"] += c["SQ_VALU_MFMA_BUSY_CYCLES"]
+                f["cyc"] += cyc
     out = {}
     for name, f in fam.items():
         mean = {c: f["sums"][c] / f["dispatches"][c] for c in f["sums"]}
@@ -66,11 +86,12 @@ def summarise(disp):
             ent["hbm_write_bytes"] = 1024.0 * mean["WRITE_SIZE"]
         if "hbm_read_bytes" in ent and "hbm_write_bytes" in ent:
             ent["hbm_bytes"] = ent["hbm_read_bytes"] + ent["hbm_write_bytes"]
-        if "SQ_VALU_MFMA_BUSY_CYCLES" in f["sums"] and "GRBM_GUI_ACTIVE" in f["sums"]:
-            cyc = f["sums"]["GRBM_GUI_ACTIVE"] / XCDS
-            ent["mfma_busy"] = f["sums"]["SQ_VALU_MFMA_BUSY_CYCLES"] / (SIMDS * cyc) if cyc else None
-        if "GRBM_GUI_ACTIVE" in mean and f["ns"]:
-            ent["clock_ghz"] = mean["GRBM_GUI_ACTIVE"] / XCDS / (sum(f["ns"]) / len(f["ns"]))
+        if f["cyc"]:
+            ent["mfma_busy"] = f["busy"] / (SIMDS * f["cyc"])
+        if f["clk_ns"]:
+            ent["clock_ghz"] = f["clk_w"] / f["clk_ns"]
+        if f["clk_n"]:
+            ent["window_inflated"] = f["inflated"] / f["clk_n"]
         out[name] = ent
     return out
 
@@ -80,7 +101,8 @@ def main(out, *paths):
     json.dump({"source": "rocprofv3 --pmc passes: " + ", ".join(os.path.basename(p) for p in paths),
                "families": res}, open(out, "w"), indent=1, sort_keys=True)
     for k, v in sorted(res.items(), key=lambda kv: -kv[1]["dispatches"])[:20]:
-        extra = " ".join(f"{x}={v[x]:.4g}" for x in ("hbm_bytes", "mfma_busy", "clock_ghz") if v.get(x) is not None)
+        extra = " ".join(f"{x}={v[x]:.4g}" for x in ("hbm_bytes", "mfma_busy", "clock_ghz", "window_inflated")
+                         if v.get(x) is not None)
         print(f"{k:<40}{v['dispatches']:>8}  {extra}")
 
 

@@ -8,11 +8,11 @@
 #      correction, MFMA-busy fraction).
 # Every GPU step has its own time limit; a fault / abort / timeout ends the session.
 set -o pipefail
-TAG=${TAG:-r02}
+TAG=${TAG:-r03}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-BENCH_ARGS="--no-cfg5 --no-kbench --no-cpu-baseline --no-fwd --no-hoist --no-host-input"
+BENCH_ARGS="--no-cfg5 --no-cfg4 --no-kbench --no-cpu-baseline --no-fwd --no-hoist --no-host-input"
 
 step() {   # step <name> <timeout> <log> cmd...
   local name=$1 t=$2 log=$3; shift 3
@@ -33,16 +33,26 @@ find $OUT/stats \( -name "*kernel_trace*" -o -name "*.db" \) -delete 2>/dev/null
 STATS=$(find $OUT/stats -name "run_kernel_stats.csv" | head -1)
 [ -n "$STATS" ] && python tools/prof_compare.py "$STATS" $OUT/bench.json > $OUT/prof_compare.txt && cat $OUT/prof_compare.txt
 REGEX='gemm|mha|bilstm|attn_|ln_fwd|policy_head|ew4|gather|adain'
-n=0
-for CTRS in "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CU_CYCLES"; do
-  n=$((n + 1))
-  step pmc$n 300 $OUT/pmc${n}_run.log rocprofv3 --pmc $CTRS --kernel-include-regex "$REGEX" --output-format csv \
-    -d $OUT/pmc$n -o run -- python3 bench.py --steps 1 --warmup 0 --no-profile $BENCH_ARGS
+# PMC per workload (each summary is attached only to its own workload's bench numbers, dasa_amd/prof.py
+# PMC_FILES): cfg2 = the timed training iteration, cfg5 = configs[4]'s B=256 rollouts (bf16 + fp32),
+# cfg4 = the README finetune iteration
+for W in ${PMC_WORKLOADS:-cfg2 cfg5 cfg4}; do
+  case $W in
+    cfg2) WARGS="--steps 1 --warmup 0 --no-profile $BENCH_ARGS" ;;
+    *) WARGS="--only $W" ;;
+  esac
+  n=0
+  for CTRS in "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CU_CYCLES"; do
+    n=$((n + 1))
+    step pmc_${W}_$n 400 $OUT/pmc_${W}_${n}_run.log rocprofv3 --pmc $CTRS --kernel-include-regex "$REGEX" \
+      --output-format csv -d $OUT/pmc_${W}_$n -o run -- python3 bench.py $WARGS
+  done
+  P1=$(find $OUT/pmc_${W}_1 -name "*counter_collection.csv" | head -1)
+  P2=$(find $OUT/pmc_${W}_2 -name "*counter_collection.csv" | head -1)
+  P3=$(find $OUT/pmc_${W}_3 -name "*counter_collection.csv" | head -1)
+  python tools/pmc_summary.py $OUT/pmc_${W}.json $P1 $P2 $P3
+  find $OUT -name "*counter_collection.csv" -delete 2>/dev/null
 done
-P1=$(find $OUT/pmc1 -name "*counter_collection.csv" | head -1)
-P2=$(find $OUT/pmc2 -name "*counter_collection.csv" | head -1)
-P3=$(find $OUT/pmc3 -name "*counter_collection.csv" | head -1)
-python tools/pmc_summary.py $OUT/pmc.json $P1 $P2 $P3
 # the raw per-dispatch counter CSVs are large: keep the summaries only
 find $OUT -name "*counter_collection.csv" -delete 2>/dev/null
 find $OUT \( -name "*kernel_trace*" -o -name "*.db" \) -delete 2>/dev/null
