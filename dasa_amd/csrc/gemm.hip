@@ -28,6 +28,8 @@ struct GemmP {
   float alpha, beta;
   float* ws;
   int group_m;   // > 1: L2-grouped tile order (64-deep K kernels, non-stream-K)
+  unsigned* cnt; // split-K of gemm_f32_kernel: per-tile arrival counters (last arriver reduces in-kernel), or
+                 // null: partials to ws in [split][b][M][N] for splitk_reduce_kernel
 };
 
 __device__ __forceinline__ float apply_act(float v, int act) {
@@ -362,6 +364,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN) * KW) void gemm_f32_kern
   }
   if (t < ntiles) step(t, la0, lb0, la1, lb1);
 
+  const bool owner = KW == 1 || kgrp == 0;   // the waves holding the block's result after the K-split fold
   if (KW > 1) {   // fold the K-split wave groups into group 0 through LDS
     float* red = smem;
     __syncthreads();
@@ -375,18 +378,78 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN) * KW) void gemm_f32_kern
             red[((((kgrp - 1) * NWG + wt) * TM + i) * TN + j) * 1024 + r * 64 + lane] = acc[i][j][r];
     }
     __syncthreads();
-    if (kgrp > 0) return;
+    if (owner) {
 #pragma unroll
-    for (int g = 1; g < KW; ++g)
+      for (int g = 1; g < KW; ++g)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              acc[i][j][r] += red[((((g - 1) * NWG + wt) * TM + i) * TN + j) * 1024 + r * 64 + lane];
+    }
+  }
+  if (p.splitk > 1 && p.cnt) {
+    // in-kernel split-K reduction (no second launch): each split stores its raw tile write-through (sc1)
+    // into its own slab; the last split to take the tile's ticket sums the slabs in split order
+    // (deterministic; the same sums as splitk_reduce_kernel) and runs the fused epilogue
+    __shared__ int s_last;
+    constexpr int SLAB_B = BM * BN * 4, NO = 64 * NWG;
+    const int tile = (b * (int)gridDim.y + m0 / BM) * (int)gridDim.x + n0 / BN;
+    const int to = wt * 64 + lane;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(p.ws, 0, 0x7fffffff, 0x00020000);
+    const long tbase = (long)tile * p.splitk;
+    if (owner) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
-          for (int r = 0; r < 16; ++r)
-            acc[i][j][r] += red[((((g - 1) * NWG + wt) * TM + i) * TN + j) * 1024 + r * 64 + lane];
+          for (int r4 = 0; r4 < 4; ++r4) {
+            const int off = (int)((tbase + split) * SLAB_B) + (((i * TN + j) * 4 + r4) * NO + to) * 16;
+            const u32x4 u = {__float_as_uint(acc[i][j][4 * r4]), __float_as_uint(acc[i][j][4 * r4 + 1]),
+                             __float_as_uint(acc[i][j][4 * r4 + 2]), __float_as_uint(acc[i][j][4 * r4 + 3])};
+            __builtin_amdgcn_raw_buffer_store_b128(u, rs, off, 0, 16);   // sc1: write-through
+          }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+      s_last = __hip_atomic_fetch_add(p.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+               (unsigned)(p.splitk - 1);
+    __syncthreads();
+    if (!s_last) return;
+    if (threadIdx.x == 0) __hip_atomic_store(p.cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler-only: sc1 loads below the ticket
+    if (!owner) return;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    for (int s2 = 0; s2 < p.splitk; ++s2) {     // fixed order: deterministic whoever arrives last
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r4 = 0; r4 < 4; ++r4) {
+            const int off = (int)((tbase + s2) * SLAB_B) + (((i * TN + j) * 4 + r4) * NO + to) * 16;
+            const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);   // sc1
+            acc[i][j][4 * r4] += __uint_as_float(u.x);
+            acc[i][j][4 * r4 + 1] += __uint_as_float(u.y);
+            acc[i][j][4 * r4 + 2] += __uint_as_float(u.z);
+            acc[i][j][4 * r4 + 3] += __uint_as_float(u.w);
+          }
+    }
+    GemmP q = p;
+    q.splitk = 1;
+    store_tile<TM, TN, BM, BN>(q, acc, b, 0, m0, n0, wm, wn, lane);
+    return;
   }
-  store_tile<TM, TN, BM, BN>(p, acc, b, split, m0, n0, wm, wn, lane);
+  if (owner) store_tile<TM, TN, BM, BN>(p, acc, b, split, m0, n0, wm, wn, lane);
 }
 
 __global__ void splitk_reduce_kernel(GemmP p) {
@@ -1308,6 +1371,162 @@ void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
   store_tile_mf<16, TM, TN, BM, BN>(p, big, b, 0, m0, n0, wm, wn, lane);
 }
 
+// LDS-DMA form (form 14): the same tile, products, order and epilogue as form 8 (bitwise equal), but the
+// pre-split W planes go HBM/L2 -> LDS by global_load_lds_dwordx4 (no VGPR staging, no ds_write pass;
+// 1 KiB per wave-instruction = 64 consecutive 16-B units of the quad-major image), one K step ahead,
+// while A keeps form 8's two register stages (two steps ahead) and its in-register split. Stages are
+// separate __shared__ arrays and the K loop is unrolled by 2, so every stage index is a compile-time
+// constant: hipcc then sees that the fragment reads of one stage never alias the DMA in flight into
+// the other and does not drain vmcnt(0) in front of them. Per K step each wave first splits A(t+1) into
+// its LDS stage (no LDS store after a DMA issue in the step, so hipcc never drains vmcnt for a possible
+// DMA/ds_write overlap), then issues W(t+1)'s DMA, then A(t+2)'s loads; vector-memory loads complete in
+// issue order, so one vmcnt(2) (A(t+2) may stay in flight) + a raw s_barrier at the end of the step
+// publishes W(t+1) and A(t+1) (__syncthreads() would add a vmcnt(0): the DMA counts as an LDS store).
+template <int BM, int BN, int WAVES_M, int WAVES_N>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) __attribute__((amdgpu_waves_per_eu(1, 2)))
+void gemm_f32x6_glds_kernel(GemmP p, long plane) {
+  constexpr int NT = 64 * WAVES_M * WAVES_N, NWV = WAVES_M * WAVES_N;
+  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N, TM = WM / 16, TN = WN / 16;
+  constexpr int NA = BM * 4 / NT;                       // 16-B K quads of A per thread
+  constexpr int PA = BM * 4, PB = BN * 4;               // uint4 per plane image
+  constexpr int IW = 3 * PB / 64 / NWV;                 // W DMA wave-instructions per wave per stage
+  static_assert(NA * NT == BM * 4 && IW * 64 * NWV == 3 * PB, "tile quads must split evenly");
+  __shared__ uint4 sA0[3 * PA], sA1[3 * PA];
+  __shared__ uint4 sW0[3 * PB], sW1[3 * PB];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave / WAVES_N) * WM, wn = (wave % WAVES_N) * WN;
+  const int wgid = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+  int m0, n0;
+  if (p.group_m > 1) {
+    const int gm = p.group_m, per = gm * gridDim.x, grp = wgid / per;
+    const int rows = min(gm, (int)gridDim.y - grp * gm), r = wgid - grp * per;
+    m0 = (grp * gm + r % rows) * BM;
+    n0 = (r / rows) * BN;
+  } else {
+    n0 = (wgid % gridDim.x) * BN;
+    m0 = (wgid / gridDim.x) * BM;
+  }
+  const int b = blockIdx.z;
+  const float* A = p.A + (long)b * p.sA;
+  const unsigned short* W = reinterpret_cast<const unsigned short*>(p.B) + (long)b * p.sB;
+
+  floatx4 big[TM][TN], small[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      big[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+      small[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+
+  // W: per-lane source of unit u = (wave * IW + j) * 64 + lane of the [plane][q][row] image (rows past N
+  // re-read row N - 1; their outputs are dropped)
+  const unsigned short* wsrc[IW];
+#pragma unroll
+  for (int j = 0; j < IW; ++j) {
+    const int u = (wave * IW + j) * 64 + lane, pl = u / PB, rem = u % PB, q = rem / BN, row = rem % BN;
+    wsrc[j] = W + pl * plane + (long)min(n0 + row, p.N - 1) * p.ldb + 8 * q;
+  }
+  // A: unit u -> (row, quad) as form 8
+  struct AStage {
+    uint4 a[NA][2];
+    __device__ __forceinline__ static void unit(int u, int& row, int& q) {
+      q = (u >> 3) & 3;
+      row = (u & 7) + 8 * (u >> 5);
+    }
+    __device__ __forceinline__ void load(const GemmP& p, const float* A, int m0, int k0, int tid) {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        int row, q;
+        unit(tid + NT * i, row, q);
+        const float* src = A + (long)min(m0 + row, p.M - 1) * p.lda + k0 + 8 * q;
+        a[i][0] = *reinterpret_cast<const uint4*>(src);
+        a[i][1] = *reinterpret_cast<const uint4*>(src + 4);
+      }
+    }
+    __device__ __forceinline__ void store(uint4* S, int tid) const {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        int row, q;
+        unit(tid + NT * i, row, q);
+        uint4 h, m, l;
+        split3_quad(__builtin_bit_cast(float4, a[i][0]), __builtin_bit_cast(float4, a[i][1]), h, m, l);
+        S[0 * PA + q * BM + row] = h;
+        S[1 * PA + q * BM + row] = m;
+        S[2 * PA + q * BM + row] = l;
+      }
+    }
+  } stg, stg2;
+
+  const int nk = p.K / 32;
+#define X6G_DMA(S, K0)                                                                                      \
+  {                                                                                                         \
+    _Pragma("unroll") for (int j = 0; j < IW; ++j) __builtin_amdgcn_global_load_lds(                        \
+        (const void*)(wsrc[j] + (K0)), (__attribute__((address_space(3))) void*)((S) + (wave * IW + j) * 64), \
+        16, 0, 0);                                                                                          \
+  }
+#define X6G_COMPUTE(SA, SW)                                                                                 \
+  {                                                                                                         \
+    const int q = lane >> 4;                                                                                \
+    bf16x8_t bf[3][TN];                                                                                     \
+    _Pragma("unroll") for (int pl = 0; pl < 3; ++pl) _Pragma("unroll") for (int j = 0; j < TN; ++j) bf[pl][j] = \
+        __builtin_bit_cast(bf16x8_t, SW[pl * PB + q * BN + wn + 16 * j + (lane & 15)]);                      \
+    _Pragma("unroll") for (int i = 0; i < TM; ++i) {                                                        \
+      bf16x8_t af[3];                                                                                       \
+      _Pragma("unroll") for (int pl = 0; pl < 3; ++pl) af[pl] =                                             \
+          __builtin_bit_cast(bf16x8_t, SA[pl * PA + q * BM + wm + 16 * i + (lane & 15)]);                    \
+      _Pragma("unroll") for (int j = 0; j < TN; ++j) {                                                      \
+        floatx4& sm = small[i][j];                                                                          \
+        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bf[1][j], sm, 0, 0, 0);                          \
+        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[2][j], sm, 0, 0, 0);                          \
+        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2], bf[0][j], sm, 0, 0, 0);                          \
+        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[1][j], sm, 0, 0, 0);                          \
+        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bf[0][j], sm, 0, 0, 0);                          \
+        big[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[0][j], big[i][j], 0, 0, 0);           \
+      }                                                                                                     \
+    }                                                                                                       \
+  }
+// hipcc's waitcnt pass reads s_waitcnt builtins (not inline asm): vmcnt(2) lgkmcnt(0) = 0x72 on gfx9
+// (vmcnt[3:0], expcnt[6:4] = 7: no wait, lgkmcnt[11:8]); the s_barrier is inline asm with a memory
+// clobber so no LDS access moves across it
+  static_assert(2 * NA == 2, "the waitcnt immediate below encodes vmcnt(2)");
+#define X6G_STEP(XA, YA, SA, SAN, SW, SWN, T)                                                               \
+  {                                                                                                         \
+    YA.store(SAN, tid);             /* A(t+1), split; its stage was last read by compute(t-1) */            \
+    __builtin_amdgcn_sched_barrier(0); /* keep the LDS stores ahead of the DMA issue */                     \
+    X6G_DMA(SWN, 32 * min((T) + 1, nk - 1)); /* unconditional (clamped re-read) */                          \
+    XA.load(p, A, m0, 32 * min((T) + 2, nk - 1), tid);                                                      \
+    __builtin_amdgcn_sched_barrier(0); /* every load of the step issued before its MFMAs */                 \
+    X6G_COMPUTE(SA, SW);                                                                                    \
+    __builtin_amdgcn_sched_barrier(0); /* the wait for W(t+1) / A(t+1) only after the MFMAs */              \
+    __builtin_amdgcn_s_waitcnt(0x72);                                                                       \
+    asm volatile("s_barrier" ::: "memory");                                                                 \
+  }
+  // prologue: W tile 0 -> stage 0, A tile 0 split into stage 0, A tile 1 in registers
+  stg.load(p, A, m0, 0, tid);
+  stg2.load(p, A, m0, 32 * min(1, nk - 1), tid);
+  stg.store(sA0, tid);
+  X6G_DMA(sW0, 0);
+  __builtin_amdgcn_s_waitcnt(0x70);   // vmcnt(0) lgkmcnt(0)
+  asm volatile("s_barrier" ::: "memory");
+  // step t stores A(t+1) (held in YA) and loads A(t+2) into XA: the sets alternate
+  for (int t = 0; t < nk; t += 2) {
+    X6G_STEP(stg, stg2, sA0, sA1, sW0, sW1, t);
+    if (t + 1 >= nk) break;
+    X6G_STEP(stg2, stg, sA1, sA0, sW1, sW0, t + 1);
+  }
+#undef X6G_STEP
+#undef X6G_COMPUTE
+#undef X6G_DMA
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA into LDS outlives the workgroup
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) big[i][j] += small[i][j];
+  store_tile_mf<16, TM, TN, BM, BN>(p, big, b, 0, m0, n0, wm, wn, lane);
+}
+
 // x [rows][ldx] fp32 -> y planes [3][rows][cols] bf16 (plane stride rows * cols), x = hi + mid + lo.
 __global__ void split3_bf16_kernel(const float* __restrict__ x, long ldx, uint4* __restrict__ y, int rows, int cols) {
   const int cq = cols / 8;
@@ -1693,7 +1912,12 @@ static Plan make_plan(const dasa_gemm_desc* d) {
   // tiles at four workgroups per CU on mid-size long-K problems (no quantisation tail).
   const bool nt64 = d->opA == 0 && d->opB == 1 && K % 64 == 0 && M > 32;
   int sk_occ = 1;
-  if (nt64 && t64 >= 2048) pl.cfg = N >= 2048 ? 27 : 25;
+  // Short GEMMs (33..192 rows, < 160 64x64 tiles: the B = 2 finetune's language / LXRT projections) are
+  // bound by one CU's fp32 MFMA rate on too few tiles: 32x64 tiles, K split to ~240 (K <= 1024) or ~480
+  // workgroups (profiles/r03/gemm_split_probe.txt: 160x768x768 18.8 -> 9.8 us, 160x768x3072 28 -> 18 us).
+  const bool short_m = M > 32 && M <= 192 && batch == 1 && t64 < 160;
+  if (short_m) pl.cfg = 5;
+  else if (nt64 && t64 >= 2048) pl.cfg = N >= 2048 ? 27 : 25;
   else if (nt64 && K >= 1536 && t64 >= 128) { pl.cfg = 34; sk_occ = 4; }
   else if (M <= 32) pl.cfg = 5;
   else if (d->opA == 1 && K >= 8192 && t64 >= 256) pl.cfg = 8;   // weight grads over many rows
@@ -1710,7 +1934,13 @@ static Plan make_plan(const dasa_gemm_desc* d) {
   const int bm = kCfgs[pl.cfg].bm, bn = kCfgs[pl.cfg].bn;
   const long blocks = tiles(bm, bn);
   int splitk = 1;
-  if (M <= 32) {
+  if (short_m) {
+    if (blocks < 128) {
+      splitk = (int)cdiv(K <= 1024 ? 240 : 480, blocks);
+      const int maxs = std::min(8, K / 128);
+      splitk = std::max(1, std::min(splitk, maxs));
+    }
+  } else if (M <= 32) {
     if (blocks < 160 && K >= 512) {
       splitk = (int)cdiv(256, blocks);
       const int maxs = K / 256;  // keep >= 8 K-tiles per split
@@ -1728,7 +1958,9 @@ static Plan make_plan(const dasa_gemm_desc* d) {
   splitk = K > 0 ? (int)cdiv(K, kchunk) : 1;
   pl.splitk = splitk;
   pl.kchunk = kchunk;
-  pl.ws = splitk > 1 ? (int64_t)splitk * batch * M * N * (int64_t)sizeof(float) : 0;
+  // split partials: [split][b][M][N] for splitk_reduce_kernel, or one BM x BN slab per (tile, split) for the
+  // in-kernel reduction of gemm_f32_kernel (padded tiles): room for either
+  pl.ws = splitk > 1 ? (int64_t)splitk * batch * (cdiv(M, bm) * bm) * (cdiv(N, bn) * bn) * (int64_t)sizeof(float) : 0;
   pl.sk_grid = pl.sk_dp = pl.sk_tiles = pl.sk_ipt = 0;
   // 64-deep K tiles over many row panels walk 4-panel groups (profiles/r01e/gemm_k32_group.txt: +1-5%
   // on the 12800-row language GEMMs, never slower)
@@ -1939,9 +2171,21 @@ extern "C" int dasa_gemm_f32(const dasa_gemm_desc* d, void* ws, int64_t ws_bytes
   int rc;
   const int kalign = pl.cfg >= 21 ? 63 : 31;
   const bool glds_ok = vec && d->opA == 0 && d->opB == 1 && (K & kalign) == 0 && (pl.kchunk & kalign) == 0;
+  // gemm_f32_kernel forms (tile configs 0..14, and every config without float4 operands) reduce their
+  // K splits in-kernel when the workspace holds one tile slab per (tile, split)
+  p.cnt = nullptr;
+  const int ecfg = (kCfgs[pl.cfg].glds && !glds_ok) ? glds_fallback(pl.cfg) : pl.cfg;   // launch_cfg's choice
+  const bool tile_kernel = !vec || !kCfgs[ecfg].glds;
+  if (pl.splitk > 1 && tile_kernel && ws != nullptr) {
+    const int bm = vec ? kCfgs[ecfg].bm : (kCfgs[ecfg].bm == 32 ? 32 : 64);
+    const int bn = vec ? kCfgs[ecfg].bn : (kCfgs[ecfg].bm == 32 ? 128 : 64);
+    const long ntile = cdiv(M, bm) * cdiv(N, bn) * batch;
+    const int64_t slabs = ntile * pl.splitk * (int64_t)bm * bn * 4;
+    if (ntile <= kCntWords && slabs < 0x7fffffffLL && kCntBytes + slabs <= ws_bytes) p.cnt = (unsigned*)ws;
+  }
   rc = launch_cfg(pl.cfg, vec, glds_ok, p, pl.sk_grid > 0 ? &sk : nullptr, d->opA, d->opB, st);
   if (rc) return rc;
-  if (pl.splitk > 1) {
+  if (pl.splitk > 1 && p.cnt == nullptr) {
     const long total = (long)batch * M * N;
     int grid = (int)cdiv(total, 256);
     if (grid > 4096) grid = 4096;
@@ -2104,6 +2348,7 @@ extern "C" int dasa_gemm_f32x6_ws(const dasa_gemm_desc* d, int64_t plane, void* 
     case 12: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<256, 128, 4, 2, true, 2, false, 1>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
     case 13: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<256, 128, 4, 2, true, 2, false, 2>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
     case 9: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true, 3>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
+    case 14: hipLaunchKernelGGL((gemm_f32x6_glds_kernel<128, 128, 4, 2>), grid, dim3(512), 0, st, p, (long)plane); break;
     default: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
   }
   DASA_CHECK_LAUNCH();

@@ -24,6 +24,24 @@ def test_linear(dev, M, N, K):
     assert (y - ref).abs().max().item() < 1e-4 * max(1.0, ref.abs().max().item())
 
 
+@pytest.mark.parametrize("M,N,K,opB", [(160, 768, 768, 1), (72, 768, 3072, 0), (100, 3072, 768, 1), (33, 70, 1000, 0)])
+def test_gemm_short_m_split(dev, M, N, K, opB):
+    """The short-GEMM plan (33..192 rows, split-K over 32x64 tiles + the fixed-order reduce) with the fused
+    bias / GELU epilogue and beta accumulation, forward (NT) and dX (NN) layouts, vs fp64."""
+    from dasa_amd import ops
+    g = torch.Generator().manual_seed(M + N + K)
+    x = _rand(M, K, g=g)
+    W = _rand(N, K, g=g, scale=0.05) if opB else _rand(K, N, g=g, scale=0.05)
+    b, c0 = _rand(N, g=g), _rand(M, N, g=g)
+    Wn = W.double() if opB else W.double().t()
+    z = x.double() @ Wn.t() + b.double()
+    ref = (z * 0.5 * (1 + torch.erf(z / math.sqrt(2))) + c0.double()).float()
+    y = c0.clone().to(dev)
+    ops.gemm(x.to(dev), W.to(dev), y, M=M, N=N, K=K, opB=opB, lda=K, ldb=K if opB else N, ldc=N, bias=b.to(dev),
+             act="gelu", beta=1.0)
+    assert (y.cpu() - ref).abs().max().item() < 1e-4 * max(1.0, ref.abs().max().item())
+
+
 @pytest.mark.parametrize("act", ["relu", "gelu", "tanh", "sigmoid"])
 def test_linear_act_and_gate(dev, act):
     from dasa_amd import ops
@@ -740,10 +758,12 @@ def test_gemm_f32x6(dev, M, N, K):
     ops.gemm(Ad, Wd, out_nat, M=M, N=N, K=K, lda=K + 8, ldb=K, ldc=N, bias=bias.to(dev))
     err_nat = (out_nat.cpu().double() - ref).abs().max().item()
     try:
-        for cfg in range(10):
+        outs = {}
+        for cfg in list(range(10)) + [14]:
             lib.dasa_gemm_force_config((1 << 21) + cfg)
             y = torch.empty(M, N, device=dev)
             ops.gemm_f32x6(Ad, planes, y, M=M, N=N, K=K, lda=K + 8, ldc=N, bias=bias.to(dev))
+            outs[cfg] = y.cpu()
             err = (y.cpu().double() - ref).abs().max().item()
             # forms 0, 3, 4, 5, 7, 8 keep the five small products in their own accumulator (default 8):
             # at most the native fp32 kernel's error; forms 1, 2, 6 (one accumulator, sweep-only) within 3x
@@ -753,6 +773,8 @@ def test_gemm_f32x6(dev, M, N, K):
                            aux=aux.to(dev), ld_aux=N, colscale=cs.to(dev), beta=0.5)
             want = torch.sigmoid(ref) * aux.double() * cs.double() + 0.5 * c0.double()
             assert (y2.cpu().double() - want).abs().max().item() < 1e-5, cfg
+        # form 14 (W planes by LDS-DMA) runs form 8's products in form 8's order: bitwise equal
+        assert torch.equal(outs[14], outs[8])
     finally:
         lib.dasa_gemm_force_config(-1)
 
