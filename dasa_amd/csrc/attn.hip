@@ -754,6 +754,136 @@ __global__ __launch_bounds__(256) void attn_split_bwd_kernel(SplitArgs a) {
   if (t < kCW) reinterpret_cast<float4*>(a.dq + (long)b * a.D)[g * kCW + t] = o;
 }
 
+// ---- two-launch D-split forward (small batches: the decision step at B = 20) ------------------------
+// A cross-workgroup hand-off inside one launch costs 3-5 us on MI355X (MI355X_MICROARCH.md price table,
+// "handoff-flag", "fanin"); a dependent kernel boundary 1.5-1.9 us ("boundary"). So the forward splits
+// the row dots from the softmax at a launch boundary instead of a group barrier, and both launches put
+// B x G workgroups (G = D / 128: 340 for the panorama at B = 20) on the chip, each holding a 128-float
+// column chunk of all N rows (thread: row lane rl = t / 32, float4 column t % 32, rows rl + 8 i).
+//   launch 1  partial row dots over the chunk -> part[b][g][n] (plain stores; the boundary publishes)
+//   launch 2  the chunk's rows re-read (L2 / MALL: launch 1 just streamed them) with their loads issued
+//             BEFORE the G x N partial loads, so the two round trips overlap; the G partials of each row
+//             summed in fixed order g = 0..G-1 (every workgroup of b gets bitwise the same scores),
+//             masked softmax, the ring shift, and the chunk of wctx = sum_n w_n ctx_n; workgroup g = 0
+//             also writes scores / probs / shifted / the tap weights.
+// Measured (profiles/r03/attn_forms_b.txt, B = 20): shift attention 8.55 us vs 8.89 for the row-split
+// kernel's in-launch merge, so the shift forward takes it; the instruction SoftDot (N = 80) ran 12.1 vs
+// 10.8 us and keeps the row-split kernel (reachable in attention mode 2, where the tests run it with
+// masks, strided rows and N up to 80).
+template <int RPT>
+__global__ __launch_bounds__(256) void attn_split_dots_kernel(SplitArgs a) {
+  const int g = blockIdx.x, b = blockIdx.y, t = threadIdx.x, col = t & 31, rl = t >> 5;
+  const int N = a.N, c = g * kCW + col;
+  const float* base = a.ctx + (long)b * N * a.ldn;
+  float4 x[RPT];
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) x[i] = reinterpret_cast<const float4*>(base + (long)min(rl + 8 * i, N - 1) * a.ldn)[c];
+  const float4 qv = reinterpret_cast<const float4*>(a.q + (long)b * a.D)[c];
+  float v[RPT];
+  chunk_row_dots<RPT>(x, qv, v);
+  if (col == 0) {
+    float* part = a.ws + (a.o_part >> 2) + ((long)b * a.G + g) * N;
+#pragma unroll
+    for (int i = 0; i < RPT; ++i)
+      if (rl + 8 * i < N) part[rl + 8 * i] = v[i];
+  }
+}
+
+template <int RPT>
+__global__ __launch_bounds__(256) void attn_split_ctx_kernel(SplitArgs a) {
+  __shared__ float4 red4[8][kCW];
+  __shared__ float spart[256 * kMaxPartPerThread];
+  __shared__ float ssc[kSplitMaxN], sw[kSplitMaxN], swk[kMaxK + 1];
+  const int g = blockIdx.x, b = blockIdx.y, t = threadIdx.x, lane = t & 63, col = t & 31, rl = t >> 5;
+  const int N = a.N, G = a.G, c = g * kCW + col;
+  const bool shift = a.shift_logits != nullptr;
+  const float* base = a.ctx + (long)b * N * a.ldn;
+  float4 x[RPT];
+  if (a.wctx) {
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) x[i] = reinterpret_cast<const float4*>(base + (long)min(rl + 8 * i, N - 1) * a.ldn)[c];
+  }
+  gather_partials(ws_rsrc(a.ws), a.o_part + (int)((long)b * G * N) * 4, G * N, spart);
+  if (t < 64) {
+    float s0 = 0.f, s1 = 0.f;
+    for (int gg = 0; gg < G; ++gg) {   // fixed order: the same scores in all G workgroups of b
+      if (lane < N) s0 += spart[gg * N + lane];
+      if (lane + 64 < N) s1 += spart[gg * N + lane + 64];
+    }
+    const bool v0 = lane < N, v1 = lane + 64 < N;
+    const bool m0 = v0 && a.mask && a.mask[(long)b * N + lane], m1 = v1 && a.mask && a.mask[(long)b * N + lane + 64];
+    const float z0 = (v0 && !m0) ? s0 : -INFINITY, z1 = (v1 && !m1) ? s1 : -INFINITY;
+    const float M = wave_max(fmaxf(z0, z1));
+    const float e0 = z0 == -INFINITY ? 0.f : __expf(z0 - M), e1 = z1 == -INFINITY ? 0.f : __expf(z1 - M);
+    const float inv = 1.f / wave_sum(e0 + e1);
+    const float p0 = e0 * inv, p1 = e1 * inv;
+    if (v0) ssc[lane] = p0;
+    if (v1) ssc[lane + 64] = p1;
+    if (g == 0) {
+      if (v0 && a.scores) a.scores[(long)b * N + lane] = s0;
+      if (v1 && a.scores) a.scores[(long)b * N + lane + 64] = s1;
+      if (v0 && a.probs) a.probs[(long)b * N + lane] = p0;
+      if (v1 && a.probs) a.probs[(long)b * N + lane + 64] = p1;
+    }
+    if (shift) {   // N = 36: three rings of 12, the K-tap circular correlation within each (model.py:337-344)
+      shift_taps(a.shift_logits + (long)b * a.K, a.K, swk, lane);
+      lds_wave_sync();
+      const int P = a.K / 2;
+      float wgt = 0.f;
+      if (v0) {
+        const int r = lane / 12, j = lane % 12;
+        for (int k = 0; k < a.K; ++k) {
+          int jj = j + k - P;
+          jj = ((jj % 12) + 12) % 12;
+          wgt = fmaf(swk[k], ssc[r * 12 + jj], wgt);
+        }
+        sw[lane] = wgt;
+      }
+      if (g == 0) {
+        if (v0 && a.shifted) a.shifted[(long)b * N + lane] = wgt;
+        if (a.wsm && lane < a.K) a.wsm[(long)b * a.K + lane] = swk[lane];
+      }
+    } else {
+      if (v0) sw[lane] = p0;
+      if (v1) sw[lane + 64] = p1;
+    }
+  }
+  if (!a.wctx) return;   // uniform: no workgroup reaches the barrier below
+  __syncthreads();
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const int r = rl + 8 * i;
+    fma4(r < N ? sw[r] : 0.f, x[i], acc);
+  }
+  const float4 o = rowlane_sum(acc, red4);
+  if (t < kCW) reinterpret_cast<float4*>(a.wctx + (long)b * a.D)[g * kCW + t] = o;
+}
+
+// Scores only (the candidate logits, model.py:276-280): one workgroup per (row, batch row), the row's
+// float4 loads all in flight at once, a block reduction, no hand-off of any kind. B < 128 only: 2.5 vs
+// 3.9 us at B = 20, but 9.4 vs 6.9 us at B = 256 (profiles/r03/attn_forms_b.txt).
+__global__ __launch_bounds__(256) void attn_dot_rows_kernel(const float* __restrict__ q, const float* __restrict__ ctx,
+                                                            long ldn, float* __restrict__ scores, int N, int D) {
+  __shared__ float red[4];
+  const int n = blockIdx.x, b = blockIdx.y, t = threadIdx.x, D4 = D >> 2;
+  const float4* row = reinterpret_cast<const float4*>(ctx + ((long)b * N + n) * ldn);
+  const float4* qv = reinterpret_cast<const float4*>(q + (long)b * D);
+  float4 x[4], y[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int k = min(t + 256 * i, D4 - 1);
+    x[i] = row[k];
+    y[i] = qv[k];
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (t + 256 * i < D4) s += dot4(x[i], y[i]);
+  s = block_sum<4>(s, red);
+  if (t == 0) scores[(long)b * N + n] = s;
+}
+
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 inline int block_threads(int D) {
@@ -817,7 +947,8 @@ int launch_bwd(BwdArgs a, int B, void* ws, hipStream_t st) {
 
 // D-split eligibility (0 = use the row-split kernels): rows per thread for N <= 80, D a multiple of 128,
 // and B x G within kSplitMaxWG when the call needs the group barrier. DASA_ATTN_SPLIT=0 disables it.
-int g_attn_mode = -1;   // dasa_attn_set_mode: 0 automatic, 1 row-split only; -1 = not read from the env yet
+int g_attn_mode = -1;   // dasa_attn_set_mode: 0 automatic, 1 row-split only, 2 = 0 + the two-launch
+                        // D-split forward for SoftDot too (tests); -1 = not read from the env yet
 
 int split_rpt(int B, int N, int D, bool spin) {
   if (g_attn_mode < 0) {
@@ -841,7 +972,7 @@ void split_launch(const SplitArgs& a, int B, hipStream_t st) {
 constexpr int kRowsMinB = 128;
 bool rows_ok(int B, int N, int D) {
   if (g_attn_mode < 0) split_rpt(1, 1, 128, false);   // reads DASA_ATTN_SPLIT once
-  return g_attn_mode == 0 && B >= kRowsMinB && N >= 1 && N <= 36 && D <= 4 * 576;
+  return g_attn_mode != 1 && B >= kRowsMinB && N >= 1 && N <= 36 && D <= 4 * 576;
 }
 
 int launch_rows(const FwdArgs& a, int B, hipStream_t st) {
@@ -870,6 +1001,35 @@ int launch_split_bwd(SplitArgs a, int rpt, int B, void* ws, hipStream_t st) {
   return 0;
 }
 
+// Two-launch D-split forward: mode 0, fewer than kRowsMinB batch rows (the whole-row form takes the large
+// batches), N <= 80, D a multiple of 128 (G <= 32 chunks).
+bool split2_ok(int B, int N, int D) {
+  if (g_attn_mode < 0) split_rpt(1, 1, 128, false);
+  return g_attn_mode != 1 && B < kRowsMinB && N >= 1 && N <= kSplitMaxN && D % (4 * kCW) == 0 && D <= 4 * kCW * 32;
+}
+
+template <int RPT>
+void split2_launch(const SplitArgs& a, int B, hipStream_t st) {
+  hipLaunchKernelGGL(attn_split_dots_kernel<RPT>, dim3(a.G, B), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(attn_split_ctx_kernel<RPT>, dim3(a.G, B), dim3(256), 0, st, a);
+}
+
+int launch_split2_fwd(const FwdArgs& f, int B, void* ws, hipStream_t st) {
+  WsLayout L = ws_layout(ws, B, f.N, f.D);
+  SplitArgs a{};
+  a.q = f.q; a.ctx = f.ctx; a.ldn = f.ldn; a.mask = f.mask; a.shift_logits = f.shift_logits; a.K = f.K;
+  a.scores = f.scores; a.probs = f.probs; a.shifted = f.shifted; a.wsm = f.wsm; a.wctx = f.wctx;
+  a.N = f.N; a.D = f.D; a.G = f.D / (4 * kCW); a.ws = (float*)ws; a.o_part = L.o_part;
+  const int rpt = f.N <= 16 ? 2 : (f.N <= 40 ? 5 : 10);
+  switch (rpt) {
+    case 2: split2_launch<2>(a, B, st); break;
+    case 5: split2_launch<5>(a, B, st); break;
+    default: split2_launch<10>(a, B, st); break;
+  }
+  DASA_CHECK_LAUNCH();
+  return 0;
+}
+
 bool bad_common(const float* q, const float* ctx, int64_t ldn, int B, int N, int D, const void* ws) {
   return N > kMaxN || D > 4096 || B > kMaxB || ws_layout(nullptr, B, N, D).bytes >= (1L << 31) || (D & 3) || (ldn & 3) || ldn < D || !aligned16(q) || !aligned16(ctx) || !ws ||
          !aligned16(ws);
@@ -878,7 +1038,7 @@ bool bad_common(const float* q, const float* ctx, int64_t ldn, int B, int N, int
 }  // namespace
 
 extern "C" int dasa_attn_set_mode(int32_t mode) {
-  if (mode != 0 && mode != 1) return (int)hipErrorInvalidValue;
+  if (mode < 0 || mode > 2) return (int)hipErrorInvalidValue;
   g_attn_mode = mode;
   return 0;
 }
@@ -895,6 +1055,13 @@ extern "C" int dasa_softdot_fwd(const float* q, const float* ctx, int64_t ldn, c
   if (bad_common(q, ctx, ldn, B, N, D, ws) || (wctx && !aligned16(wctx))) return (int)hipErrorInvalidValue;
   FwdArgs a{q, ctx, (long)ldn, mask, nullptr, 0, scores, probs, nullptr, nullptr, wctx, N, D};
   if ((probs || wctx) && rows_ok(B, N, D)) return launch_rows(a, B, (hipStream_t)stream);
+  if (!probs && !wctx && scores && g_attn_mode != 1 && B < kRowsMinB && D <= 4 * 1024) {   // scores only
+    hipLaunchKernelGGL(attn_dot_rows_kernel, dim3(N, B), dim3(256), 0, (hipStream_t)stream, q, ctx, (long)ldn,
+                       scores, N, D);
+    DASA_CHECK_LAUNCH();
+    return 0;
+  }
+  if (g_attn_mode == 2 && split2_ok(B, N, D)) return launch_split2_fwd(a, B, ws, (hipStream_t)stream);
   return launch_fwd<16>(a, B, ws, (hipStream_t)stream);
 }
 
@@ -926,6 +1093,7 @@ extern "C" int dasa_shift_attn_fwd(const float* q, const float* ctx, int64_t ldn
     return (int)hipErrorInvalidValue;
   FwdArgs a{q, ctx, (long)ldn, nullptr, shift_logits, K, nullptr, attn, shifted, wsm, wctx, N, D};
   if (rows_ok(B, N, D)) return launch_rows(a, B, (hipStream_t)stream);
+  if (split2_ok(B, N, D)) return launch_split2_fwd(a, B, ws, (hipStream_t)stream);
   return launch_fwd<12>(a, B, ws, (hipStream_t)stream);
 }
 

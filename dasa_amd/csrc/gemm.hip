@@ -1371,162 +1371,6 @@ void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
   store_tile_mf<16, TM, TN, BM, BN>(p, big, b, 0, m0, n0, wm, wn, lane);
 }
 
-// LDS-DMA form (form 14): the same tile, products, order and epilogue as form 8 (bitwise equal), but the
-// pre-split W planes go HBM/L2 -> LDS by global_load_lds_dwordx4 (no VGPR staging, no ds_write pass;
-// 1 KiB per wave-instruction = 64 consecutive 16-B units of the quad-major image), one K step ahead,
-// while A keeps form 8's two register stages (two steps ahead) and its in-register split. Stages are
-// separate __shared__ arrays and the K loop is unrolled by 2, so every stage index is a compile-time
-// constant: hipcc then sees that the fragment reads of one stage never alias the DMA in flight into
-// the other and does not drain vmcnt(0) in front of them. Per K step each wave first splits A(t+1) into
-// its LDS stage (no LDS store after a DMA issue in the step, so hipcc never drains vmcnt for a possible
-// DMA/ds_write overlap), then issues W(t+1)'s DMA, then A(t+2)'s loads; vector-memory loads complete in
-// issue order, so one vmcnt(2) (A(t+2) may stay in flight) + a raw s_barrier at the end of the step
-// publishes W(t+1) and A(t+1) (__syncthreads() would add a vmcnt(0): the DMA counts as an LDS store).
-template <int BM, int BN, int WAVES_M, int WAVES_N>
-__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) __attribute__((amdgpu_waves_per_eu(1, 2)))
-void gemm_f32x6_glds_kernel(GemmP p, long plane) {
-  constexpr int NT = 64 * WAVES_M * WAVES_N, NWV = WAVES_M * WAVES_N;
-  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N, TM = WM / 16, TN = WN / 16;
-  constexpr int NA = BM * 4 / NT;                       // 16-B K quads of A per thread
-  constexpr int PA = BM * 4, PB = BN * 4;               // uint4 per plane image
-  constexpr int IW = 3 * PB / 64 / NWV;                 // W DMA wave-instructions per wave per stage
-  static_assert(NA * NT == BM * 4 && IW * 64 * NWV == 3 * PB, "tile quads must split evenly");
-  __shared__ uint4 sA0[3 * PA], sA1[3 * PA];
-  __shared__ uint4 sW0[3 * PB], sW1[3 * PB];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = (wave / WAVES_N) * WM, wn = (wave % WAVES_N) * WN;
-  const int wgid = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
-  int m0, n0;
-  if (p.group_m > 1) {
-    const int gm = p.group_m, per = gm * gridDim.x, grp = wgid / per;
-    const int rows = min(gm, (int)gridDim.y - grp * gm), r = wgid - grp * per;
-    m0 = (grp * gm + r % rows) * BM;
-    n0 = (r / rows) * BN;
-  } else {
-    n0 = (wgid % gridDim.x) * BN;
-    m0 = (wgid / gridDim.x) * BM;
-  }
-  const int b = blockIdx.z;
-  const float* A = p.A + (long)b * p.sA;
-  const unsigned short* W = reinterpret_cast<const unsigned short*>(p.B) + (long)b * p.sB;
-
-  floatx4 big[TM][TN], small[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      big[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-      small[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-    }
-
-  // W: per-lane source of unit u = (wave * IW + j) * 64 + lane of the [plane][q][row] image (rows past N
-  // re-read row N - 1; their outputs are dropped)
-  const unsigned short* wsrc[IW];
-#pragma unroll
-  for (int j = 0; j < IW; ++j) {
-    const int u = (wave * IW + j) * 64 + lane, pl = u / PB, rem = u % PB, q = rem / BN, row = rem % BN;
-    wsrc[j] = W + pl * plane + (long)min(n0 + row, p.N - 1) * p.ldb + 8 * q;
-  }
-  // A: unit u -> (row, quad) as form 8
-  struct AStage {
-    uint4 a[NA][2];
-    __device__ __forceinline__ static void unit(int u, int& row, int& q) {
-      q = (u >> 3) & 3;
-      row = (u & 7) + 8 * (u >> 5);
-    }
-    __device__ __forceinline__ void load(const GemmP& p, const float* A, int m0, int k0, int tid) {
-#pragma unroll
-      for (int i = 0; i < NA; ++i) {
-        int row, q;
-        unit(tid + NT * i, row, q);
-        const float* src = A + (long)min(m0 + row, p.M - 1) * p.lda + k0 + 8 * q;
-        a[i][0] = *reinterpret_cast<const uint4*>(src);
-        a[i][1] = *reinterpret_cast<const uint4*>(src + 4);
-      }
-    }
-    __device__ __forceinline__ void store(uint4* S, int tid) const {
-#pragma unroll
-      for (int i = 0; i < NA; ++i) {
-        int row, q;
-        unit(tid + NT * i, row, q);
-        uint4 h, m, l;
-        split3_quad(__builtin_bit_cast(float4, a[i][0]), __builtin_bit_cast(float4, a[i][1]), h, m, l);
-        S[0 * PA + q * BM + row] = h;
-        S[1 * PA + q * BM + row] = m;
-        S[2 * PA + q * BM + row] = l;
-      }
-    }
-  } stg, stg2;
-
-  const int nk = p.K / 32;
-#define X6G_DMA(S, K0)                                                                                      \
-  {                                                                                                         \
-    _Pragma("unroll") for (int j = 0; j < IW; ++j) __builtin_amdgcn_global_load_lds(                        \
-        (const void*)(wsrc[j] + (K0)), (__attribute__((address_space(3))) void*)((S) + (wave * IW + j) * 64), \
-        16, 0, 0);                                                                                          \
-  }
-#define X6G_COMPUTE(SA, SW)                                                                                 \
-  {                                                                                                         \
-    const int q = lane >> 4;                                                                                \
-    bf16x8_t bf[3][TN];                                                                                     \
-    _Pragma("unroll") for (int pl = 0; pl < 3; ++pl) _Pragma("unroll") for (int j = 0; j < TN; ++j) bf[pl][j] = \
-        __builtin_bit_cast(bf16x8_t, SW[pl * PB + q * BN + wn + 16 * j + (lane & 15)]);                      \
-    _Pragma("unroll") for (int i = 0; i < TM; ++i) {                                                        \
-      bf16x8_t af[3];                                                                                       \
-      _Pragma("unroll") for (int pl = 0; pl < 3; ++pl) af[pl] =                                             \
-          __builtin_bit_cast(bf16x8_t, SA[pl * PA + q * BM + wm + 16 * i + (lane & 15)]);                    \
-      _Pragma("unroll") for (int j = 0; j < TN; ++j) {                                                      \
-        floatx4& sm = small[i][j];                                                                          \
-        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bf[1][j], sm, 0, 0, 0);                          \
-        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[2][j], sm, 0, 0, 0);                          \
-        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2], bf[0][j], sm, 0, 0, 0);                          \
-        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[1][j], sm, 0, 0, 0);                          \
-        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bf[0][j], sm, 0, 0, 0);                          \
-        big[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[0][j], big[i][j], 0, 0, 0);           \
-      }                                                                                                     \
-    }                                                                                                       \
-  }
-// hipcc's waitcnt pass reads s_waitcnt builtins (not inline asm): vmcnt(2) lgkmcnt(0) = 0x72 on gfx9
-// (vmcnt[3:0], expcnt[6:4] = 7: no wait, lgkmcnt[11:8]); the s_barrier is inline asm with a memory
-// clobber so no LDS access moves across it
-  static_assert(2 * NA == 2, "the waitcnt immediate below encodes vmcnt(2)");
-#define X6G_STEP(XA, YA, SA, SAN, SW, SWN, T)                                                               \
-  {                                                                                                         \
-    YA.store(SAN, tid);             /* A(t+1), split; its stage was last read by compute(t-1) */            \
-    __builtin_amdgcn_sched_barrier(0); /* keep the LDS stores ahead of the DMA issue */                     \
-    X6G_DMA(SWN, 32 * min((T) + 1, nk - 1)); /* unconditional (clamped re-read) */                          \
-    XA.load(p, A, m0, 32 * min((T) + 2, nk - 1), tid);                                                      \
-    __builtin_amdgcn_sched_barrier(0); /* every load of the step issued before its MFMAs */                 \
-    X6G_COMPUTE(SA, SW);                                                                                    \
-    __builtin_amdgcn_sched_barrier(0); /* the wait for W(t+1) / A(t+1) only after the MFMAs */              \
-    __builtin_amdgcn_s_waitcnt(0x72);                                                                       \
-    asm volatile("s_barrier" ::: "memory");                                                                 \
-  }
-  // prologue: W tile 0 -> stage 0, A tile 0 split into stage 0, A tile 1 in registers
-  stg.load(p, A, m0, 0, tid);
-  stg2.load(p, A, m0, 32 * min(1, nk - 1), tid);
-  stg.store(sA0, tid);
-  X6G_DMA(sW0, 0);
-  __builtin_amdgcn_s_waitcnt(0x70);   // vmcnt(0) lgkmcnt(0)
-  asm volatile("s_barrier" ::: "memory");
-  // step t stores A(t+1) (held in YA) and loads A(t+2) into XA: the sets alternate
-  for (int t = 0; t < nk; t += 2) {
-    X6G_STEP(stg, stg2, sA0, sA1, sW0, sW1, t);
-    if (t + 1 >= nk) break;
-    X6G_STEP(stg2, stg, sA1, sA0, sW1, sW0, t + 1);
-  }
-#undef X6G_STEP
-#undef X6G_COMPUTE
-#undef X6G_DMA
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA into LDS outlives the workgroup
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) big[i][j] += small[i][j];
-  store_tile_mf<16, TM, TN, BM, BN>(p, big, b, 0, m0, n0, wm, wn, lane);
-}
-
 // x [rows][ldx] fp32 -> y planes [3][rows][cols] bf16 (plane stride rows * cols), x = hi + mid + lo.
 __global__ void split3_bf16_kernel(const float* __restrict__ x, long ldx, uint4* __restrict__ y, int rows, int cols) {
   const int cq = cols / 8;
@@ -2348,7 +2192,7 @@ extern "C" int dasa_gemm_f32x6_ws(const dasa_gemm_desc* d, int64_t plane, void* 
     case 12: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<256, 128, 4, 2, true, 2, false, 1>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
     case 13: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<256, 128, 4, 2, true, 2, false, 2>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
     case 9: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true, 3>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
-    case 14: hipLaunchKernelGGL((gemm_f32x6_glds_kernel<128, 128, 4, 2>), grid, dim3(512), 0, st, p, (long)plane); break;
+    case 15: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, false, 2>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
     default: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
   }
   DASA_CHECK_LAUNCH();

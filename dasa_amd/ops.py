@@ -566,7 +566,8 @@ _AWS = {}
 
 
 def attn_set_mode(mode):
-    """Attention implementation (include/dasa_hip.h dasa_attn_set_mode): 0 automatic, 1 row-split only."""
+    """Attention implementation (include/dasa_hip.h dasa_attn_set_mode): 0 automatic, 1 row-split only,
+    2 automatic + the two-launch D-split SoftDot forward (tests)."""
     _lib.check(_lib.lib().dasa_attn_set_mode(int(mode)), "dasa_attn_set_mode")
 
 
