@@ -98,7 +98,7 @@ class StepGraphs:
         return e
 
     def run(self, key, fn, inputs):
-        """fn(*inputs) -> tuple of tensors, forward-only; returns fresh copies of its outputs."""
+        """fn(*inputs) -> tuple of tensors (or None), forward-only; returns fresh copies of its outputs."""
         if prof.active() or _NESTED[0]:
             # per-launch HIP-event profiling (bench.py's kernel table) runs eagerly; inside an enclosing
             # region's capture this region becomes part of that graph
@@ -119,7 +119,7 @@ class StepGraphs:
             s.copy_(x)
         e.graph.replay()
         self.replays += 1
-        return tuple(o.clone() for o in e.static_out)
+        return tuple(o.clone() if o is not None else None for o in e.static_out)
 
     def clear(self):
         self.entries.clear()

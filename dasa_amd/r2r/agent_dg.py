@@ -595,11 +595,13 @@ class Seq2SeqAgent(BaseAgent):
             if args.depth_drop:
                 df_t = self._noise_mult(df_t, noise)
         img = f_t if args.use_dropout_vision else all_img_feats
+        wv = bool(args.ctx_v)   # vision_outputs are consumed only with --ctx_v (agent_dg.py:807-808)
         if T == 1:
-            ctx, en_ht, en_ct, _, ctx_v = self.encoder(seq, mask=seq_mask, lengths=lens_dev, f_t_all=img)
+            ctx, en_ht, en_ct, _, ctx_v = self.encoder(seq, mask=seq_mask, lengths=lens_dev, f_t_all=img,
+                                                       want_vision=wv)
         else:
             ctx, en_ht, en_ct, _, ctx_v = self.encoder(seq.repeat(T, 1), mask=seq_mask.repeat(T, 1),
-                                                       lengths=lens_dev.repeat(T), f_t_all=img)
+                                                       lengths=lens_dev.repeat(T), f_t_all=img, want_vision=wv)
         if args.ctx_v:
             df_t = df_t + ctx_v
         out = []

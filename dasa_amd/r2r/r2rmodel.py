@@ -205,13 +205,17 @@ class DicEncoder(nn.Module):
         return None
 
     # ------------------------------------------------------------------ forward
-    def forward(self, inputs, mask, lengths, f_t_all=None):
+    def forward(self, inputs, mask, lengths, f_t_all=None, want_vision=True):
+        """r2rmodel.py:2204-2365. want_vision (extra, default on): False returns None for vision_outputs
+        and skips the last LXRT layer's vision branch, their only producer (the agent passes
+        args.ctx_v: with it off the reference discards them, agent_dg.py:807)."""
         B = inputs.size(0)
         L = mask.size(1)
         att_mask = ~mask
         ids = inputs[:, :L]
         text = self._language(ids, att_mask)
-        embeds, pooled, vision_outputs = self.bert(ids, None, att_mask, img_feats=f_t_all, text_embeds=text)
+        embeds, _, vision_outputs = self.bert(ids, None, att_mask, img_feats=f_t_all, text_embeds=text,
+                                              want_visn=want_vision or args.ctx_v, want_pooled=False)
         if not self.config.update_add_layer:
             embeds = embeds.detach()
         lens = lengths if torch.is_tensor(lengths) else torch.as_tensor(list(lengths))

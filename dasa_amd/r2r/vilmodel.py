@@ -295,7 +295,14 @@ class LXRTXLayer(nn.Module):
         visn = self.visn_output(self.visn_inter(visn_input), visn_input)
         return lang, visn
 
-    def forward(self, lang_feats, lang_attention_mask, visn_feats, visn_attention_mask):
+    def forward(self, lang_feats, lang_attention_mask, visn_feats, visn_attention_mask, want_visn=True):
+        if not want_visn:
+            # the caller drops this layer's vision output (the last layer when ctx_v is off: DicEncoder's
+            # vision_outputs are unused, agent_dg.py:807): its vision branch has no consumer, so only the
+            # language branch runs — the language output is the same either way
+            la = self.visual_attention(lang_feats, visn_feats, ctx_att_mask=visn_attention_mask)
+            la = self.lang_self_att(la, lang_attention_mask)[0]
+            return self.lang_output(self.lang_inter(la), la), None
         if torch.is_grad_enabled() or not _TWO_STREAMS:
             la, va = self.cross_att(lang_feats, lang_attention_mask, visn_feats, visn_attention_mask)
             la, va = self.self_att(la, lang_attention_mask, va, visn_attention_mask)
@@ -369,8 +376,9 @@ class DicModel(nn.Module):
                 m.weight.data.fill_(1.0)
                 m.bias.data.zero_()
 
-    def _vl_stack(self, text_embeds, ext, img_feats):
-        """VisionEncoder + the vl LXRT layers (vilmodel.py:1383-1406)."""
+    def _vl_stack(self, text_embeds, ext, img_feats, want_visn=True):
+        """VisionEncoder + the vl LXRT layers (vilmodel.py:1383-1406). want_visn=False: the last
+        layer's vision branch is skipped and None returned for the vision output."""
         B, V = img_feats.shape[0], img_feats.shape[1]
         img_mask = torch.zeros(B, 1, 1, V, dtype=torch.float32, device=img_feats.device)
         lang = text_embeds
@@ -378,8 +386,9 @@ class DicModel(nn.Module):
         if args.d_v_layers > 0:
             for layer in self.vlayer:
                 visn = layer(visn, img_mask)[0]
-        for layer in self.addlayer:
-            lang, visn = layer(lang, ext, visn, img_mask)
+        last = len(self.addlayer) - 1
+        for i, layer in enumerate(self.addlayer):
+            lang, visn = layer(lang, ext, visn, img_mask, want_visn=want_visn or i < last)
         return lang, visn
 
     def language(self, input_ids, ext_mask):
@@ -390,7 +399,10 @@ class DicModel(nn.Module):
         return x
 
     def forward(self, input_ids, token_type_ids=None, attention_mask=None, position_ids=None, head_mask=None,
-                img_feats=None, text_embeds=None):
+                img_feats=None, text_embeds=None, want_visn=True, want_pooled=True):
+        """want_visn / want_pooled (extras, default on = the reference's outputs): False returns None for the
+        vision output / pooled output and skips the work that only they need (the last LXRT layer's
+        vision branch; the pooler). The language output is unchanged."""
         if head_mask is not None or position_ids is not None:
             raise NotImplementedError("head_mask / position_ids")
         if attention_mask is None:
@@ -410,15 +422,17 @@ class DicModel(nn.Module):
                     mods = [self.vision_encoder, self.addlayer] + ([self.vlayer] if args.d_v_layers > 0 else [])
                     self._graphs = graph.StepGraphs(mods)
                 key = (tuple(text_embeds.shape), tuple(ext.shape), tuple(img_feats.shape), img_feats.stride(),
-                       self.training)
-                lang, visn = self._graphs.run(key, self._vl_stack, (text_embeds, ext, img_feats))
+                       self.training, bool(want_visn))
+                lang, visn = self._graphs.run(key, lambda t, e, f: self._vl_stack(t, e, f, want_visn),
+                                              (text_embeds, ext, img_feats))
             else:
                 with torch.set_grad_enabled(vl_grad):
-                    lang, visn = self._vl_stack(text_embeds, ext, img_feats)
+                    lang, visn = self._vl_stack(text_embeds, ext, img_feats, want_visn)
             if not self.update_add_layer:
-                lang, visn = lang.detach(), visn.detach()
+                lang = lang.detach()
+                visn = visn.detach() if visn is not None else None
             sequence_output = lang
         else:
             sequence_output = text_embeds
-        pooled_output = self.pooler(sequence_output)
+        pooled_output = self.pooler(sequence_output) if want_pooled else None
         return sequence_output, pooled_output, visn_output if img_feats is None else visn

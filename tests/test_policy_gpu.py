@@ -491,6 +491,50 @@ def test_vl_stack_graph_replay(R, dev, monkeypatch):
         assert (x - c).abs().mean().item() < 2.0 * (c - ref_v).abs().mean().item() + 1e-3
 
 
+def test_vl_stack_without_vision_output(R, dev, monkeypatch):
+    """want_visn=False / want_pooled=False (the agent without --ctx_v: the reference discards
+    vision_outputs, agent_dg.py:807-808, and DicEncoder never reads the pooler): the last LXRT layer's
+    vision branch and the pooler are skipped, the language output is bitwise the full stack's — eager,
+    graph-replayed, and under autograd (update_add_layer), where the skipped branch's parameters get
+    no gradient exactly as in the reference, whose loss never reaches them."""
+    from dasa_amd import graph
+    vilmodel = R[4]
+    cfg = vilmodel.BertConfig()
+    cfg.img_feature_dim, cfg.img_feature_type = 2176, ""
+    cfg.update_lang_bert, cfg.update_add_layer, cfg.vl_layers, cfg.la_layers = False, False, 3, 1
+    m = init_params(vilmodel.DicModel(cfg), 78).to(dev)
+    g = torch.Generator().manual_seed(6)
+    B, L = 4, 9
+    ids = torch.randint(1, 1000, (B, L), generator=g).to(dev)
+    att = torch.ones(B, L, dtype=torch.long, device=dev)
+    att[2, 5:] = 0
+    img = torch.rand(B, 36, 2176, generator=g).to(dev)
+    m.eval()
+    with torch.no_grad():
+        for enabled in (False, True):
+            monkeypatch.setattr(graph, "ENABLED", enabled)
+            full_l, pooled, full_v = m(ids, None, att, img_feats=img)
+            for _ in range(2):
+                lang, p2, v2 = m(ids, None, att, img_feats=img, want_visn=False, want_pooled=False)
+                assert torch.equal(lang, full_l) and p2 is None and v2 is None
+            assert pooled is not None and full_v is not None
+    cfg.update_add_layer = True
+    m2 = init_params(vilmodel.DicModel(cfg), 78).to(dev)
+    m2.update_add_layer = True
+    m2.eval()
+    monkeypatch.setattr(graph, "ENABLED", False)
+    lang, _, _ = m2(ids, None, att, img_feats=img, want_visn=False)
+    lang.square().sum().backward()
+    last = m2.addlayer[-1]
+    for name, p in last.named_parameters():
+        if name.startswith(("visn_self_att", "visn_inter", "visn_output")):
+            assert p.grad is None, name
+        elif name.startswith(("lang_", "visual_attention")):
+            assert p.grad is not None, name
+    full_l2, _, _ = m2(ids, None, att, img_feats=img)
+    assert torch.equal(lang.detach(), full_l2.detach())
+
+
 def test_adain_musigma_vs_reference(R, dev):
     """mu/sigma AdaIN (adaIn_type default, model.py:1822-1840): forward and content/style gradients
     against the reference's golden."""

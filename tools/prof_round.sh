@@ -25,6 +25,7 @@ step() {   # step <name> <timeout> <log> cmd...
   return 0
 }
 
+if [ "${SKIP_STATS:-0}" != "1" ]; then   # SKIP_STATS=1: the PMC passes only (a second session)
 step bench 400 $OUT/bench.log python bench.py --steps 3 --warmup 1 --shapes 40 $BENCH_ARGS
 grep '^{"metric"' $OUT/bench.log | tail -1 > $OUT/bench.json
 step stats 500 $OUT/stats_run.log rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- \
@@ -32,6 +33,7 @@ step stats 500 $OUT/stats_run.log rocprofv3 --kernel-trace --stats --output-form
 find $OUT/stats \( -name "*kernel_trace*" -o -name "*.db" \) -delete 2>/dev/null
 STATS=$(find $OUT/stats -name "run_kernel_stats.csv" | head -1)
 [ -n "$STATS" ] && python tools/prof_compare.py "$STATS" $OUT/bench.json > $OUT/prof_compare.txt && cat $OUT/prof_compare.txt
+fi
 REGEX='gemm|mha|bilstm|attn_|ln_fwd|policy_head|ew4|gather|adain'
 # PMC per workload (each summary is attached only to its own workload's bench numbers, dasa_amd/prof.py
 # PMC_FILES): cfg2 = the timed training iteration, cfg5 = configs[4]'s B=256 rollouts (bf16 + fp32),
