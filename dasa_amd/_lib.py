@@ -49,6 +49,7 @@ SIGNATURES = {
     "dasa_gemm_f32x6_ws": (i32, [C.POINTER(GemmDesc), i64, vp, i64, vp]),
     "dasa_f32_split3_bf16": (i32, [vp, i64, vp, i32, i32, vp]),
     "dasa_gemm_force_config": (i32, [i32]),
+    "dasa_gemm_x6_set_balance": (i32, [i32]),
     "dasa_gemm_skinny_tune": (i32, [i32, i32]),
     "dasa_layernorm_fwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, f32, f32, u64, vp]),
     "dasa_layernorm_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp]),

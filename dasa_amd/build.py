@@ -15,7 +15,7 @@ OUT = os.path.join(HERE, "libdasa_hip.so")
 BUILD_DIR = os.path.join(HERE, "build")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
-FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-pass-failed",
+FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-pass-failed", "-Wno-inline-asm",
          "-I" + os.path.join(os.path.dirname(HERE), "include")]
 
 

@@ -1371,6 +1371,146 @@ void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
   store_tile_mf<16, TM, TN, BM, BN>(p, big, b, 0, m0, n0, wm, wn, lane);
 }
 
+// All-DMA form (form 16, sweeps only: 0.80-0.90x form 8 on the 12800-row shapes, profiles/r03/
+// x6_dma_form.txt): the same tile, products, product order and epilogue as form 8 (bitwise equal),
+// but nothing is staged through VGPRs or written by ds_write: A (fp32) and the pre-split W planes go
+// HBM/L2 -> LDS by global_load_lds_dwordx4 into a ring of three K stages, two steps ahead, and A is split
+// into its bf16 planes at fragment-read time (each A fragment is split by the WAVES_N waves that read it:
+// 2x form 8's split VALU, issued between MFMAs instead of in a split + ds_write phase that every wave of
+// a SIMD reaches at once after the barrier). Per K step a wave waits for its own stage-t DMAs (counted
+// vmcnt: stage t+1's stay in flight), one s_barrier (every wave's stage-t DMAs landed; every wave is
+// done reading stage t-1, whose slot stage t+2 now refills), issues stage t+2, and computes stage t.
+// LDS images (16-B units, DMA lane-linear: one wave-instruction = 64 consecutive units):
+//   A  [q2][row], q2 = the 4-float K group (0..7) -> the 16x16x32 fragment of lane l (row l & 15, K
+//      quad q = l >> 4) is units (2q, row), (2q + 1, row): 16 lanes read 16 consecutive units
+//   W  [plane][q][row] as form 8
+// The DMAs and the waits on them are inline asm, outside hipcc's waitcnt model: its LDS-DMA tracking
+// merged the ring's stages at the loop header and drained vmcnt(0) before reading the stage that had
+// landed (profiles/r03/x6_dma_form.txt). The asm barrier / waits carry "memory" clobbers, so no LDS
+// read of a stage moves across the barrier that frees or publishes it; M0 (the DMA's LDS base) is set
+// in the same asm statement and is used by nothing else in this kernel.
+__device__ __forceinline__ void lds_dma16(const void* g, unsigned lds_base) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(lds_base)
+               : "memory", "m0");
+}
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(size_t)((const __attribute__((address_space(3))) void*)p);
+}
+
+template <int BM, int BN, int WAVES_M, int WAVES_N>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) __attribute__((amdgpu_waves_per_eu(1, 2)))
+void gemm_f32x6_dma_kernel(GemmP p, long plane) {
+  constexpr int NWV = WAVES_M * WAVES_N;
+  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N, TM = WM / 16, TN = WN / 16;
+  constexpr int UA = BM * 8, PB = BN * 4;                    // 16-B units: A stage, one W plane
+  constexpr int IA = UA / 64 / NWV, IW = 3 * PB / 64 / NWV;  // DMA wave-instructions per wave per stage
+  static_assert(IA * 64 * NWV == UA && IW * 64 * NWV == 3 * PB, "stage units must split evenly");
+  static_assert(IA + IW == 5, "the vmcnt immediates below are written for 5 DMAs per wave per stage");
+  __shared__ uint4 sA[3][UA];
+  __shared__ uint4 sW[3][3 * PB];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave / WAVES_N) * WM, wn = (wave % WAVES_N) * WN;
+  const int wgid = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+  int m0, n0;
+  if (p.group_m > 1) {
+    const int gm = p.group_m, per = gm * gridDim.x, grp = wgid / per;
+    const int rows = min(gm, (int)gridDim.y - grp * gm), r = wgid - grp * per;
+    m0 = (grp * gm + r % rows) * BM;
+    n0 = (r / rows) * BN;
+  } else {
+    n0 = (wgid % gridDim.x) * BN;
+    m0 = (wgid / gridDim.x) * BM;
+  }
+  const int b = blockIdx.z;
+  const float* A = p.A + (long)b * p.sA;
+  const unsigned short* W = reinterpret_cast<const unsigned short*>(p.B) + (long)b * p.sB;
+
+  floatx4 big[TM][TN], small[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      big[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+      small[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+
+  // per-lane DMA sources (rows past M / N re-read the last row; their outputs are dropped) and the
+  // wave-uniform LDS bases of its DMA slots in stage 0 (stage s adds s * the stage size)
+  const float* asrc[IA];
+  unsigned adst[IA];
+#pragma unroll
+  for (int j = 0; j < IA; ++j) {
+    const int u = (wave * IA + j) * 64 + lane, q2 = u / BM, row = u % BM;
+    asrc[j] = A + (long)min(m0 + row, p.M - 1) * p.lda + 4 * q2;
+    adst[j] = __builtin_amdgcn_readfirstlane(lds_addr(&sA[0][(wave * IA + j) * 64]));
+  }
+  const unsigned short* wsrc[IW];
+  unsigned wdst[IW];
+#pragma unroll
+  for (int j = 0; j < IW; ++j) {
+    const int u = (wave * IW + j) * 64 + lane, pl = u / PB, rem = u % PB, q = rem / BN, row = rem % BN;
+    wsrc[j] = W + pl * plane + (long)min(n0 + row, p.N - 1) * p.ldb + 8 * q;
+    wdst[j] = __builtin_amdgcn_readfirstlane(lds_addr(&sW[0][(wave * IW + j) * 64]));
+  }
+  const int nk = p.K / 32;
+  auto dma = [&](int stage, int t) {   // stage t's slice of this wave, unconditional (clamped re-read)
+    const int k0 = 32 * min(t, nk - 1);
+#pragma unroll
+    for (int j = 0; j < IA; ++j) lds_dma16(asrc[j] + k0, adst[j] + stage * UA * 16);
+#pragma unroll
+    for (int j = 0; j < IW; ++j) lds_dma16(wsrc[j] + k0, wdst[j] + stage * 3 * PB * 16);
+  };
+  const int q = lane >> 4;
+  auto compute = [&](int stage) {
+    const uint4* SA = sA[stage];
+    const uint4* SW = sW[stage];
+    bf16x8_t af[TM][3];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row = wm + 16 * i + (lane & 15);
+      uint4 h, m, l;
+      split3_quad(__builtin_bit_cast(float4, SA[(2 * q) * BM + row]), __builtin_bit_cast(float4, SA[(2 * q + 1) * BM + row]),
+                  h, m, l);
+      af[i][0] = __builtin_bit_cast(bf16x8_t, h);
+      af[i][1] = __builtin_bit_cast(bf16x8_t, m);
+      af[i][2] = __builtin_bit_cast(bf16x8_t, l);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      bf16x8_t bf[3];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) bf[pl] = __builtin_bit_cast(bf16x8_t, SW[pl * PB + q * BN + wn + 16 * j + (lane & 15)]);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        floatx4& sm = small[i][j];
+        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][1], bf[1], sm, 0, 0, 0);
+        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], bf[2], sm, 0, 0, 0);
+        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][2], bf[0], sm, 0, 0, 0);
+        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], bf[1], sm, 0, 0, 0);
+        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][1], bf[0], sm, 0, 0, 0);
+        big[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][0], bf[0], big[i][j], 0, 0, 0);
+      }
+    }
+  };
+  dma(0, 0);
+  dma(1, 1);
+  int stage = 0;
+  for (int t = 0; t < nk; ++t) {
+    // own stage-t DMAs landed (the 5 of stage t+1 may still fly), then everyone's; stage t-1 is free
+    asm volatile("s_waitcnt vmcnt(5)\n\ts_barrier" ::: "memory");
+    dma(stage == 0 ? 2 : stage - 1, t + 2);
+    compute(stage);
+    stage = stage == 2 ? 0 : stage + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA into LDS outlives the workgroup
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) big[i][j] += small[i][j];
+  store_tile_mf<16, TM, TN, BM, BN>(p, big, b, 0, m0, n0, wm, wn, lane);
+}
+
 // x [rows][ldx] fp32 -> y planes [3][rows][cols] bf16 (plane stride rows * cols), x = hi + mid + lo.
 __global__ void split3_bf16_kernel(const float* __restrict__ x, long ldx, uint4* __restrict__ y, int rows, int cols) {
   const int cq = cols / 8;
@@ -1945,6 +2085,25 @@ extern "C" int dasa_gemm_skinny_tune(int target_waves, int ks) {
   return 0;
 }
 
+// DASA_X6_BALANCE: 0 = no split-K on many-tile problems (default), 1 = 2- or 3-way, 2 = 2-way only. Off:
+// measured slower in isolation on every shape but 12800 x 768 x 3072 (+4 %; 1600 x 4096 x 768 -23 %,
+// 720 x 3072 x 768 -20 %) and within run-to-run noise in the training iteration (3359-3604 on vs
+// 3550-3558 off, profiles/r03/x6_balance_ab.txt): the split slabs cost more than the idle tail saves.
+static int g_x6_balance = -1;
+static int x6_balance() {
+  if (g_x6_balance < 0) {
+    const char* e = getenv("DASA_X6_BALANCE");
+    g_x6_balance = (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
+  }
+  return g_x6_balance;
+}
+
+extern "C" int dasa_gemm_x6_set_balance(int32_t mode) {
+  if (mode < 0 || mode > 2) return (int)hipErrorInvalidValue;
+  g_x6_balance = mode;
+  return 0;
+}
+
 extern "C" int dasa_gemm_force_config(int cfg) {
   g_force_cfg = cfg;
   if (cfg < 0) g_force_group = -1;
@@ -2089,14 +2248,15 @@ extern "C" int dasa_gemm_bf16(const dasa_gemm_desc* d, void* stream) {
   return 0;
 }
 
-// bf16x6 plan: forms 0..9 = tile / accumulator / prefetch variants (sweeps: dasa_gemm_force_config(
-// kX6Force + cfg + 16 * splitk)). Default: 128x128 tiles, separate small-term accumulator, two register
+// bf16x6 plan: forms 0..9 = tile / accumulator / prefetch variants, 15 = 128x128 one accumulator, 16 =
+// all-DMA 128x128 (3 x 40 KB ring; 256x128 would need 168 KB) (sweeps: dasa_gemm_force_config(kX6Force + cfg + 32 * splitk)). Default: 128x128 tiles, separate small-term accumulator, two register
 // stages of prefetch (form 8) — the fastest accurate form on every shape with >= 128 output tiles
 // (profiles/r02/gemm_x6_sweep_b.txt: 136-178 fp32-equivalent TFLOP/s on the 1600- to 20480-row
 // language / LXRT / LSTM shapes). Fewer tiles (the 720- / 1600-row LXRT and vision GEMMs: 36-108
 // tiles) split K over the tiles' workgroups until ~256 workgroups fill the chip, reduced in-kernel by
 // the last split to arrive (X6Split); needs the workspace.
 struct X6Plan { int cfg, bm, bn, splitk, kchunk; int64_t ws; };
+
 
 static X6Plan x6_plan(const dasa_gemm_desc* d) {
   const int M = d->M, N = d->N, K = d->K, batch = d->batch < 1 ? 1 : d->batch;
@@ -2107,8 +2267,8 @@ static X6Plan x6_plan(const dasa_gemm_desc* d) {
   // (profiles/r02/x6_forms.txt)
   if (M >= 4096 && N >= 2048) pl.cfg = 7;
   if (g_force_cfg >= kX6Force) {
-    pl.cfg = (g_force_cfg - kX6Force) % 16;
-    fsplit = ((g_force_cfg - kX6Force) / 16) % 64;
+    pl.cfg = (g_force_cfg - kX6Force) % 32;
+    fsplit = ((g_force_cfg - kX6Force) / 32) % 64;
   }
   pl.bm = (pl.cfg == 1 || pl.cfg == 3 || pl.cfg == 6 || pl.cfg == 7 || pl.cfg == 12 || pl.cfg == 13) ? 256
           : (pl.cfg == 4 || pl.cfg == 5) ? 64 : 128;
@@ -2119,6 +2279,17 @@ static X6Plan x6_plan(const dasa_gemm_desc* d) {
   int splitk = 1;
   if (fsplit > 0) splitk = fsplit < K / 128 ? fsplit : K / 128;
   else if (tiles < 128) splitk = (int)(256 / tiles) < K / 256 ? (int)(256 / tiles) : K / 256;
+  else if (pl.cfg == 8 && x6_balance() > 0) {
+    // (opt-in, see x6_balance) many tiles, one workgroup per CU: the last round of tiles can leave most
+    // of the chip idle (12800 x 768: 600 tiles = 2.34 rounds -> 78 % of the CU-time busy). Split K 2- or
+    // 3-way when that fills the rounds at least 8 points better (2 splits: 4.69 rounds -> 94 %) and every
+    // split keeps >= 8 K steps; the split partials are reduced in-kernel by the last arriver.
+    const double cus = (double)num_cus();
+    auto fill = [&](int s) { const double u = (double)tiles * s / cus; return u / ceil(u); };
+    double best = fill(1);
+    for (int s = 2; s <= (x6_balance() == 2 ? 2 : 3); ++s)
+      if (K / s >= 256 && fill(s) > best + 0.08) { best = fill(s); splitk = s; }
+  }
   const bool spl_form = pl.cfg == 8 || pl.cfg == 4 || pl.cfg == 5;
   if (!spl_form || splitk < 1 || tiles * splitk > 32767 || tiles > kCntWords) splitk = 1;
   if (splitk > 1) {
@@ -2193,6 +2364,7 @@ extern "C" int dasa_gemm_f32x6_ws(const dasa_gemm_desc* d, int64_t plane, void* 
     case 13: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<256, 128, 4, 2, true, 2, false, 2>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
     case 9: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true, 3>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
     case 15: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, false, 2>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
+    case 16: hipLaunchKernelGGL((gemm_f32x6_dma_kernel<128, 128, 4, 2>), grid, dim3(512), 0, st, p, (long)plane); break;
     default: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
   }
   DASA_CHECK_LAUNCH();

@@ -289,6 +289,9 @@ def _emu_ok(M, N, K, lda, x):
     return tiles >= 128 or (K >= 2048 and tiles * _x6_splitk(M, N, K) >= 192)
 
 
+_X6_WS_NEED = {}   # (M, N, K) -> split-K workspace bytes of the many-tile bf16x6 plan (a per-shape constant)
+
+
 def gemm_f32x6(x, planes, out, *, M, N, K, lda, ldc, bias=None, act=None, aux=None, ld_aux=0, colscale=None,
                alpha=1.0, beta=0.0):
     d = GemmDesc()
@@ -306,8 +309,12 @@ def gemm_f32x6(x, planes, out, *, M, N, K, lda, ldc, bias=None, act=None, aux=No
     ws, ws_bytes = 0, 0
     if -(-M // 128) * -(-N // 128) < 128:          # few tiles: the split-K form needs the workspace
         need = L.dasa_gemm_f32x6_workspace(ctypes.byref(d))
-        if need:
-            ws, ws_bytes = _gemm_ws(out.device, d, need)
+    else:                                          # many tiles: the plan may split to fill the last round
+        need = _X6_WS_NEED.get((M, N, K))
+        if need is None:
+            need = _X6_WS_NEED[(M, N, K)] = L.dasa_gemm_f32x6_workspace(ctypes.byref(d))
+    if need:
+        ws, ws_bytes = _gemm_ws(out.device, d, need)
     _call("dasa_gemm_f32x6", "gemm_x6", L.dasa_gemm_f32x6_ws, ctypes.byref(d), int(N) * int(K), ws, ws_bytes,
           _stream(), flops=2.0 * M * N * K, nbytes=4.0 * M * K + 6.0 * K * N + 4.0 * M * N,
           detail=(int(M), int(N), int(K)))

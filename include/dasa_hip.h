@@ -59,6 +59,10 @@ int64_t dasa_gemm_f32_workspace(const dasa_gemm_desc* d);
  * subsequent calls (-1 = automatic choice).
  * Returns the number of configurations. Host-only; not thread-safe with concurrent GEMM planning. */
 int dasa_gemm_force_config(int cfg);
+/* A/B hook for the bf16x6 plan (dasa_gemm_f32x6): split-K on many-tile problems to fill the last round of
+ * tiles; 0 = off (the default; DASA_X6_BALANCE=1/2 in the environment starts on), 1 = 2- or 3-way,
+ * 2 = 2-way only. Host-only setting. */
+int dasa_gemm_x6_set_balance(int32_t mode);
 /* Tuning hook for the skinny (M <= 32) weight-streaming GEMMs: target wave count of the plan (0 = do
  * not use the skinny kernels, -1 = default) and a pinned K-steps-per-wave (1/2/4/8, -1 = plan);
  * ks + 16 (16 = plan's KS) also turns the 17..20-row hybrid MFMA + VALU form off. Host-only; returns 0. */

@@ -1,4 +1,5 @@
 """Kernel-level parity of libdasa_hip.so against plain fp32 math on the host."""
+import ctypes
 import math
 
 import pytest
@@ -760,7 +761,7 @@ def test_gemm_f32x6(dev, M, N, K):
     err_nat = (out_nat.cpu().double() - ref).abs().max().item()
     try:
         outs = {}
-        for cfg in list(range(10)) + [15]:
+        for cfg in list(range(10)) + [15, 16]:
             lib.dasa_gemm_force_config((1 << 21) + cfg)
             y = torch.empty(M, N, device=dev)
             ops.gemm_f32x6(Ad, planes, y, M=M, N=N, K=K, lda=K + 8, ldc=N, bias=bias.to(dev))
@@ -774,8 +775,65 @@ def test_gemm_f32x6(dev, M, N, K):
                            aux=aux.to(dev), ld_aux=N, colscale=cs.to(dev), beta=0.5)
             want = torch.sigmoid(ref) * aux.double() * cs.double() + 0.5 * c0.double()
             assert (y2.cpu().double() - want).abs().max().item() < 1e-5, cfg
+        # the all-DMA form (A split at fragment-read time) runs form 8's products in form 8's order: bitwise
+        # equal to form 8 without split-K (the forced form-8 run above may split K on few-tile shapes)
+        lib.dasa_gemm_force_config((1 << 21) + 8 + 32 * 1)
+        y8 = torch.empty(M, N, device=dev)
+        ops.gemm_f32x6(Ad, planes, y8, M=M, N=N, K=K, lda=K + 8, ldc=N, bias=bias.to(dev))
+        assert torch.equal(outs[16], y8.cpu())
     finally:
         lib.dasa_gemm_force_config(-1)
+
+
+@pytest.mark.parametrize("M,N,K", [(1664, 1280, 768), (12800, 768, 768)])
+def test_gemm_f32x6_balanced_split(dev, M, N, K):
+    """Many output tiles whose last round would leave most CUs idle (130 tiles: 0.51 of a round; 600:
+    2.34 rounds), with the opt-in balanced plan (dasa_gemm_x6_set_balance(1)): K split 3- / 2-way and
+    reduced in-kernel. Error against fp64 at most the native kernel's (+10%) and the unsplit form's,
+    bitwise-deterministic repeats."""
+    from dasa_amd import _lib, ops
+    _lib.lib().dasa_gemm_x6_set_balance(1)
+    ops._X6_WS_NEED.clear()
+    try:
+        _balanced_split_case(dev, M, N, K)
+    finally:
+        _lib.lib().dasa_gemm_x6_set_balance(0)
+        ops._X6_WS_NEED.clear()
+
+
+def _balanced_split_case(dev, M, N, K):
+    from dasa_amd import _lib, ops
+    g = torch.Generator().manual_seed(M + 3 * N + K)
+    A = torch.randn(M, K, generator=g)
+    W = torch.randn(N, K, generator=g) * 0.05
+    bias = torch.randn(N, generator=g) * 0.1
+    ref = (A.double() @ W.double().t() + bias.double())
+    Ad, Wd, bd = A.to(dev), W.to(dev), bias.to(dev)
+    planes = ops.split3_bf16(Wd)
+    lib = _lib.lib()
+    d = ops.GemmDesc()
+    d.M, d.N, d.K, d.batch, d.opA, d.opB, d.lda, d.ldb, d.ldc = M, N, K, 1, 0, 1, K, K, N
+    assert lib.dasa_gemm_f32x6_workspace(ctypes.byref(d)) > 0          # the plan splits
+    out_nat = torch.empty(M, N, device=dev)
+    ops.gemm(Ad, Wd, out_nat, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, bias=bd)
+    err_nat = (out_nat.cpu().double() - ref).abs().max().item()
+    outs = []
+    for _ in range(2):
+        y = torch.full((M, N), float("nan"), device=dev)
+        ops.gemm_f32x6(Ad, planes, y, M=M, N=N, K=K, lda=K, ldc=N, bias=bd)
+        outs.append(y.cpu())
+    assert torch.equal(outs[0], outs[1])
+    err = (outs[0].double() - ref).abs().max().item()
+    try:
+        lib.dasa_gemm_force_config((1 << 21) + 8 + 32 * 1)                 # form 8, one split
+        ops._X6_WS_NEED.clear()
+        y1 = torch.empty(M, N, device=dev)
+        ops.gemm_f32x6(Ad, planes, y1, M=M, N=N, K=K, lda=K, ldc=N, bias=bd)
+        err1 = (y1.cpu().double() - ref).abs().max().item()
+    finally:
+        lib.dasa_gemm_force_config(-1)
+        ops._X6_WS_NEED.clear()
+    assert err <= 1.1 * err_nat + 1e-7 and err <= 1.5 * err1 + 1e-7, (err, err_nat, err1)
 
 
 @pytest.mark.parametrize("M,N,K", [(517, 200, 768), (720, 768, 768), (1600, 768, 3072), (100, 2048, 2048),
@@ -803,7 +861,7 @@ def test_gemm_f32x6_splitk(dev, M, N, K):
     err_nat = (out_nat.cpu().double() - ref).abs().max().item()
     try:
         for cfg, spl in ((8, 0), (8, 2), (8, 3), (4, 2), (4, 5), (5, 3)):
-            lib.dasa_gemm_force_config((1 << 21) + cfg + 16 * spl if spl else -1)
+            lib.dasa_gemm_force_config((1 << 21) + cfg + 32 * spl if spl else -1)
             outs = []
             for _ in range(3):
                 y = torch.full((M, N), float("nan"), device=dev)

@@ -85,7 +85,7 @@ def main():
             forms = {}
             for f in a.forms:
                 cfg, spl = (int(v) for v in f.split(":"))
-                L.dasa_gemm_force_config((1 << 21) + cfg + 16 * spl)
+                L.dasa_gemm_force_config((1 << 21) + cfg + 32 * spl)
                 x6()
                 us = timeit(x6, a.reps)
                 forms[f] = (round(fl / us / 1e6, 1), (y2.double() - ref).abs().max().item() / scale)

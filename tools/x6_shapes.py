@@ -31,12 +31,14 @@ def main():
         ref = y.clone()
         for f in forms:
             lib.dasa_gemm_force_config((1 << 21) + f)
+            ops._X6_WS_NEED.clear()      # the forced plan has its own split / workspace
             try:
                 uf = _time_graph(lambda: ops.linear(x, W, b, out=y), reps=20)
                 torch.cuda.synchronize()
                 line += f" | form {f} {uf:7.1f} us {2.0 * M * N * K / uf / 1e6:6.1f} TF d={(y - ref).abs().max().item():.1e}"
             finally:
                 lib.dasa_gemm_force_config(-1)
+                ops._X6_WS_NEED.clear()
         print(line, flush=True)
 
 
