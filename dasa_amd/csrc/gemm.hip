@@ -985,7 +985,9 @@ __device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
 
 __device__ __forceinline__ int bswz(int row) { return (row >> 1) & 7; }
 
-template <int BM, int BN, int WAVES_M, int WAVES_N, int PF = 1>
+// ASM: PF = 2 with the stage loads as inline asm and explicit counted vmcnt waits (the bf16x6 kernel's
+// form 18): hipcc merges the two register stages' pending loads at the loop header and drains vmcnt(0).
+template <int BM, int BN, int WAVES_M, int WAVES_N, int PF = 1, bool ASM = false>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_nt_kernel(GemmP p) {
   constexpr int NT = 64 * WAVES_M * WAVES_N;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N, TM = WM / 16, TN = WN / 16;
@@ -1019,36 +1021,50 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_nt_kernel(Ge
 
   // staging registers of the next K tile (a struct with member functions like TileLoader: hipcc keeps
   // it in VGPRs, where lambda-captured local arrays were promoted to LDS)
+  static_assert(!ASM || (PF == 2 && NA == 2 && NB == 2), "the asm-load form is written for NA = NB = 2");
   struct Stage {
-    float4 a[NA][2];
-    uint4 b[NB];
+    floatx4 a[NA][2];   // vector types: usable as inline-asm operands
+    u32x4 b[NB];
     __device__ __forceinline__ void load(const GemmP& p, const float* A, const unsigned short* W, int m0, int n0,
                                          int k0, int tid) {
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
         const int q = tid + NT * i, row = q >> 3, kq = q & 7;
         const float* src = A + (long)min(m0 + row, p.M - 1) * p.lda + k0 + 8 * kq;
-        a[i][0] = *reinterpret_cast<const float4*>(src);
-        a[i][1] = *reinterpret_cast<const float4*>(src + 4);
+        if (ASM) {
+          asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(a[i][0]) : "v"(src));
+          asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(a[i][1]) : "v"(src + 4));
+        } else {
+          a[i][0] = *reinterpret_cast<const floatx4*>(src);
+          a[i][1] = *reinterpret_cast<const floatx4*>(src + 4);
+        }
       }
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
         const int q = tid + NT * i, row = q >> 3, kq = q & 7;
-        b[i] = *reinterpret_cast<const uint4*>(W + (long)min(n0 + row, p.N - 1) * p.ldb + k0 + 8 * kq);
+        const unsigned short* src = W + (long)min(n0 + row, p.N - 1) * p.ldb + k0 + 8 * kq;
+        if (ASM) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(b[i]) : "v"(src));
+        else b[i] = *reinterpret_cast<const u32x4*>(src);
       }
+    }
+    // ASM: this stage's 6 loads landed; the other stage's 6, issued after them, stay in flight
+    __device__ __forceinline__ void landed() {
+      if constexpr (ASM)
+        asm volatile("s_waitcnt vmcnt(6)" : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(a[1][0]), "+v"(a[1][1]), "+v"(b[0]),
+                     "+v"(b[1]));
     }
     __device__ __forceinline__ void store(uint4* S, int tid) const {
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
         const int q = tid + NT * i, row = q >> 3, kq = q & 7;
-        const float4 x = a[i][0], y = a[i][1];
-        S[row * 8 + (kq ^ bswz(row))] = uint4{pack_bf16x2(x.x, x.y), pack_bf16x2(x.z, x.w),
-                                              pack_bf16x2(y.x, y.y), pack_bf16x2(y.z, y.w)};
+        const floatx4 x = a[i][0], y = a[i][1];
+        S[row * 8 + (kq ^ bswz(row))] = uint4{pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]),
+                                              pack_bf16x2(y[0], y[1]), pack_bf16x2(y[2], y[3])};
       }
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
         const int q = tid + NT * i, row = q >> 3, kq = q & 7;
-        S[BM * 8 + row * 8 + (kq ^ bswz(row))] = b[i];
+        S[BM * 8 + row * 8 + (kq ^ bswz(row))] = __builtin_bit_cast(uint4, b[i]);
       }
     }
   } stg, stg2;
@@ -1093,19 +1109,23 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_nt_kernel(Ge
   } else {
     // two register stages (as gemm_f32x6_nt_kernel): tile t + 2's loads are issued before tile t's MFMAs
     stg2.load(p, A, W, m0, n0, 64 * min(1, nk - 1), tid);
+    stg.landed();
     stg.store(smem, tid);
     __syncthreads();
     for (int t = 0; t < nk; t += 2) {
       stg.load(p, A, W, m0, n0, 64 * min(t + 2, nk - 1), tid);
       compute(smem);
+      stg2.landed();
       stg2.store(smem + STAGE, tid);
       __syncthreads();
       if (t + 1 >= nk) break;
       stg2.load(p, A, W, m0, n0, 64 * min(t + 3, nk - 1), tid);
       compute(smem + STAGE);
+      stg.landed();
       stg.store(smem, tid);
       __syncthreads();
     }
+    if (ASM) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the clamped tail loads
   }
   store_tile_mf<16, TM, TN, BM, BN>(p, acc, b, 0, m0, n0, wm, wn, lane);
 }
@@ -1149,7 +1169,11 @@ struct X6Split { unsigned* cnt; float* slab; int splitk, kchunk; };
 // lets it use 256 VGPRs instead of spilling to reach an occupancy the LDS forbids)
 // PRIO (A/B forms 10-13): 1 = s_setprio(1) around every MFMA cluster (cdna_hip_programming.md T5),
 // 2 = one static s_setprio(1) for the second half of the workgroup's waves (T5 static form).
-template <int BM, int BN, int WAVES_M, int WAVES_N, bool SEP, int PF = 1, bool SPL = false, int PRIO = 0>
+// ASM (form 18): the PF = 2 stage loads as inline asm with explicit vmcnt(5) waits (see the ping-pong
+// form): hipcc merged the two register stages' pending loads at the loop header and drained vmcnt(0)
+// before the first fragment reads of every other K step (profiles/r03/x6_pingpong.txt).
+template <int BM, int BN, int WAVES_M, int WAVES_N, bool SEP, int PF = 1, bool SPL = false, int PRIO = 0,
+          bool ASM = false>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) __attribute__((amdgpu_waves_per_eu(1, 2)))
 void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
   constexpr int NT = 64 * WAVES_M * WAVES_N;
@@ -1193,9 +1217,10 @@ void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
 
   // unit u -> (row, quad): 8 consecutive lanes take 8 consecutive rows of one quad (coalesced 128-B
   // row segments per 4 x 8 lanes on the global side, conflict-free ds_write_b128 groups on the LDS side)
+  static_assert(!ASM || (NA == 1 && NB == 1 && PF == 2 && !SPL), "the asm-load form is written for form 8");
   struct Stage {
-    uint4 a[NA][2];   // 8 fp32 of A as bit patterns (uint4 storage keeps the stages out of scratch)
-    uint4 w[3][NB];
+    u32x4 a[NA][2];   // 8 fp32 of A as bit patterns (integer vectors keep the stages out of scratch)
+    u32x4 w[3][NB];
     __device__ __forceinline__ static void unit(int u, int& row, int& q) {
       q = (u >> 3) & 3;
       row = (u & 7) + 8 * (u >> 5);
@@ -1207,8 +1232,13 @@ void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
         int row, q;
         unit(tid + NT * i, row, q);
         const float* src = A + (long)min(m0 + row, p.M - 1) * p.lda + k0 + 8 * q;
-        a[i][0] = *reinterpret_cast<const uint4*>(src);
-        a[i][1] = *reinterpret_cast<const uint4*>(src + 4);
+        if (ASM) {
+          asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(a[i][0]) : "v"(src));
+          asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(a[i][1]) : "v"(src + 4));
+        } else {
+          a[i][0] = *reinterpret_cast<const u32x4*>(src);
+          a[i][1] = *reinterpret_cast<const u32x4*>(src + 4);
+        }
       }
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
@@ -1216,8 +1246,16 @@ void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
         unit(tid + NT * i, row, q);
         const unsigned short* src = W + (long)min(n0 + row, p.N - 1) * p.ldb + k0 + 8 * q;
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) w[pl][i] = *reinterpret_cast<const uint4*>(src + pl * plane);
+        for (int pl = 0; pl < 3; ++pl) {
+          if (ASM) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(w[pl][i]) : "v"(src + pl * plane));
+          else w[pl][i] = *reinterpret_cast<const u32x4*>(src + pl * plane);
+        }
       }
+    }
+    // ASM: this stage's loads landed; the 5 loads issued after them (the other stage) stay in flight
+    __device__ __forceinline__ void landed() {
+      if (ASM)
+        asm volatile("s_waitcnt vmcnt(5)" : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(w[0][0]), "+v"(w[1][0]), "+v"(w[2][0]));
     }
     __device__ __forceinline__ void store(uint4* S, int tid) const {
 #pragma unroll
@@ -1235,7 +1273,7 @@ void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
         int row, q;
         unit(tid + NT * i, row, q);
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) S[3 * PA + pl * PB + q * BN + row] = w[pl][i];
+        for (int pl = 0; pl < 3; ++pl) S[3 * PA + pl * PB + q * BN + row] = __builtin_bit_cast(uint4, w[pl][i]);
       }
     }
   } stg, stg2, stg3;
@@ -1306,19 +1344,23 @@ void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
     // two register stages: the loads of tile t + 2 are issued before tile t's MFMAs, so each tile's
     // global reads have two K steps of compute to land in (the L2 / MALL latency under full load)
     stg2.load(p, A, W, plane, m0, n0, 32 * min(1, nk - 1), tid);
+    stg.landed();
     stg.store(smem, tid);
     __syncthreads();
     for (int t = 0; t < nk; t += 2) {
       stg.load(p, A, W, plane, m0, n0, 32 * min(t + 2, nk - 1), tid);
       compute(smem);
+      stg2.landed();
       stg2.store(smem + STAGE, tid);
       __syncthreads();
       if (t + 1 >= nk) break;
       stg2.load(p, A, W, plane, m0, n0, 32 * min(t + 3, nk - 1), tid);
       compute(smem + STAGE);
+      stg.landed();
       stg.store(smem, tid);
       __syncthreads();
     }
+    if (ASM) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the clamped tail loads
   }
   if (SEP) {
 #pragma unroll
@@ -1504,6 +1546,149 @@ void gemm_f32x6_dma_kernel(GemmP p, long plane) {
     stage = stage == 2 ? 0 : stage + 1;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA into LDS outlives the workgroup
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) big[i][j] += small[i][j];
+  store_tile_mf<16, TM, TN, BM, BN>(p, big, b, 0, m0, n0, wm, wn, lane);
+}
+
+// Ping-pong form (form 17): form 8's tile (128 x 128, 8 waves of 32 x 64), products, order and epilogue
+// (bitwise equal), with the two waves of each SIMD offset by half a K step. Waves 0-3 (group 0: output
+// rows 0-63) and 4-7 (group 1: rows 64-127) each stage half of every K step (their own 64 A rows and 64
+// of the 128 W rows: one 8-float A unit + one unit per W plane per thread, as in form 8). Every wave runs
+// the same loop, step t = { phase A: split + store stage t+1 (registers -> LDS), load stage t+3 into the
+// freed registers | barrier | phase B: MFMAs on stage t | barrier }, but group 1 enters it one barrier
+// late (and group 0 leaves it with one barrier more), so while group 0 runs phase B, group 1 runs phase
+// A, and vice versa: on every SIMD one wave's split / ds_write / load issue sits under the other wave's
+// MFMAs instead of both waves reaching it together after the barrier (form 8). Stage s lives in LDS
+// buffer s % 3 (three 48 KB stages): a buffer is refilled two phases after the later group finished
+// reading it. One straight-line loop body for both groups keeps hipcc's vmcnt tracking exact (a
+// group-dependent branch made it drain vmcnt(0) before every compute phase).
+template <int BM, int BN>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2)))
+void gemm_f32x6_pp_kernel(GemmP p, long plane) {
+  constexpr int WAVES_M = 4, WAVES_N = 2, HT = 256;
+  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N, TM = WM / 16, TN = WN / 16;
+  constexpr int PA = BM * 4, PB = BN * 4;   // uint4 per plane image
+  constexpr int STAGE = 3 * (PA + PB);
+  static_assert(BM / 2 * 4 == HT && BN / 2 * 4 == HT, "one A unit and one W unit per plane per thread");
+  __shared__ uint4 smem[3 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int grp = __builtin_amdgcn_readfirstlane(wave >> 2), gt = tid & (HT - 1);
+  const int wm = (wave / WAVES_N) * WM, wn = (wave % WAVES_N) * WN;
+  const int wgid = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+  int m0, n0;
+  if (p.group_m > 1) {
+    const int gm = p.group_m, per = gm * gridDim.x, gg = wgid / per;
+    const int rows = min(gm, (int)gridDim.y - gg * gm), r = wgid - gg * per;
+    m0 = (gg * gm + r % rows) * BM;
+    n0 = (r / rows) * BN;
+  } else {
+    n0 = (wgid % gridDim.x) * BN;
+    m0 = (wgid / gridDim.x) * BM;
+  }
+  const int b = blockIdx.z;
+  const float* A = p.A + (long)b * p.sA;
+  const unsigned short* W = reinterpret_cast<const unsigned short*>(p.B) + (long)b * p.sB;
+
+  floatx4 big[TM][TN], small[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      big[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+      small[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+
+  // this thread's staging unit: (row, K quad) of its group's 64-row half, for A and for W
+  const int urow = 64 * grp + (gt & 7) + 8 * (gt >> 5), uq = (gt >> 3) & 3;
+  const float* asrc = A + (long)min(m0 + urow, p.M - 1) * p.lda + 8 * uq;
+  const unsigned short* wsrc = W + (long)min(n0 + urow, p.N - 1) * p.ldb + 8 * uq;
+  struct Stage {
+    u32x4 a[2];   // vector types: an inline-asm operand cannot be a struct
+    u32x4 w[3];
+  } s0, s1;
+  const int nk = p.K / 32;
+  // the stage loads are inline asm: hipcc's waitcnt pass does not see them, so it cannot merge the two
+  // register sets' pending loads at the loop header and drain vmcnt(0) (it did: profiles/r03/
+  // x6_pingpong.txt); the wait before a set is stored is explicit, vmcnt(5) = the other set's five
+  // loads stay in flight, and it names the set's registers as operands so no use moves above it
+  auto load = [&](Stage& s, int t) {
+    const int k0 = 32 * min(t, nk - 1);   // unconditional (clamped re-read)
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(s.a[0]) : "v"(asrc + k0));
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(s.a[1]) : "v"(asrc + k0 + 4));
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(s.w[pl]) : "v"(wsrc + pl * plane + k0));
+  };
+  auto landed = [&](Stage& s) {
+    asm volatile("s_waitcnt vmcnt(5)" : "+v"(s.a[0]), "+v"(s.a[1]), "+v"(s.w[0]), "+v"(s.w[1]), "+v"(s.w[2]));
+  };
+  auto store = [&](const Stage& s, uint4* S) {
+    uint4 h, m, l;
+    split3_quad(__builtin_bit_cast(float4, s.a[0]), __builtin_bit_cast(float4, s.a[1]), h, m, l);
+    S[0 * PA + uq * BM + urow] = h;
+    S[1 * PA + uq * BM + urow] = m;
+    S[2 * PA + uq * BM + urow] = l;
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) S[3 * PA + pl * PB + uq * BN + urow] = __builtin_bit_cast(uint4, s.w[pl]);
+  };
+  auto compute = [&](const uint4* S) {
+    const int q = lane >> 4;
+    bf16x8_t bf[3][TN];
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bf[pl][j] = __builtin_bit_cast(bf16x8_t, S[3 * PA + pl * PB + q * BN + wn + 16 * j + (lane & 15)]);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      bf16x8_t af[3];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        af[pl] = __builtin_bit_cast(bf16x8_t, S[pl * PA + q * BM + wm + 16 * i + (lane & 15)]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        floatx4& sm = small[i][j];
+        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bf[1][j], sm, 0, 0, 0);
+        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[2][j], sm, 0, 0, 0);
+        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2], bf[0][j], sm, 0, 0, 0);
+        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[1][j], sm, 0, 0, 0);
+        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bf[0][j], sm, 0, 0, 0);
+        big[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[0][j], big[i][j], 0, 0, 0);
+      }
+    }
+  };
+  // prologue: stage 0 staged by both groups into buffer 0; stage 1 in s1, stage 2 in s0
+  load(s0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(s0.a[0]), "+v"(s0.a[1]), "+v"(s0.w[0]), "+v"(s0.w[1]), "+v"(s0.w[2]));
+  store(s0, smem);
+  load(s1, 1);
+  load(s0, 2);
+  __syncthreads();
+  if (grp == 1) __builtin_amdgcn_s_barrier();   // group 1 runs half a step behind
+  // step t: X holds stage t+1 (stored this step into buffer (t+1) % 3, then reloaded with stage t+3)
+  int bc = 0, bn = 1;   // buffers of stages t and t+1
+#define X6P_STEP(X, T)                                                                                      \
+  {                                                                                                         \
+    landed(X);                                                                                              \
+    store(X, smem + bn * STAGE);                                                                            \
+    load(X, (T) + 3);                                                                                       \
+    __syncthreads();                                                                                        \
+    compute(smem + bc * STAGE);                                                                             \
+    __syncthreads();                                                                                        \
+    bc = bn;                                                                                                \
+    bn = bn == 2 ? 0 : bn + 1;                                                                              \
+  }
+  for (int t = 0; t < nk; t += 2) {
+    X6P_STEP(s1, t);
+    if (t + 1 >= nk) break;
+    X6P_STEP(s0, t + 1);
+  }
+#undef X6P_STEP
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the clamped tail loads, before the epilogue's own
+  if (grp == 0) __builtin_amdgcn_s_barrier();   // pairs with group 1's last barrier
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -2085,6 +2270,16 @@ extern "C" int dasa_gemm_skinny_tune(int target_waves, int ks) {
   return 0;
 }
 
+// DASA_X6_FORM=<form>: A/B override of the default non-split bf16x6 form (the split-K plan keeps form 8)
+static int g_x6_form = -1;
+static int x6_form_override() {
+  if (g_x6_form < 0) {
+    const char* e = getenv("DASA_X6_FORM");
+    g_x6_form = e ? atoi(e) : 0;
+  }
+  return g_x6_form;
+}
+
 // DASA_X6_BALANCE: 0 = no split-K on many-tile problems (default), 1 = 2- or 3-way, 2 = 2-way only. Off:
 // measured slower in isolation on every shape but 12800 x 768 x 3072 (+4 %; 1600 x 4096 x 768 -23 %,
 // 720 x 3072 x 768 -20 %) and within run-to-run noise in the training iteration (3359-3604 on vs
@@ -2226,8 +2421,8 @@ extern "C" int dasa_gemm_bf16(const dasa_gemm_desc* d, void* stream) {
   // +8-25% over 128x128 on the configs[4] shapes (profiles/r02/gemm_bf16_sweep.txt)
   int cfg = cdiv(M, 256) * cdiv(N, 256) * batch >= 200 ? 9 : 2;
   if (g_force_cfg >= kBf16Force && g_force_cfg < kX6Force) cfg = (g_force_cfg - kBf16Force) % 16;
-  const int bm = (cfg == 1 || cfg == 5 || cfg == 7 || cfg == 9) ? 256 : 128,
-            bn = cfg == 3 ? 64 : (cfg == 6 || cfg == 9 || cfg == 10) ? 256 : 128;
+  const int bm = (cfg == 1 || cfg == 5 || cfg == 7 || cfg == 9 || cfg == 12) ? 256 : 128,
+            bn = cfg == 3 ? 64 : (cfg == 6 || cfg == 9 || cfg == 10 || cfg == 12) ? 256 : 128;
   p.group_m = cdiv(M, bm) >= 8 ? 4 : 1;
   dim3 grid((unsigned)cdiv(N, bn), (unsigned)cdiv(M, bm), batch);
   hipStream_t st = (hipStream_t)stream;
@@ -2242,6 +2437,8 @@ extern "C" int dasa_gemm_bf16(const dasa_gemm_desc* d, void* stream) {
     case 8: hipLaunchKernelGGL((gemm_bf16_nt_kernel<128, 128, 4, 2, 2>), grid, dim3(512), 0, st, p); break;
     case 9: hipLaunchKernelGGL((gemm_bf16_nt_kernel<256, 256, 4, 4>), grid, dim3(1024), 0, st, p); break;
     case 10: hipLaunchKernelGGL((gemm_bf16_nt_kernel<128, 256, 2, 4, 2>), grid, dim3(512), 0, st, p); break;
+    case 11: hipLaunchKernelGGL((gemm_bf16_nt_kernel<128, 128, 4, 2, 2, true>), grid, dim3(512), 0, st, p); break;
+    case 12: hipLaunchKernelGGL((gemm_bf16_nt_kernel<256, 256, 4, 4, 2, true>), grid, dim3(1024), 0, st, p); break;
     default: hipLaunchKernelGGL((gemm_bf16_nt_kernel<128, 128, 2, 2>), grid, dim3(256), 0, st, p); break;
   }
   DASA_CHECK_LAUNCH();
@@ -2249,7 +2446,7 @@ extern "C" int dasa_gemm_bf16(const dasa_gemm_desc* d, void* stream) {
 }
 
 // bf16x6 plan: forms 0..9 = tile / accumulator / prefetch variants, 15 = 128x128 one accumulator, 16 =
-// all-DMA 128x128 (3 x 40 KB ring; 256x128 would need 168 KB) (sweeps: dasa_gemm_force_config(kX6Force + cfg + 32 * splitk)). Default: 128x128 tiles, separate small-term accumulator, two register
+// all-DMA 128x128 (3 x 40 KB ring; 256x128 would need 168 KB), 17 = ping-pong 128x128, 18 = form 8 with asm stage loads (sweeps: dasa_gemm_force_config(kX6Force + cfg + 32 * splitk)). Default: 128x128 tiles, separate small-term accumulator, two register
 // stages of prefetch (form 8) — the fastest accurate form on every shape with >= 128 output tiles
 // (profiles/r02/gemm_x6_sweep_b.txt: 136-178 fp32-equivalent TFLOP/s on the 1600- to 20480-row
 // language / LXRT / LSTM shapes). Fewer tiles (the 720- / 1600-row LXRT and vision GEMMs: 36-108
@@ -2297,6 +2494,11 @@ static X6Plan x6_plan(const dasa_gemm_desc* d) {
     pl.splitk = (int)cdiv(K, pl.kchunk);
   }
   if (pl.splitk > 1) pl.ws = kCntBytes + tiles * pl.splitk * (int64_t)pl.bm * pl.bn * (int64_t)sizeof(float);
+  else if (g_force_cfg < kX6Force && x6_form_override() > 0) {   // A/B: DASA_X6_FORM replaces forms 7 / 8
+    pl.cfg = x6_form_override();
+    pl.bm = pl.cfg == 7 ? 256 : 128;
+    pl.bn = 128;
+  }
   return pl;
 }
 
@@ -2365,6 +2567,8 @@ extern "C" int dasa_gemm_f32x6_ws(const dasa_gemm_desc* d, int64_t plane, void* 
     case 9: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true, 3>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
     case 15: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, false, 2>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
     case 16: hipLaunchKernelGGL((gemm_f32x6_dma_kernel<128, 128, 4, 2>), grid, dim3(512), 0, st, p, (long)plane); break;
+    case 17: hipLaunchKernelGGL((gemm_f32x6_pp_kernel<128, 128>), grid, dim3(512), 0, st, p, (long)plane); break;
+    case 18: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true, 2, false, 0, true>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
     default: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
   }
   DASA_CHECK_LAUNCH();

@@ -684,7 +684,7 @@ def test_gemm_bf16(dev, M, N, K):
     b = _rand(N, g=g)
     xb, Wb = x.to(torch.bfloat16).double(), W.to(torch.bfloat16).double()
     L = _lib.lib()
-    for cfg in [(1 << 20) + c for c in range(11)] + [-1]:
+    for cfg in [(1 << 20) + c for c in range(13)] + [-1]:
         L.dasa_gemm_force_config(cfg)
         try:
             with torch.no_grad(), ops.bf16_matmul():
@@ -761,7 +761,7 @@ def test_gemm_f32x6(dev, M, N, K):
     err_nat = (out_nat.cpu().double() - ref).abs().max().item()
     try:
         outs = {}
-        for cfg in list(range(10)) + [15, 16]:
+        for cfg in list(range(10)) + [15, 16, 17, 18]:
             lib.dasa_gemm_force_config((1 << 21) + cfg)
             y = torch.empty(M, N, device=dev)
             ops.gemm_f32x6(Ad, planes, y, M=M, N=N, K=K, lda=K + 8, ldc=N, bias=bias.to(dev))
@@ -775,12 +775,13 @@ def test_gemm_f32x6(dev, M, N, K):
                            aux=aux.to(dev), ld_aux=N, colscale=cs.to(dev), beta=0.5)
             want = torch.sigmoid(ref) * aux.double() * cs.double() + 0.5 * c0.double()
             assert (y2.cpu().double() - want).abs().max().item() < 1e-5, cfg
-        # the all-DMA form (A split at fragment-read time) runs form 8's products in form 8's order: bitwise
-        # equal to form 8 without split-K (the forced form-8 run above may split K on few-tile shapes)
+        # forms 16-18 run form 8's products in form 8's order: bitwise equal to form 8 without split-K (the
+        # forced form-8 run above may split K on few-tile shapes)
         lib.dasa_gemm_force_config((1 << 21) + 8 + 32 * 1)
         y8 = torch.empty(M, N, device=dev)
         ops.gemm_f32x6(Ad, planes, y8, M=M, N=N, K=K, lda=K + 8, ldc=N, bias=bias.to(dev))
-        assert torch.equal(outs[16], y8.cpu())
+        for cfg in (16, 17, 18):   # all-DMA, ping-pong, asm-load forms: form 8's products in form 8's order
+            assert torch.equal(outs[cfg], y8.cpu()), cfg
     finally:
         lib.dasa_gemm_force_config(-1)
 
