@@ -985,9 +985,7 @@ __device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
 
 __device__ __forceinline__ int bswz(int row) { return (row >> 1) & 7; }
 
-// ASM: PF = 2 with the stage loads as inline asm and explicit counted vmcnt waits (the bf16x6 kernel's
-// form 18): hipcc merges the two register stages' pending loads at the loop header and drains vmcnt(0).
-template <int BM, int BN, int WAVES_M, int WAVES_N, int PF = 1, bool ASM = false>
+template <int BM, int BN, int WAVES_M, int WAVES_N, int PF = 1>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_nt_kernel(GemmP p) {
   constexpr int NT = 64 * WAVES_M * WAVES_N;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N, TM = WM / 16, TN = WN / 16;
@@ -1021,9 +1019,8 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_nt_kernel(Ge
 
   // staging registers of the next K tile (a struct with member functions like TileLoader: hipcc keeps
   // it in VGPRs, where lambda-captured local arrays were promoted to LDS)
-  static_assert(!ASM || (PF == 2 && NA == 2 && NB == 2), "the asm-load form is written for NA = NB = 2");
   struct Stage {
-    floatx4 a[NA][2];   // vector types: usable as inline-asm operands
+    floatx4 a[NA][2];
     u32x4 b[NB];
     __device__ __forceinline__ void load(const GemmP& p, const float* A, const unsigned short* W, int m0, int n0,
                                          int k0, int tid) {
@@ -1031,27 +1028,15 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_nt_kernel(Ge
       for (int i = 0; i < NA; ++i) {
         const int q = tid + NT * i, row = q >> 3, kq = q & 7;
         const float* src = A + (long)min(m0 + row, p.M - 1) * p.lda + k0 + 8 * kq;
-        if (ASM) {
-          asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(a[i][0]) : "v"(src));
-          asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(a[i][1]) : "v"(src + 4));
-        } else {
-          a[i][0] = *reinterpret_cast<const floatx4*>(src);
-          a[i][1] = *reinterpret_cast<const floatx4*>(src + 4);
-        }
+        a[i][0] = *reinterpret_cast<const floatx4*>(src);
+        a[i][1] = *reinterpret_cast<const floatx4*>(src + 4);
       }
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
         const int q = tid + NT * i, row = q >> 3, kq = q & 7;
         const unsigned short* src = W + (long)min(n0 + row, p.N - 1) * p.ldb + k0 + 8 * kq;
-        if (ASM) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(b[i]) : "v"(src));
-        else b[i] = *reinterpret_cast<const u32x4*>(src);
+        b[i] = *reinterpret_cast<const u32x4*>(src);
       }
-    }
-    // ASM: this stage's 6 loads landed; the other stage's 6, issued after them, stay in flight
-    __device__ __forceinline__ void landed() {
-      if constexpr (ASM)
-        asm volatile("s_waitcnt vmcnt(6)" : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(a[1][0]), "+v"(a[1][1]), "+v"(b[0]),
-                     "+v"(b[1]));
     }
     __device__ __forceinline__ void store(uint4* S, int tid) const {
 #pragma unroll
@@ -1109,23 +1094,19 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_nt_kernel(Ge
   } else {
     // two register stages (as gemm_f32x6_nt_kernel): tile t + 2's loads are issued before tile t's MFMAs
     stg2.load(p, A, W, m0, n0, 64 * min(1, nk - 1), tid);
-    stg.landed();
-    stg.store(smem, tid);
+        stg.store(smem, tid);
     __syncthreads();
     for (int t = 0; t < nk; t += 2) {
       stg.load(p, A, W, m0, n0, 64 * min(t + 2, nk - 1), tid);
       compute(smem);
-      stg2.landed();
-      stg2.store(smem + STAGE, tid);
+            stg2.store(smem + STAGE, tid);
       __syncthreads();
       if (t + 1 >= nk) break;
       stg2.load(p, A, W, m0, n0, 64 * min(t + 3, nk - 1), tid);
       compute(smem + STAGE);
-      stg.landed();
-      stg.store(smem, tid);
+            stg.store(smem, tid);
       __syncthreads();
     }
-    if (ASM) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the clamped tail loads
   }
   store_tile_mf<16, TM, TN, BM, BN>(p, acc, b, 0, m0, n0, wm, wn, lane);
 }
@@ -1169,11 +1150,7 @@ struct X6Split { unsigned* cnt; float* slab; int splitk, kchunk; };
 // lets it use 256 VGPRs instead of spilling to reach an occupancy the LDS forbids)
 // PRIO (A/B forms 10-13): 1 = s_setprio(1) around every MFMA cluster (cdna_hip_programming.md T5),
 // 2 = one static s_setprio(1) for the second half of the workgroup's waves (T5 static form).
-// ASM (form 18): the PF = 2 stage loads as inline asm with explicit vmcnt(5) waits (see the ping-pong
-// form): hipcc merged the two register stages' pending loads at the loop header and drained vmcnt(0)
-// before the first fragment reads of every other K step (profiles/r03/x6_pingpong.txt).
-template <int BM, int BN, int WAVES_M, int WAVES_N, bool SEP, int PF = 1, bool SPL = false, int PRIO = 0,
-          bool ASM = false>
+template <int BM, int BN, int WAVES_M, int WAVES_N, bool SEP, int PF = 1, bool SPL = false, int PRIO = 0>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) __attribute__((amdgpu_waves_per_eu(1, 2)))
 void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
   constexpr int NT = 64 * WAVES_M * WAVES_N;
@@ -1217,7 +1194,6 @@ void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
 
   // unit u -> (row, quad): 8 consecutive lanes take 8 consecutive rows of one quad (coalesced 128-B
   // row segments per 4 x 8 lanes on the global side, conflict-free ds_write_b128 groups on the LDS side)
-  static_assert(!ASM || (NA == 1 && NB == 1 && PF == 2 && !SPL), "the asm-load form is written for form 8");
   struct Stage {
     u32x4 a[NA][2];   // 8 fp32 of A as bit patterns (integer vectors keep the stages out of scratch)
     u32x4 w[3][NB];
@@ -1232,13 +1208,8 @@ void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
         int row, q;
         unit(tid + NT * i, row, q);
         const float* src = A + (long)min(m0 + row, p.M - 1) * p.lda + k0 + 8 * q;
-        if (ASM) {
-          asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(a[i][0]) : "v"(src));
-          asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(a[i][1]) : "v"(src + 4));
-        } else {
-          a[i][0] = *reinterpret_cast<const u32x4*>(src);
-          a[i][1] = *reinterpret_cast<const u32x4*>(src + 4);
-        }
+        a[i][0] = *reinterpret_cast<const u32x4*>(src);
+        a[i][1] = *reinterpret_cast<const u32x4*>(src + 4);
       }
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
@@ -1246,16 +1217,8 @@ void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
         unit(tid + NT * i, row, q);
         const unsigned short* src = W + (long)min(n0 + row, p.N - 1) * p.ldb + k0 + 8 * q;
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) {
-          if (ASM) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(w[pl][i]) : "v"(src + pl * plane));
-          else w[pl][i] = *reinterpret_cast<const u32x4*>(src + pl * plane);
-        }
+        for (int pl = 0; pl < 3; ++pl) w[pl][i] = *reinterpret_cast<const u32x4*>(src + pl * plane);
       }
-    }
-    // ASM: this stage's loads landed; the 5 loads issued after them (the other stage) stay in flight
-    __device__ __forceinline__ void landed() {
-      if (ASM)
-        asm volatile("s_waitcnt vmcnt(5)" : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(w[0][0]), "+v"(w[1][0]), "+v"(w[2][0]));
     }
     __device__ __forceinline__ void store(uint4* S, int tid) const {
 #pragma unroll
@@ -1344,23 +1307,19 @@ void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
     // two register stages: the loads of tile t + 2 are issued before tile t's MFMAs, so each tile's
     // global reads have two K steps of compute to land in (the L2 / MALL latency under full load)
     stg2.load(p, A, W, plane, m0, n0, 32 * min(1, nk - 1), tid);
-    stg.landed();
-    stg.store(smem, tid);
+        stg.store(smem, tid);
     __syncthreads();
     for (int t = 0; t < nk; t += 2) {
       stg.load(p, A, W, plane, m0, n0, 32 * min(t + 2, nk - 1), tid);
       compute(smem);
-      stg2.landed();
-      stg2.store(smem + STAGE, tid);
+            stg2.store(smem + STAGE, tid);
       __syncthreads();
       if (t + 1 >= nk) break;
       stg2.load(p, A, W, plane, m0, n0, 32 * min(t + 3, nk - 1), tid);
       compute(smem + STAGE);
-      stg.landed();
-      stg.store(smem, tid);
+            stg.store(smem, tid);
       __syncthreads();
     }
-    if (ASM) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the clamped tail loads
   }
   if (SEP) {
 #pragma unroll
@@ -1546,149 +1505,6 @@ void gemm_f32x6_dma_kernel(GemmP p, long plane) {
     stage = stage == 2 ? 0 : stage + 1;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA into LDS outlives the workgroup
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) big[i][j] += small[i][j];
-  store_tile_mf<16, TM, TN, BM, BN>(p, big, b, 0, m0, n0, wm, wn, lane);
-}
-
-// Ping-pong form (form 17): form 8's tile (128 x 128, 8 waves of 32 x 64), products, order and epilogue
-// (bitwise equal), with the two waves of each SIMD offset by half a K step. Waves 0-3 (group 0: output
-// rows 0-63) and 4-7 (group 1: rows 64-127) each stage half of every K step (their own 64 A rows and 64
-// of the 128 W rows: one 8-float A unit + one unit per W plane per thread, as in form 8). Every wave runs
-// the same loop, step t = { phase A: split + store stage t+1 (registers -> LDS), load stage t+3 into the
-// freed registers | barrier | phase B: MFMAs on stage t | barrier }, but group 1 enters it one barrier
-// late (and group 0 leaves it with one barrier more), so while group 0 runs phase B, group 1 runs phase
-// A, and vice versa: on every SIMD one wave's split / ds_write / load issue sits under the other wave's
-// MFMAs instead of both waves reaching it together after the barrier (form 8). Stage s lives in LDS
-// buffer s % 3 (three 48 KB stages): a buffer is refilled two phases after the later group finished
-// reading it. One straight-line loop body for both groups keeps hipcc's vmcnt tracking exact (a
-// group-dependent branch made it drain vmcnt(0) before every compute phase).
-template <int BM, int BN>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2)))
-void gemm_f32x6_pp_kernel(GemmP p, long plane) {
-  constexpr int WAVES_M = 4, WAVES_N = 2, HT = 256;
-  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N, TM = WM / 16, TN = WN / 16;
-  constexpr int PA = BM * 4, PB = BN * 4;   // uint4 per plane image
-  constexpr int STAGE = 3 * (PA + PB);
-  static_assert(BM / 2 * 4 == HT && BN / 2 * 4 == HT, "one A unit and one W unit per plane per thread");
-  __shared__ uint4 smem[3 * STAGE];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int grp = __builtin_amdgcn_readfirstlane(wave >> 2), gt = tid & (HT - 1);
-  const int wm = (wave / WAVES_N) * WM, wn = (wave % WAVES_N) * WN;
-  const int wgid = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
-  int m0, n0;
-  if (p.group_m > 1) {
-    const int gm = p.group_m, per = gm * gridDim.x, gg = wgid / per;
-    const int rows = min(gm, (int)gridDim.y - gg * gm), r = wgid - gg * per;
-    m0 = (gg * gm + r % rows) * BM;
-    n0 = (r / rows) * BN;
-  } else {
-    n0 = (wgid % gridDim.x) * BN;
-    m0 = (wgid / gridDim.x) * BM;
-  }
-  const int b = blockIdx.z;
-  const float* A = p.A + (long)b * p.sA;
-  const unsigned short* W = reinterpret_cast<const unsigned short*>(p.B) + (long)b * p.sB;
-
-  floatx4 big[TM][TN], small[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      big[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-      small[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-    }
-
-  // this thread's staging unit: (row, K quad) of its group's 64-row half, for A and for W
-  const int urow = 64 * grp + (gt & 7) + 8 * (gt >> 5), uq = (gt >> 3) & 3;
-  const float* asrc = A + (long)min(m0 + urow, p.M - 1) * p.lda + 8 * uq;
-  const unsigned short* wsrc = W + (long)min(n0 + urow, p.N - 1) * p.ldb + 8 * uq;
-  struct Stage {
-    u32x4 a[2];   // vector types: an inline-asm operand cannot be a struct
-    u32x4 w[3];
-  } s0, s1;
-  const int nk = p.K / 32;
-  // the stage loads are inline asm: hipcc's waitcnt pass does not see them, so it cannot merge the two
-  // register sets' pending loads at the loop header and drain vmcnt(0) (it did: profiles/r03/
-  // x6_pingpong.txt); the wait before a set is stored is explicit, vmcnt(5) = the other set's five
-  // loads stay in flight, and it names the set's registers as operands so no use moves above it
-  auto load = [&](Stage& s, int t) {
-    const int k0 = 32 * min(t, nk - 1);   // unconditional (clamped re-read)
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(s.a[0]) : "v"(asrc + k0));
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(s.a[1]) : "v"(asrc + k0 + 4));
-#pragma unroll
-    for (int pl = 0; pl < 3; ++pl) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(s.w[pl]) : "v"(wsrc + pl * plane + k0));
-  };
-  auto landed = [&](Stage& s) {
-    asm volatile("s_waitcnt vmcnt(5)" : "+v"(s.a[0]), "+v"(s.a[1]), "+v"(s.w[0]), "+v"(s.w[1]), "+v"(s.w[2]));
-  };
-  auto store = [&](const Stage& s, uint4* S) {
-    uint4 h, m, l;
-    split3_quad(__builtin_bit_cast(float4, s.a[0]), __builtin_bit_cast(float4, s.a[1]), h, m, l);
-    S[0 * PA + uq * BM + urow] = h;
-    S[1 * PA + uq * BM + urow] = m;
-    S[2 * PA + uq * BM + urow] = l;
-#pragma unroll
-    for (int pl = 0; pl < 3; ++pl) S[3 * PA + pl * PB + uq * BN + urow] = __builtin_bit_cast(uint4, s.w[pl]);
-  };
-  auto compute = [&](const uint4* S) {
-    const int q = lane >> 4;
-    bf16x8_t bf[3][TN];
-#pragma unroll
-    for (int pl = 0; pl < 3; ++pl)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        bf[pl][j] = __builtin_bit_cast(bf16x8_t, S[3 * PA + pl * PB + q * BN + wn + 16 * j + (lane & 15)]);
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      bf16x8_t af[3];
-#pragma unroll
-      for (int pl = 0; pl < 3; ++pl)
-        af[pl] = __builtin_bit_cast(bf16x8_t, S[pl * PA + q * BM + wm + 16 * i + (lane & 15)]);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        floatx4& sm = small[i][j];
-        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bf[1][j], sm, 0, 0, 0);
-        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[2][j], sm, 0, 0, 0);
-        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2], bf[0][j], sm, 0, 0, 0);
-        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[1][j], sm, 0, 0, 0);
-        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bf[0][j], sm, 0, 0, 0);
-        big[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[0][j], big[i][j], 0, 0, 0);
-      }
-    }
-  };
-  // prologue: stage 0 staged by both groups into buffer 0; stage 1 in s1, stage 2 in s0
-  load(s0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" : "+v"(s0.a[0]), "+v"(s0.a[1]), "+v"(s0.w[0]), "+v"(s0.w[1]), "+v"(s0.w[2]));
-  store(s0, smem);
-  load(s1, 1);
-  load(s0, 2);
-  __syncthreads();
-  if (grp == 1) __builtin_amdgcn_s_barrier();   // group 1 runs half a step behind
-  // step t: X holds stage t+1 (stored this step into buffer (t+1) % 3, then reloaded with stage t+3)
-  int bc = 0, bn = 1;   // buffers of stages t and t+1
-#define X6P_STEP(X, T)                                                                                      \
-  {                                                                                                         \
-    landed(X);                                                                                              \
-    store(X, smem + bn * STAGE);                                                                            \
-    load(X, (T) + 3);                                                                                       \
-    __syncthreads();                                                                                        \
-    compute(smem + bc * STAGE);                                                                             \
-    __syncthreads();                                                                                        \
-    bc = bn;                                                                                                \
-    bn = bn == 2 ? 0 : bn + 1;                                                                              \
-  }
-  for (int t = 0; t < nk; t += 2) {
-    X6P_STEP(s1, t);
-    if (t + 1 >= nk) break;
-    X6P_STEP(s0, t + 1);
-  }
-#undef X6P_STEP
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the clamped tail loads, before the epilogue's own
-  if (grp == 0) __builtin_amdgcn_s_barrier();   // pairs with group 1's last barrier
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -2437,8 +2253,6 @@ extern "C" int dasa_gemm_bf16(const dasa_gemm_desc* d, void* stream) {
     case 8: hipLaunchKernelGGL((gemm_bf16_nt_kernel<128, 128, 4, 2, 2>), grid, dim3(512), 0, st, p); break;
     case 9: hipLaunchKernelGGL((gemm_bf16_nt_kernel<256, 256, 4, 4>), grid, dim3(1024), 0, st, p); break;
     case 10: hipLaunchKernelGGL((gemm_bf16_nt_kernel<128, 256, 2, 4, 2>), grid, dim3(512), 0, st, p); break;
-    case 11: hipLaunchKernelGGL((gemm_bf16_nt_kernel<128, 128, 4, 2, 2, true>), grid, dim3(512), 0, st, p); break;
-    case 12: hipLaunchKernelGGL((gemm_bf16_nt_kernel<256, 256, 4, 4, 2, true>), grid, dim3(1024), 0, st, p); break;
     default: hipLaunchKernelGGL((gemm_bf16_nt_kernel<128, 128, 2, 2>), grid, dim3(256), 0, st, p); break;
   }
   DASA_CHECK_LAUNCH();
@@ -2446,7 +2260,10 @@ extern "C" int dasa_gemm_bf16(const dasa_gemm_desc* d, void* stream) {
 }
 
 // bf16x6 plan: forms 0..9 = tile / accumulator / prefetch variants, 15 = 128x128 one accumulator, 16 =
-// all-DMA 128x128 (3 x 40 KB ring; 256x128 would need 168 KB), 17 = ping-pong 128x128, 18 = form 8 with asm stage loads (sweeps: dasa_gemm_force_config(kX6Force + cfg + 32 * splitk)). Default: 128x128 tiles, separate small-term accumulator, two register
+// all-DMA 128x128 (3 x 40 KB ring; 256x128 would need 168 KB) (sweeps: dasa_gemm_force_config(kX6Force +
+// cfg + 32 * splitk)). r03 also measured and removed a ping-pong form (wave groups offset by half a K
+// step) and inline-asm stage loads: 0.90-0.98x form 8 (profiles/r03/x6_forms_pp_asm.txt). Default:
+// 128x128 tiles, separate small-term accumulator, two register
 // stages of prefetch (form 8) — the fastest accurate form on every shape with >= 128 output tiles
 // (profiles/r02/gemm_x6_sweep_b.txt: 136-178 fp32-equivalent TFLOP/s on the 1600- to 20480-row
 // language / LXRT / LSTM shapes). Fewer tiles (the 720- / 1600-row LXRT and vision GEMMs: 36-108
@@ -2567,8 +2384,6 @@ extern "C" int dasa_gemm_f32x6_ws(const dasa_gemm_desc* d, int64_t plane, void* 
     case 9: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true, 3>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
     case 15: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, false, 2>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
     case 16: hipLaunchKernelGGL((gemm_f32x6_dma_kernel<128, 128, 4, 2>), grid, dim3(512), 0, st, p, (long)plane); break;
-    case 17: hipLaunchKernelGGL((gemm_f32x6_pp_kernel<128, 128>), grid, dim3(512), 0, st, p, (long)plane); break;
-    case 18: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true, 2, false, 0, true>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
     default: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
   }
   DASA_CHECK_LAUNCH();

@@ -393,6 +393,33 @@ def test_bilstm(dev, B, L, mode):
         lib.dasa_bilstm_set_mode(0)
 
 
+@pytest.mark.parametrize("B,L", [(40, 9), (700, 16)])
+def test_bilstm_bptt_x6_vs_native(dev, B, L):
+    """The B > 32 BPTT's recurrent product on the bf16x6 GEMM (default) against dasa_gemm_f32: the
+    dgates of every step agree to fp32 rounding (both are fp32-accurate; errors compound over steps)."""
+    from dasa_amd import _lib, ops
+    lib = _lib.lib()
+    torch.manual_seed(7)
+    H = 1024
+    whh_f, whh_b = [(torch.rand(4 * H, H, device=dev) - 0.5) * 0.1 for _ in range(2)]
+    xproj = torch.randn(B, L, 2, 4 * H, device=dev)
+    li = torch.randint(1, L + 1, (B,)).sort(descending=True)[0].to(torch.int32).to(dev)
+    out, h_n, c_n, saved = ops.bilstm_fwd(xproj, whh_f, whh_b, li, H, save=True)
+    gout = torch.randn(B, L, 2 * H, device=dev)
+    ghn, gcn = torch.randn(2, B, H, device=dev), torch.randn(2, B, H, device=dev)
+    prev = lib.dasa_bilstm_bptt_x6(1)
+    try:
+        dg6 = ops.bilstm_bwd(whh_f, whh_b, li, saved, gout, ghn, gcn, H)
+        lib.dasa_bilstm_bptt_x6(0)
+        dgn = ops.bilstm_bwd(whh_f, whh_b, li, saved, gout, ghn, gcn, H)
+    finally:
+        lib.dasa_bilstm_bptt_x6(prev)
+    torch.cuda.synchronize()
+    assert torch.isfinite(dg6).all()
+    scale = dgn.abs().max().item()
+    assert (dg6 - dgn).abs().max().item() < 2e-5 * scale
+
+
 def _check_bilstm(dev, B, L):
     from dasa_amd import ops
     torch.manual_seed(B + L)
@@ -684,7 +711,7 @@ def test_gemm_bf16(dev, M, N, K):
     b = _rand(N, g=g)
     xb, Wb = x.to(torch.bfloat16).double(), W.to(torch.bfloat16).double()
     L = _lib.lib()
-    for cfg in [(1 << 20) + c for c in range(13)] + [-1]:
+    for cfg in [(1 << 20) + c for c in range(11)] + [-1]:
         L.dasa_gemm_force_config(cfg)
         try:
             with torch.no_grad(), ops.bf16_matmul():
@@ -761,7 +788,7 @@ def test_gemm_f32x6(dev, M, N, K):
     err_nat = (out_nat.cpu().double() - ref).abs().max().item()
     try:
         outs = {}
-        for cfg in list(range(10)) + [15, 16, 17, 18]:
+        for cfg in list(range(10)) + [15, 16]:
             lib.dasa_gemm_force_config((1 << 21) + cfg)
             y = torch.empty(M, N, device=dev)
             ops.gemm_f32x6(Ad, planes, y, M=M, N=N, K=K, lda=K + 8, ldc=N, bias=bias.to(dev))
@@ -775,13 +802,12 @@ def test_gemm_f32x6(dev, M, N, K):
                            aux=aux.to(dev), ld_aux=N, colscale=cs.to(dev), beta=0.5)
             want = torch.sigmoid(ref) * aux.double() * cs.double() + 0.5 * c0.double()
             assert (y2.cpu().double() - want).abs().max().item() < 1e-5, cfg
-        # forms 16-18 run form 8's products in form 8's order: bitwise equal to form 8 without split-K (the
+        # form 16 runs form 8's products in form 8's order: bitwise equal to form 8 without split-K (the
         # forced form-8 run above may split K on few-tile shapes)
         lib.dasa_gemm_force_config((1 << 21) + 8 + 32 * 1)
         y8 = torch.empty(M, N, device=dev)
         ops.gemm_f32x6(Ad, planes, y8, M=M, N=N, K=K, lda=K + 8, ldc=N, bias=bias.to(dev))
-        for cfg in (16, 17, 18):   # all-DMA, ping-pong, asm-load forms: form 8's products in form 8's order
-            assert torch.equal(outs[cfg], y8.cpu()), cfg
+        assert torch.equal(outs[16], y8.cpu())   # all-DMA form: form 8's products in form 8's order
     finally:
         lib.dasa_gemm_force_config(-1)
 

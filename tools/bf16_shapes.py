@@ -26,7 +26,7 @@ def main():
         W = torch.randn(N, K, device=dev) * 0.05
         b = torch.randn(N, device=dev)
         y = torch.empty(M, N, device=dev)
-        with ops.bf16_matmul():
+        with torch.no_grad(), ops.bf16_matmul():
             us = _time_graph(lambda: ops.linear(x, W, b, out=y), reps=20)
             line = f"{M:>6}x{N:>5}x{K:>5}  {us:8.1f} us  {2.0 * M * N * K / us / 1e6:6.1f} TF"
             ref = y.clone()
