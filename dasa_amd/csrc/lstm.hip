@@ -454,14 +454,32 @@ static dasa_gemm_desc bptt_rec_desc(int B, int L, int H) {
   d.alpha = 1.f; d.beta = 0.f;
   return d;
 }
+// The recurrent product on the bf16x6 fp32 GEMM (dasa_gemm_f32x6_ws: fp32-accurate, 1.5-2x the native
+// fp32 MFMA kernels on these few-tile long-K shapes through its split-K form) with W_hh^T pre-split into
+// three bf16 planes [3][2][H][4H] once per call. DASA_BPTT_X6=0 (or DASA_GEMM_EMU=0) keeps dasa_gemm_f32.
+static int g_bptt_x6 = -1;
+static bool bptt_x6() {
+  if (g_bptt_x6 < 0) {
+    const char* e = getenv("DASA_BPTT_X6");
+    const char* g = getenv("DASA_GEMM_EMU");
+    g_bptt_x6 = !(e && e[0] == '0') && !(g && g[0] == '0');
+  }
+  return g_bptt_x6 != 0;
+}
+extern "C" int dasa_bilstm_bptt_x6(int32_t on) {
+  const int prev = bptt_x6() ? 1 : 0;
+  if (on >= 0) g_bptt_x6 = on ? 1 : 0;
+  return prev;
+}
 static long bptt_gemm_ws_floats(int B, int L, int H) {
   dasa_gemm_desc d = bptt_rec_desc(B, L, H);
-  return (dasa_gemm_f32_workspace(&d) + 15) / 4 + 4;
+  const int64_t f = dasa_gemm_f32_workspace(&d), x = dasa_gemm_f32x6_workspace(&d);
+  return ((f > x ? f : x) + 15) / 4 + 4;
 }
 
 extern "C" int64_t dasa_bilstm_bwd_workspace(int32_t B, int32_t H) {
-  if (B > 32)   // carries + rec, W_hh^T of both directions, GEMM workspace (L does not change its size)
-    return (int64_t)((6L * B * H + 8L * H * H + 8 + bptt_gemm_ws_floats(B, 1, H)) * sizeof(float));
+  if (B > 32)   // carries + rec, W_hh^T of both directions (fp32 + three bf16 planes), GEMM workspace
+    return (int64_t)((6L * B * H + 8L * H * H + 12L * H * H + 16 + bptt_gemm_ws_floats(B, 1, H)) * sizeof(float));
   return (int64_t)((4L * B * H + 8L * H * H) * sizeof(float));
 }
 
@@ -488,7 +506,8 @@ extern "C" int dasa_bilstm_bwd(const float* whh_fwd, const float* whh_bwd, const
     DASA_CHECK_LAUNCH();
     float* wt = rec + S;
     wt += (16 - ((uintptr_t)wt & 15) / 4) % 4;            // 16-B aligned W_hh^T [2][H][4H]
-    float* gws = wt + 8L * H * H;
+    uint16_t* planes = reinterpret_cast<uint16_t*>(wt + 8L * H * H);   // [3][2][H][4H] bf16, 16-B aligned
+    float* gws = wt + 8L * H * H + 12L * H * H;
     gws += (16 - ((uintptr_t)gws & 15) / 4) % 4;
     const long gws_floats = bptt_gemm_ws_floats(B, L, H) - 4;
     hipLaunchKernelGGL(fill_kernel, dim3(64), dim3(256), 0, st, gws, 16384L, 0.f);   // GEMM arrival counters
@@ -498,6 +517,11 @@ extern "C" int dasa_bilstm_bwd(const float* whh_fwd, const float* whh_bwd, const
     hipLaunchKernelGGL(transpose_kernel, dim3(H / 32, 4 * H / 32), dim3(256), 0, st, whh_bwd, wt + 4L * H * H,
                        4 * H, H);
     DASA_CHECK_LAUNCH();
+    const bool x6 = bptt_x6();
+    if (x6) {
+      const int rc = dasa_f32_split3_bf16(wt, 4L * H, planes, 2 * H, 4 * H, stream);
+      if (rc) return rc;
+    }
     BpttArgs a{nullptr, nullptr, lengths, save_act, save_c, dout, dgates, dh, dc, B, L, H};
     for (int s = 0; s < L; ++s) {
       if (s > 0) {   // both directions in one launch: dir 0 reads step t+1 = L-s, dir 1 step t-1 = s-1
@@ -505,9 +529,15 @@ extern "C" int dasa_bilstm_bwd(const float* whh_fwd, const float* whh_bwd, const
         const long a0 = ((long)(L - s) * 2 + 0) * 4 * H, a1 = ((long)(s - 1) * 2 + 1) * 4 * H;
         d.A = dgates + a0;
         d.strideA = a1 - a0;
-        d.B = wt;
         d.C = rec;
-        const int rc = dasa_gemm_f32(&d, gws, gws_floats * (int64_t)sizeof(float), stream);
+        int rc;
+        if (x6) {
+          d.B = reinterpret_cast<const float*>(planes);   // hi plane; mid / lo 8H^2 on, direction 1 at +4H^2
+          rc = dasa_gemm_f32x6_ws(&d, 8L * H * H, gws, gws_floats * (int64_t)sizeof(float), stream);
+        } else {
+          d.B = wt;
+          rc = dasa_gemm_f32(&d, gws, gws_floats * (int64_t)sizeof(float), stream);
+        }
         if (rc) return rc;
       }
       hipLaunchKernelGGL(bilstm_bptt_cell_kernel, dim3(cdivi(S, 256)), dim3(256), 0, st, a, (const float*)rec, s);

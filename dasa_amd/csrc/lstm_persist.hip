@@ -22,6 +22,7 @@
 // sync point and raises on (dasa_amd.ops.check_device_errors).
 #include "common.h"
 #include "lstm_internal.h"
+#include <cstdlib>
 
 namespace {
 
@@ -111,14 +112,56 @@ __device__ __forceinline__ void stamp(unsigned long long* buf, int i) {
   }
 }
 
+// bf16x6 recurrent product (X6): h and the W_hh slice split exactly into three bf16 planes each
+// (x = hi + mid + lo), the six kept products (hh, hm, mh, hl, lh, mm) on v_mfma_f32_16x16x32_bf16 —
+// fp32-accurate, as gemm.hip's gemm_f32x6_nt_kernel — at 6/16 of the 32x32x2 f32 MFMA cycles per FLOP.
+typedef short bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned pk_bf16(float a, float b) {
+  const f32x2_t w = {a, b};
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(w, bf16x2_t));
+}
+__device__ __forceinline__ void split3_pair(float a, float b, unsigned& h, unsigned& m, unsigned& l) {
+  h = pk_bf16(a, b);
+  const float ra = a - __uint_as_float(h << 16), rb = b - __uint_as_float(h & 0xffff0000u);
+  m = pk_bf16(ra, rb);
+  l = pk_bf16(ra - __uint_as_float(m << 16), rb - __uint_as_float(m & 0xffff0000u));
+}
+// 8 consecutive fp32 (x then y) -> the three bf16x8 planes
+__device__ __forceinline__ void split3_8(const float4& x, const float4& y, bf16x8_t (&o)[3]) {
+  unsigned h0, h1, h2, h3, m0, m1, m2, m3, l0, l1, l2, l3;
+  split3_pair(x.x, x.y, h0, m0, l0);
+  split3_pair(x.z, x.w, h1, m1, l1);
+  split3_pair(y.x, y.y, h2, m2, l2);
+  split3_pair(y.z, y.w, h3, m3, l3);
+  o[0] = __builtin_bit_cast(bf16x8_t, u32x4{h0, h1, h2, h3});
+  o[1] = __builtin_bit_cast(bf16x8_t, u32x4{m0, m1, m2, m3});
+  o[2] = __builtin_bit_cast(bf16x8_t, u32x4{l0, l1, l2, l3});
+}
+// b: the hi and mid planes (VGPRs), blo: the lo plane (read back from LDS)
+__device__ __forceinline__ void mfma_x6(const bf16x8_t (&a)[3], const bf16x8_t (&b)[2], const bf16x8_t& blo,
+                                        floatx4& big, floatx4& sm) {
+  sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], sm, 0, 0, 0);
+  sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], blo, sm, 0, 0, 0);
+  sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], sm, 0, 0, 0);
+  sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], sm, 0, 0, 0);
+  sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], sm, 0, 0, 0);
+  big = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], big, 0, 0, 0);
+}
+
 // NG = H / 128: K-groups of 8 per wave (the wave's K slice is H / 16). NBT = 32-row batch tiles
 // (B <= 32 * NBT): every timestep runs the MFMA pass, the 16-wave reduction and the cell update once
 // per tile, then ONE direction barrier. Thread i < 256 owns (row i / 8 of every tile, unit i % 8); the
 // c / h state of tiles past the first lives in LDS (registers are capped at 128 per lane here).
-template <int NG, int NBT>
+// X6: the recurrent product on bf16 MFMA (above); the wave's K slice is KS = NG / 4 steps of 32, its
+// 32 x 32 output four 16 x 16 tiles; the W_hh slice is split into three bf16 planes once: hi and mid
+// live in VGPRs (32), lo in LDS (64 KB per workgroup, lane-linear, read back per product).
+template <int NG, int NBT, bool X6 = false>
 __global__ __launch_bounds__(1024) void bilstm_persist_fwd_kernel(PFwd a) {
   __shared__ __attribute__((aligned(16))) float smem[PW * 1024 + 4];
   __shared__ float cst[NBT > 1 ? NBT * 256 : 1], hst[NBT > 1 ? NBT * 256 : 1];
+  __shared__ uint4 wlo_s[X6 ? PW * 2 * (NG / 4) * 64 : 1];   // X6: [wave][j][K step][lane]
   const int H = a.H, B = a.B, L = a.L, G = H / PU;
   const int dir = blockIdx.x / G, u0 = (blockIdx.x % G) * PU;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -126,10 +169,29 @@ __global__ __launch_bounds__(1024) void bilstm_persist_fwd_kernel(PFwd a) {
   const int k0 = w * (8 * NG);
   // This workgroup's 32 W_hh rows (gate q = n / 8 of unit u0 + n % 8), this wave's K slice, in the
   // 32x32x2 B-operand layout with the K-permuted float4 per lane (k = 8g + 4hh + e feeds MFMA e).
-  const float* wp = (dir ? a.whh1 : a.whh0) + ((long)(n / PU) * H + u0 + (n % PU)) * H + k0 + 4 * hh;
-  float4 wf[NG];
+  constexpr int KS = X6 ? NG / 4 : 1;
+  static_assert(!X6 || (NG % 4 == 0), "X6: the wave's K slice is whole 32-deep steps");
+  float4 wf[X6 ? 1 : NG];
+  bf16x8_t wx[X6 ? 2 : 1][KS][2];   // X6: [16-column tile j][K step][hi, mid]; lane: col l & 15, k 8(l >> 4)..+7
+  if constexpr (!X6) {
+    const float* wp = (dir ? a.whh1 : a.whh0) + ((long)(n / PU) * H + u0 + (n % PU)) * H + k0 + 4 * hh;
 #pragma unroll
-  for (int g = 0; g < NG; ++g) wf[g] = *reinterpret_cast<const float4*>(wp + 8 * g);
+    for (int g = 0; g < NG; ++g) wf[g] = *reinterpret_cast<const float4*>(wp + 8 * g);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int nn = 16 * j + (lane & 15);
+      const float* wp = (dir ? a.whh1 : a.whh0) + ((long)(nn / PU) * H + u0 + (nn % PU)) * H + k0 + 8 * (lane >> 4);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        bf16x8_t t[3];
+        split3_8(*reinterpret_cast<const float4*>(wp + 32 * ks), *reinterpret_cast<const float4*>(wp + 32 * ks + 4), t);
+        wx[j][ks][0] = t[0];
+        wx[j][ks][1] = t[1];
+        wlo_s[((w * 2 + j) * KS + ks) * 64 + lane] = __builtin_bit_cast(uint4, t[2]);   // own slot: no barrier
+      }
+    }
+  }
 
   const bool own = threadIdx.x < 32 * PU;
   const int oi = threadIdx.x / PU, ou = threadIdx.x % PU, uj = u0 + ou;   // row in tile, unit
@@ -147,31 +209,74 @@ __global__ __launch_bounds__(1024) void bilstm_persist_fwd_kernel(PFwd a) {
     const int t = dir == 0 ? s : L - 1 - s;
     const float* hin = a.hbuf + (long)((s & 1) * 2 + dir) * B * H;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)hin, (short)0, B * H * 4, 0x00020000);
-#pragma unroll
+#pragma unroll(X6 ? 1 : NBT)   // X6 unrolled over tiles spills (the compiler hoists the next tile's loads)
     for (int bt = 0; bt < NBT; ++bt) {
       if (bt * 32 >= B) break;   // uniform
-      floatx16 acc;
+      if constexpr (!X6) {
+        floatx16 acc;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-      if (s > 0) {   // h_0 = 0: the first step has no recurrent term
-        const int row = bt * 32 + b, bc = min(row, B - 1);
-        const bool bval = row < B;
-        float4 hf[NG];
+        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+        if (s > 0) {   // h_0 = 0: the first step has no recurrent term
+          const int row = bt * 32 + b, bc = min(row, B - 1);
+          const bool bval = row < B;
+          float4 hf[NG];
 #pragma unroll
-        for (int g = 0; g < NG; ++g) hf[g] = selz(bval, ld_sc1(rs, (bc * H + k0 + 8 * g + 4 * hh) * 4));
+          for (int g = 0; g < NG; ++g) hf[g] = selz(bval, ld_sc1(rs, (bc * H + k0 + 8 * g + 4 * hh) * 4));
 #pragma unroll
-        for (int g = 0; g < NG; ++g)
+          for (int g = 0; g < NG; ++g)
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(f4e(hf[g], e), f4e(wf[g], e), acc, 0, 0, 0);
+            for (int e = 0; e < 4; ++e)
+              acc = __builtin_amdgcn_mfma_f32_32x32x2f32(f4e(hf[g], e), f4e(wf[g], e), acc, 0, 0, 0);
+        }
+        // C[b][n] partial over this wave's K slice: lane -> col n, reg r -> row (r&3) + 8(r>>2) + 4hh
+        if (bt == 0) {
+          asm volatile("" :: "v"(acc[0]));
+          stamp(a.stamps, 8 * s + 1);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) smem[w * 1024 + r * 64 + lane] = acc[r];
+      } else {
+        floatx4 big[2][2], sml[2][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) big[i][j] = sml[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        if (s > 0) {
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) {
+            float4 hx[2][2];   // [16-row tile i][half]: row l & 15 of tile i, k 8(l >> 4)..+7 of step ks
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+              const int row = bt * 32 + 16 * i + (lane & 15), bc = min(row, B - 1);
+              const int off = (bc * H + k0 + 32 * ks + 8 * (lane >> 4)) * 4;
+              hx[i][0] = selz(row < B, ld_sc1(rs, off));
+              hx[i][1] = selz(row < B, ld_sc1(rs, off + 16));
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+              bf16x8_t ha[3];
+              split3_8(hx[i][0], hx[i][1], ha);
+#pragma unroll
+              for (int j = 0; j < 2; ++j)
+                mfma_x6(ha, wx[j][ks], __builtin_bit_cast(bf16x8_t, wlo_s[((w * 2 + j) * KS + ks) * 64 + lane]),
+                        big[i][j], sml[i][j]);
+            }
+          }
+        }
+        if (bt == 0) {
+          asm volatile("" :: "v"(big[0][0][0]));
+          stamp(a.stamps, 8 * s + 1);
+        }
+        // C[b][n] partial, natural [b][n] layout: tile (i, j), lane -> col 16j + (l & 15), reg r -> row
+        // 16i + 4(l >> 4) + r
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              smem[w * 1024 + (16 * i + 4 * (lane >> 4) + r) * 32 + 16 * j + (lane & 15)] = big[i][j][r] + sml[i][j][r];
       }
-      // C[b][n] partial over this wave's K slice: lane -> col n, reg r -> row (r&3) + 8(r>>2) + 4hh
-      if (bt == 0) {
-        asm volatile("" :: "v"(acc[0]));
-        stamp(a.stamps, 8 * s + 1);
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) smem[w * 1024 + r * 64 + lane] = acc[r];
       __syncthreads();
       if (bt == 0) stamp(a.stamps, 8 * s + 2);
       {   // sum the 16 wave partials: thread i owns element i of the 32x32 tile
@@ -183,11 +288,11 @@ __global__ __launch_bounds__(1024) void bilstm_persist_fwd_kernel(PFwd a) {
       __syncthreads();
       const int ob = bt * 32 + oi;
       if (own && ob < B) {
-        const int rr = (oi & 3) + 4 * (oi >> 3), lh = ((oi >> 2) & 1) * 32;
+        const int rr = (oi & 3) + 4 * (oi >> 3), lh = ((oi >> 2) & 1) * 32;   // (32x32x2 C layout)
         const float* xp = a.xproj + (((long)ob * L + t) * 2 + dir) * 4 * H;
         float gq[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) gq[q] = xp[q * H + uj] + smem[rr * 64 + lh + q * PU + ou];
+        for (int q = 0; q < 4; ++q) gq[q] = xp[q * H + uj] + smem[X6 ? oi * 32 + q * PU + ou : rr * 64 + lh + q * PU + ou];
         float* outp = a.out + ((long)ob * L + t) * 2 * H + dir * H + uj;
         float* sa = a.save_act ? a.save_act + (((long)t * 2 + dir) * B + ob) * 4 * H : nullptr;
         float c = NBT > 1 ? cst[bt * 256 + threadIdx.x] : c1;
@@ -433,12 +538,35 @@ bool bilstm_persist_fwd_ok(int B, int H) {
   return bilstm_persist_ok(B, H) || (H == 1024 && B >= 1 && B <= 192);
 }
 
+// X6 recurrence switch (dasa_bilstm_fwd_x6; env DASA_LSTM_X6=0 or DASA_GEMM_EMU=0 start it off)
+static int g_fwd_x6 = -1;
+static bool fwd_x6() {
+  if (g_fwd_x6 < 0) {
+    const char* e = getenv("DASA_LSTM_X6");
+    const char* g = getenv("DASA_GEMM_EMU");
+    g_fwd_x6 = !(e && e[0] == '0') && !(g && g[0] == '0');
+  }
+  return g_fwd_x6 != 0;
+}
+extern "C" int dasa_bilstm_fwd_x6(int32_t on) {
+  const int prev = fwd_x6() ? 1 : 0;
+  if (on >= 0) g_fwd_x6 = on ? 1 : 0;
+  return prev;
+}
+
 int bilstm_persist_fwd(const float* xproj, const float* whh_fwd, const float* whh_bwd, const int32_t* lengths,
                        float* out, float* h_n, float* c_n, float* save_act, float* save_c, int B, int L, int H,
                        float* hbuf, unsigned* sync, hipStream_t st) {
   PFwd a{xproj, whh_fwd, whh_bwd, lengths, out, save_act, save_c, h_n, c_n, hbuf, sync, g_err_word, g_force_tmo,
          B, L, H, g_stamps};
   const int grid = 2 * H / PU;
+  // X6 at one or two 32-row tiles only (profiles/r03/lstm_x6_probe.txt, L = 80: B = 20 0.69-0.74 vs 0.76
+  // ms, B = 40 1.03-1.05 vs 1.16-1.20; B = 96 / 160 3-5 % slower, the tile loop then spills): the step
+  // is bound by the h-state hand-off latency and the direction barrier more than by the MFMA cycles
+  if (H == 1024 && B <= 64 && fwd_x6()) {
+    if (B > 32) return launch_persistent(bilstm_persist_fwd_kernel<8, 2, true>, grid, a, st);
+    return launch_persistent(bilstm_persist_fwd_kernel<8, 1, true>, grid, a, st);
+  }
   if (B > 32) {
     if (H != 1024 || B > 192) return (int)hipErrorInvalidValue;
     switch ((B + 31) / 32) {

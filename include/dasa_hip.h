@@ -202,6 +202,14 @@ int dasa_bilstm_bwd(const float* whh_fwd, const float* whh_bwd, const int32_t* l
  * per sequence when B <= 32 and H is a multiple of 256 up to 1024, else one launch per timestep),
  * 1 = per-timestep launches only, 2 = persistent only (error when not eligible). Host-only setting. */
 int dasa_bilstm_set_mode(int mode);
+/* B > 32 BPTT recurrent product (dgates_prev . W_hh per timestep): 1 = the bf16x6 fp32 GEMM on W_hh^T
+ * pre-split per call (default; env DASA_BPTT_X6=0 or DASA_GEMM_EMU=0 start at 0), 0 = dasa_gemm_f32;
+ * < 0 only queries. Returns the previous setting. Host-only.                                     */
+int dasa_bilstm_bptt_x6(int32_t on);
+/* Persistent forward recurrence at H = 1024, B <= 64: 1 = recurrent product as bf16x6 (three exact bf16 planes of
+ * h and W_hh, six products on bf16 MFMA; fp32-accurate; default; env DASA_LSTM_X6=0 or DASA_GEMM_EMU=0
+ * start at 0), 0 = native fp32 MFMA; < 0 only queries. Returns the previous setting. Host-only.   */
+int dasa_bilstm_fwd_x6(int32_t on);
 /* Error word for failures that a kernel can only detect on the device (no host sync inside a call):
  * a persistent bi-LSTM launch whose inter-workgroup barrier times out (a workgroup was not
  * co-resident) ORs 1 (forward) / 2 (BPTT) into *dev_word and fills its outputs with NaN; a D-split

@@ -379,6 +379,22 @@ def test_lstm_cell(dev):
     assert (dg.cpu() - gates.grad).abs().max() < 1e-5 and (dc0.cpu() - c0.grad).abs().max() < 1e-5
 
 
+@pytest.mark.parametrize("x6", [0, 1])
+@pytest.mark.parametrize("B,L", [(20, 80), (3, 11), (40, 9), (160, 12)])
+def test_bilstm_persist_fwd_x6(dev, B, L, x6):
+    """The persistent forward with the recurrent product as bf16x6 (default at H = 1024) and as native
+    fp32 MFMA: both against torch's packed nn.LSTM (fp32, CPU) at the tolerance of test_bilstm."""
+    from dasa_amd import _lib
+    lib = _lib.lib()
+    assert lib.dasa_bilstm_set_mode(2) == 0
+    prev = lib.dasa_bilstm_fwd_x6(x6)
+    try:
+        _check_bilstm(dev, B, L)
+    finally:
+        lib.dasa_bilstm_fwd_x6(prev)
+        lib.dasa_bilstm_set_mode(0)
+
+
 @pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("B,L", [(20, 80), (3, 11), (40, 9), (160, 12)])
 def test_bilstm(dev, B, L, mode):
