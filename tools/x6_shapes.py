@@ -12,7 +12,8 @@ from dasa_amd import _lib, ops  # noqa: E402
 from dasa_amd.kbench import _time_graph  # noqa: E402
 
 SHAPES = [(12800, 3072, 768), (12800, 2304, 768), (12800, 768, 3072), (12800, 768, 768), (1600, 3072, 768),
-          (1600, 768, 3072), (720, 3072, 768), (720, 768, 3072), (1600, 4096, 768), (720, 2048, 2048)]
+          (1600, 768, 3072), (720, 3072, 768), (720, 768, 3072), (1600, 4096, 768), (720, 2048, 2048),
+          (1600, 768, 768), (720, 768, 768), (720, 1536, 768), (720, 2304, 768)]
 
 
 def main():
