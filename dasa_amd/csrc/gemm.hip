@@ -1150,8 +1150,13 @@ struct X6Split { unsigned* cnt; float* slab; int splitk, kchunk; };
 // lets it use 256 VGPRs instead of spilling to reach an occupancy the LDS forbids)
 // PRIO (A/B forms 10-13): 1 = s_setprio(1) around every MFMA cluster (cdna_hip_programming.md T5),
 // 2 = one static s_setprio(1) for the second half of the workgroup's waves (T5 static form).
+// PF = -1 (form 20): ONE LDS stage (48 KB at 128 x 128) and one register stage, two barriers per K step,
+// at most 128 registers (waves_per_eu 4): two workgroups share a CU and overlap each other's split / LDS
+// phase with their MFMAs — form 8's products in form 8's order (bitwise equal), 1.07-1.14x the previous
+// plan on the many-tile K = 768, N >= 2048 shapes (profiles/r03/x6_lds1_forms.txt).
 template <int BM, int BN, int WAVES_M, int WAVES_N, bool SEP, int PF = 1, bool SPL = false, int PRIO = 0>
-__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) __attribute__((amdgpu_waves_per_eu(1, 2)))
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N)
+__attribute__((amdgpu_waves_per_eu(PF < 0 ? 4 : 1, PF < 0 ? 4 : 2)))
 void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
   constexpr int NT = 64 * WAVES_M * WAVES_N;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N, TM = WM / 16, TN = WN / 16;
@@ -1159,7 +1164,7 @@ void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
   static_assert((BM * 4) % NT == 0 && (BN * 4) % NT == 0, "tile quads must split evenly");
   constexpr int PA = BM * 4, PB = BN * 4;               // uint4 per plane image
   constexpr int STAGE = 3 * (PA + PB);
-  __shared__ uint4 smem[2 * STAGE];
+  __shared__ uint4 smem[(PF < 0 ? 1 : 2) * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (PRIO == 2 && __builtin_amdgcn_readfirstlane(tid) >= NT / 2) __builtin_amdgcn_s_setprio(1);
@@ -1272,7 +1277,17 @@ void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
 
   const int nk = (SPL ? min(xs.kchunk, p.K - kb) : p.K) / 32;
   stg.load(p, A, W, plane, m0, n0, 0, tid);
-  if (PF == 1) {
+  if (PF < 0) {
+    stg.store(smem, tid);
+    __syncthreads();
+    for (int t = 0; t < nk; ++t) {
+      stg.load(p, A, W, plane, m0, n0, 32 * min(t + 1, nk - 1), tid);   // unconditional (clamped re-read)
+      compute(smem);
+      __syncthreads();
+      stg.store(smem, tid);
+      __syncthreads();
+    }
+  } else if (PF == 1) {
     stg.store(smem, tid);
     __syncthreads();
     for (int t = 0; t < nk; ++t) {
@@ -2272,6 +2287,15 @@ extern "C" int dasa_gemm_bf16(const dasa_gemm_desc* d, void* stream) {
 struct X6Plan { int cfg, bm, bn, splitk, kchunk; int64_t ws; };
 
 
+static bool x6_lds1() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("DASA_X6_LDS1");
+    on = !(e && e[0] == '0');
+  }
+  return on != 0;
+}
+
 static X6Plan x6_plan(const dasa_gemm_desc* d) {
   const int M = d->M, N = d->N, K = d->K, batch = d->batch < 1 ? 1 : d->batch;
   X6Plan pl{8, 128, 128, 1, K, 0};
@@ -2280,6 +2304,10 @@ static X6Plan x6_plan(const dasa_gemm_desc* d) {
   // 12800-row language GEMMs: +4-8 % on 12800 x 2304 / 3072 x 768, slower on N = 768 and on fewer rows
   // (profiles/r02/x6_forms.txt)
   if (M >= 4096 && N >= 2048) pl.cfg = 7;
+  // form 20 (one LDS stage, two workgroups per CU) on short-K wide problems with >= 256 tiles: 12800 x
+  // {3072, 2304} x 768 1.07-1.08x form 7, 1600 x {3072, 4096} x 768 1.11-1.14x form 8; slower at K = 3072,
+  // N = 768 and below ~2 tiles per CU (profiles/r03/x6_lds1_forms.txt). DASA_X6_LDS1=0 turns it off (A/B).
+  if (K <= 1024 && N >= 2048 && (long)cdiv(M, 128) * cdiv(N, 128) * batch >= 256 && x6_lds1()) pl.cfg = 20;
   if (g_force_cfg >= kX6Force) {
     pl.cfg = (g_force_cfg - kX6Force) % 32;
     fsplit = ((g_force_cfg - kX6Force) / 32) % 64;
@@ -2384,6 +2412,7 @@ extern "C" int dasa_gemm_f32x6_ws(const dasa_gemm_desc* d, int64_t plane, void* 
     case 9: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true, 3>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
     case 15: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, false, 2>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
     case 16: hipLaunchKernelGGL((gemm_f32x6_dma_kernel<128, 128, 4, 2>), grid, dim3(512), 0, st, p, (long)plane); break;
+    case 20: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true, -1>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
     default: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
   }
   DASA_CHECK_LAUNCH();
