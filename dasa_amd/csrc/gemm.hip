@@ -2275,13 +2275,15 @@ extern "C" int dasa_gemm_bf16(const dasa_gemm_desc* d, void* stream) {
 }
 
 // bf16x6 plan: forms 0..9 = tile / accumulator / prefetch variants, 15 = 128x128 one accumulator, 16 =
-// all-DMA 128x128 (3 x 40 KB ring; 256x128 would need 168 KB) (sweeps: dasa_gemm_force_config(kX6Force +
-// cfg + 32 * splitk)). r03 also measured and removed a ping-pong form (wave groups offset by half a K
-// step) and inline-asm stage loads: 0.90-0.98x form 8 (profiles/r03/x6_forms_pp_asm.txt). Default:
-// 128x128 tiles, separate small-term accumulator, two register
-// stages of prefetch (form 8) — the fastest accurate form on every shape with >= 128 output tiles
-// (profiles/r02/gemm_x6_sweep_b.txt: 136-178 fp32-equivalent TFLOP/s on the 1600- to 20480-row
-// language / LXRT / LSTM shapes). Fewer tiles (the 720- / 1600-row LXRT and vision GEMMs: 36-108
+// all-DMA 128x128 (3 x 40 KB ring; 256x128 would need 168 KB), 20 = form 8 with one LDS stage in <= 128
+// registers (two workgroups per CU) (sweeps: dasa_gemm_force_config(kX6Force + cfg + 32 * splitk)). r03
+// also measured and removed a ping-pong form (wave groups offset by half a K step), inline-asm stage
+// loads (0.90-0.98x form 8, profiles/r03/x6_forms_pp_asm.txt) and small-tile high-occupancy forms
+// (x6_occupancy_forms_rejected.txt). Default: 128x128 tiles, separate small-term accumulator, two
+// register stages of prefetch (form 8) on every shape with >= 128 output tiles (profiles/r02/
+// gemm_x6_sweep_b.txt: 136-178 fp32-equivalent TFLOP/s on the 1600- to 20480-row language / LXRT / LSTM
+// shapes), 256x128 (form 7) on the wide >= 4096-row ones, form 20 on short-K wide ones with >= 256
+// tiles (below). Fewer tiles (the 720- / 1600-row LXRT and vision GEMMs: 36-108
 // tiles) split K over the tiles' workgroups until ~256 workgroups fill the chip, reduced in-kernel by
 // the last split to arrive (X6Split); needs the workspace.
 struct X6Plan { int cfg, bm, bn, splitk, kchunk; int64_t ws; };
