@@ -42,6 +42,27 @@ def test_gemm_workspace_query_is_host_only():
     assert _lib.lib().dasa_gemm_f32_workspace(ctypes.byref(d)) > cnt    # mid-size long K: stream-K slabs
 
 
+def test_x6_plan_and_lstm_switches_are_host_only():
+    """The bf16x6 workspace query (split-K only on few-tile problems) and the r03 bi-LSTM x6 switches
+    (set / query semantics, the large-batch BPTT workspace holding W_hh^T and its three bf16 planes)."""
+    import ctypes
+    from dasa_amd import _lib
+    L = _lib.lib()
+    d = _lib.GemmDesc()
+    d.M, d.N, d.K, d.batch, d.opA, d.opB = 720, 768, 3072, 1, 0, 1
+    assert L.dasa_gemm_f32x6_workspace(ctypes.byref(d)) > 0          # 36 tiles: K split over workgroups
+    d.M, d.N, d.K = 12800, 3072, 768
+    assert L.dasa_gemm_f32x6_workspace(ctypes.byref(d)) == 0         # 2400 tiles: one workgroup per tile
+    for hook in (L.dasa_bilstm_bptt_x6, L.dasa_bilstm_fwd_x6):
+        prev = hook(-1)
+        assert prev in (0, 1)
+        assert hook(0) == prev and hook(-1) == 0
+        assert hook(1) == 0 and hook(-1) == 1
+        hook(prev)
+    B, H = 700, 1024
+    assert L.dasa_bilstm_bwd_workspace(B, H) >= (6 * B * H + 20 * H * H) * 4
+
+
 def test_product_schema_matches_reference():
     from dasa_amd.r2r import param
     param.readme_train(["--d_vl_layers", "1"])
