@@ -2251,9 +2251,13 @@ extern "C" int dasa_gemm_bf16(const dasa_gemm_desc* d, void* stream) {
   // 256x256 tiles of 16 waves (128 KB LDS, one workgroup per CU) once there are >= 200 of them:
   // +8-25% over 128x128 on the configs[4] shapes (profiles/r02/gemm_bf16_sweep.txt)
   int cfg = cdiv(M, 256) * cdiv(N, 256) * batch >= 200 ? 9 : 2;
-  if (g_force_cfg >= kBf16Force && g_force_cfg < kX6Force) cfg = (g_force_cfg - kBf16Force) % 16;
-  const int bm = (cfg == 1 || cfg == 5 || cfg == 7 || cfg == 9 || cfg == 12) ? 256 : 128,
-            bn = cfg == 3 ? 64 : (cfg == 6 || cfg == 9 || cfg == 10 || cfg == 12) ? 256 : 128;
+  if (g_force_cfg >= kBf16Force && g_force_cfg < kX6Force) {
+    cfg = (g_force_cfg - kBf16Force) % 16;
+    if (cfg > 10) return (int)hipErrorInvalidValue;   // forms 0..10 only (the switch below)
+  }
+  // tile rows / columns of each form, as the kernel instantiations below
+  const int bm = (cfg == 1 || cfg == 5 || cfg == 7 || cfg == 9) ? 256 : 128,
+            bn = cfg == 3 ? 64 : (cfg == 6 || cfg == 9 || cfg == 10) ? 256 : 128;
   p.group_m = cdiv(M, bm) >= 8 ? 4 : 1;
   dim3 grid((unsigned)cdiv(N, bn), (unsigned)cdiv(M, bm), batch);
   hipStream_t st = (hipStream_t)stream;
@@ -2298,6 +2302,13 @@ static bool x6_lds1() {
   return on != 0;
 }
 
+// tile rows / columns of each bf16x6 form (the kernel instantiations of dasa_gemm_f32x6_ws)
+static int x6_form_bm(int cfg) {
+  return (cfg == 1 || cfg == 3 || cfg == 6 || cfg == 7 || cfg == 12 || cfg == 13) ? 256
+         : (cfg == 4 || cfg == 5) ? 64 : 128;
+}
+static int x6_form_bn(int cfg) { return cfg == 5 ? 64 : 128; }
+
 static X6Plan x6_plan(const dasa_gemm_desc* d) {
   const int M = d->M, N = d->N, K = d->K, batch = d->batch < 1 ? 1 : d->batch;
   X6Plan pl{8, 128, 128, 1, K, 0};
@@ -2314,9 +2325,8 @@ static X6Plan x6_plan(const dasa_gemm_desc* d) {
     pl.cfg = (g_force_cfg - kX6Force) % 32;
     fsplit = ((g_force_cfg - kX6Force) / 32) % 64;
   }
-  pl.bm = (pl.cfg == 1 || pl.cfg == 3 || pl.cfg == 6 || pl.cfg == 7 || pl.cfg == 12 || pl.cfg == 13) ? 256
-          : (pl.cfg == 4 || pl.cfg == 5) ? 64 : 128;
-  pl.bn = pl.cfg == 5 ? 64 : 128;
+  pl.bm = x6_form_bm(pl.cfg);
+  pl.bn = x6_form_bn(pl.cfg);
   const long tiles = (long)cdiv(M, pl.bm) * cdiv(N, pl.bn) * batch;
   // split count (profiles/r02/gemm_x6_splitk.txt): the most splits that keep tiles x splits <= 256
   // (one wave of workgroups) with >= 8 32-deep K steps per split; forced splits may go to 4 steps
@@ -2343,8 +2353,8 @@ static X6Plan x6_plan(const dasa_gemm_desc* d) {
   if (pl.splitk > 1) pl.ws = kCntBytes + tiles * pl.splitk * (int64_t)pl.bm * pl.bn * (int64_t)sizeof(float);
   else if (g_force_cfg < kX6Force && x6_form_override() > 0) {   // A/B: DASA_X6_FORM replaces forms 7 / 8
     pl.cfg = x6_form_override();
-    pl.bm = pl.cfg == 7 ? 256 : 128;
-    pl.bn = 128;
+    pl.bm = x6_form_bm(pl.cfg);
+    pl.bn = x6_form_bn(pl.cfg);
   }
   return pl;
 }

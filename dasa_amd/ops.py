@@ -764,22 +764,9 @@ def bilstm_fwd(xproj, whh_f, whh_b, lengths_i32, H, save=False):
     return out, h_n, c_n, ((sa, sc) if save else None)
 
 
-_PERSIST_BWD = [False]
-
-
-def persistent_bwd_ran():
-    """True (once) if a persistent bi-LSTM BPTT (B <= 32, lstm_persist.hip bilstm_persist_ok) was
-    enqueued since the last call: its barrier timeout poisons dgates and is only visible through
-    the device error word, so the caller checks it before the gradients are used."""
-    r, _PERSIST_BWD[0] = _PERSIST_BWD[0], False
-    return r
-
-
 def bilstm_bwd(whh_f, whh_b, lengths_i32, saved, dout, dh_n, dc_n, H):
     sa, sc = saved
     L, _, B, _ = sa.shape
-    if B <= 32 and H % 256 == 0 and 256 <= H <= 1024:
-        _PERSIST_BWD[0] = True
     dev = sa.device
     dgates = torch.empty(B, L, 2, 4 * H, dtype=torch.float32, device=dev)
     ws = torch.empty(_lib.lib().dasa_bilstm_bwd_workspace(B, H) // 4 + 4, dtype=torch.float32, device=dev)

@@ -22,14 +22,14 @@ FAMILIES = {
     "gemm_x6": ("mfma", "gemm_f32x6_nt_kernel"),
     "bilstm": ("mfma", "bilstm_step_fused_kernel"),
     "bilstm_bptt": ("mfma", "bilstm_bptt_step_kernel"),
-    "shift_attn": ("hbm", "attn_split_fwd_kernel<5> (B*17 <= 1024) / attn_fwd_kernel<12>"),
-    "shift_attn_bwd": ("hbm", "attn_split_bwd_kernel<5> / attn_bwd_dp_kernel<12>+attn_bwd_apply_kernel<12>"),
-    "softdot": ("hbm", "attn_split_fwd_kernel<10> / attn_fwd_kernel<16>"),
+    "shift_attn": ("hbm", "attn_split_dots_kernel<5> + attn_split_ctx_kernel<5> (B < 128) / attn_rows_fwd_kernel<3>"),
+    "shift_attn_bwd": ("hbm", "attn_split_bwd_kernel<5> (B*17 <= 1024) / attn_bwd_dp_kernel<12>+attn_bwd_apply_kernel<12>"),
+    "softdot": ("hbm", "attn_fwd_kernel<16> (B < 128) / attn_rows_fwd_kernel<N/12>"),
     "softdot_bwd": ("hbm", "attn_split_bwd_kernel<10> / attn_bwd_dp_kernel<16>+attn_bwd_apply_kernel<16>"),
-    "cand_logit": ("hbm", "attn_split_fwd_kernel<2> / attn_fwd_kernel<16>"),
+    "cand_logit": ("hbm", "attn_dot_rows_kernel (B < 128) / attn_fwd_kernel<16>"),
     "cand_logit_bwd": ("hbm", "attn_split_bwd_kernel<2> / attn_bwd_apply_kernel<16>"),
     "mha": ("mfma", "mha_fwd_kernel"),
-    "mha_bwd": ("mfma", "mha_bwd_kernel"),
+    "mha_bwd": ("mfma", "mha_bwd_kernel / mha_bwd_lds_kernel"),
     "layernorm": ("hbm", "ln_fwd_kernel"),
     "layernorm_bwd": ("hbm", "ln_bwd_kernel"),
     "embed": ("hbm", "embed_kernel"),
@@ -135,8 +135,7 @@ def _pmc_traffic(workload):
 
 # the committed PMC summaries per workload the roofline's `traffic` / `mfma_busy` come from
 # (tools/prof_round.sh -> tools/pmc_summary.py); a workload without one reports no PMC values
-PMC_FILES = {"cfg2": "profiles/r03/prof_f/pmc_cfg2.json", "cfg5": "profiles/r03/prof/pmc_cfg5.json",
-             "cfg4": "profiles/r03/prof/pmc_cfg4.json"}
+PMC_FILES = {"cfg2": "profiles/r03/prof_f/pmc_cfg2.json"}
 
 
 def active():

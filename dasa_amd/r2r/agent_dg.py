@@ -941,8 +941,10 @@ class Seq2SeqAgent(BaseAgent):
             self.loss.backward()
         DF.flush_bilstm_backward()
         DF.flush_weight_grads()
-        if ops.persistent_bwd_ran():
-            ops.check_device_errors()   # a timed-out BPTT barrier NaN-poisons dgates: raise before any step
+        # every kernel with a bounded inter-workgroup barrier (persistent bi-LSTM BPTT, D-split attention
+        # backward) NaN-poisons its outputs and sets an error bit when the barrier times out: read the
+        # error word (one host sync) before the gradients reach grad_sync, clipping and the optimizers
+        ops.check_device_errors()
         if self.grad_sync is not None:
             self.grad_sync()
         torch.nn.utils.clip_grad_norm_(self.encoder.parameters(), 40.0)

@@ -238,7 +238,7 @@ def _zero_dropout(agent):
                 sub.p = 0.0
 
 
-def _train_iteration(R, agent, out, prefix, forced=None, **kw):
+def _train_iteration(R, agent, out, prefix, forced=None, no_stop=False, **kw):
     """accumulate_gradient('sample') with argmax 'sampling' (or, given `forced`, the seeded action table
     of GI.reference_forced_sample), then backward; losses, logs + gradients."""
     A = R.args
@@ -246,7 +246,7 @@ def _train_iteration(R, agent, out, prefix, forced=None, **kw):
     orig_sample = torch.distributions.Categorical.sample
     uninstall = None
     if forced is not None:
-        sample, install, uninstall = GI.reference_forced_sample(forced, R.utils)
+        sample, install, uninstall = GI.reference_forced_sample(forced, R.utils, no_stop)
         install()
     else:
         sample = lambda self, *a, **k: self.probs.argmax(-1)   # noqa: E731
@@ -334,6 +334,37 @@ def cfg2(R):
     agent = make_agent(R, env, cfg["train_max_action"])
     _zero_dropout(agent)
     _train_iteration(R, agent, out, "trainf/", forced=GI.forced_table(cfg["train_max_action"], cfg["batch"]))
+    return out
+
+
+def cfg2_full(R):
+    """The headline training iteration at its real length (GI.CFG2_FULL: B=20, vl=3, maxAction 35,
+    'wander' episodes, dropout 0, sampled draws from a no-stop forced table): one
+    accumulate_gradient('sample') — 35 teacher steps, 35 sampled steps and the A2C bootstrap — then
+    backward. Records the raw logits of every decoder call (agent_dg.py:817; before the in-place mask of
+    :841), the losses / per-step logs and every gradient."""
+    A = R.args
+    cfg = GI.CFG2_FULL
+    A.d_vl_layers, A.batchSize, A.views, A.maxAction = cfg["vl_layers"], cfg["batch"], 36, cfg["max_action"]
+    world = SynthWorld(n_viewpoints=cfg["viewpoints"], feat_seed=0, graph_seed=cfg["graph_seed"])
+    env = SynthR2RBatch(world, cfg["batch"], seed=cfg["env_seed"], mode="wander", instr_len=cfg["instr_len"],
+                        variable_len=True)
+    agent = make_agent(R, env, cfg["max_action"])
+    _zero_dropout(agent)
+    logits = []
+    dec_fwd = agent.decoder.forward
+
+    def dec_wrap(*a, **k):
+        r = dec_fwd(*a, **k)
+        logits.append(f32(r[2]))
+        return r
+    agent.decoder.forward = dec_wrap
+    out = {}
+    _train_iteration(R, agent, out, "full/", forced=GI.forced_table(cfg["max_action"], cfg["batch"],
+                                                                   seed=cfg["forced_seed"]), no_stop=True)
+    out["full/n_decoder_calls"] = np.array(len(logits))
+    for t, lg in enumerate(logits):
+        out[f"full/logit/{t}"] = lg
     return out
 
 
@@ -778,6 +809,7 @@ FIXTURES = {
     "cfg1_rollout": lambda R: {**rollouts(R), **checkpoint_schema(R)},
     "cfg4_finetune": finetune,
     "cfg2": cfg2,
+    "cfg2_full": cfg2_full,
     "cfg5": cfg5,
     "io": io_readers,
     "eval": eval_score,

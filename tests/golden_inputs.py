@@ -127,12 +127,18 @@ def forced_table(steps, batch, seed=FORCED_SEED):
     return np.random.default_rng(seed).random((steps, batch))
 
 
-def forced_actions(table, t, lens):
+def forced_actions(table, t, lens, no_stop=False):
+    """Row b takes candidate floor(u[t, b] * n_b); with no_stop the draw is over the navigable
+    candidates only (n_b - 1 of them; the stop entry is the last, agent_dg.py:305-306), so a
+    'wander' episode runs every one of its maxAction steps."""
     lens = np.asarray(lens, np.int64)
+    if no_stop:
+        n = np.maximum(lens - 1, 1)
+        return np.minimum((table[t] * n).astype(np.int64), n - 1)
     return np.minimum((table[t] * lens).astype(np.int64), lens - 1)
 
 
-def reference_forced_sample(table, utils_mod):
+def reference_forced_sample(table, utils_mod, no_stop=False):
     """A Categorical.sample replacement for the reference run: the t-th call returns the table's step t,
     over the candidate counts the step passed to utils.length2mask (agent_dg.py:834, right before the
     draw; counting probs > 0 instead would miss candidates whose probability underflows). Returns
@@ -145,7 +151,7 @@ def reference_forced_sample(table, utils_mod):
         return orig(length, size) if size is not None else orig(length)
 
     def sample(self, *a, **k):
-        out = torch.from_numpy(forced_actions(table, state["t"], state["lens"]))
+        out = torch.from_numpy(forced_actions(table, state["t"], state["lens"], no_stop))
         state["t"] += 1
         return out
 
@@ -222,6 +228,15 @@ CFG_OPTIM = dict(batch=2, vl_layers=1, la_layers=9, max_action=5, instr_len=80, 
 
 # ---- cfg4 at its README configuration (README.md:104-116: vl=3, B=2, maxAction 35 -> 6 steps here) --
 CFG4R = dict(batch=2, vl_layers=3, la_layers=9, max_action=6, instr_len=80, env_seed=10)
+
+# ---- the headline iteration at its real length (BASELINE configs[1], the bench workload) -------------
+# accumulate_gradient('sample') at B=20, vl=3, maxAction 35 on 'wander' episodes (the teacher never
+# stops: 35 teacher steps) with the sampled draws from a no-stop forced table (35 sampled steps), dropout
+# 0: the timed path end to end — 8-step teacher chunks (the language pipe and the persistent bi-LSTM at
+# 160 rows), the fused policy head in TEACHER and FORCED modes, the batched BPTT over all 70 encoder calls
+# and the deferred weight gradients with K = T*B.
+CFG2_FULL = dict(batch=20, vl_layers=3, la_layers=9, max_action=35, instr_len=80, viewpoints=32, graph_seed=5,
+                 env_seed=24, forced_seed=33)
 
 # ---- --pretrain_model_name (agent_dg.py:165-188): a DicAddActionPreTrain checkpoint directory -------
 # whose config.json says vl_layers=2 while the command line says d_vl_layers=3 (the checkpoint decides)

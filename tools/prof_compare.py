@@ -13,13 +13,16 @@ FAMILY_PREFIX = [
     ("gemm_splitk_reduce", ("splitk_reduce_kernel",)),
     ("bilstm", ("bilstm_persist_fwd_kernel", "bilstm_step_fused_kernel", "bilstm_step_cell_kernel")),
     ("bilstm_bptt", ("bilstm_persist_bwd_kernel", "bilstm_bptt_step_kernel", "bilstm_bptt_cell_kernel")),
-    ("mha", ("mha_fwd_kernel", "mha_bwd_kernel")),
+    ("mha", ("mha_fwd_kernel", "mha_bwd_kernel", "mha_bwd_lds_kernel")),
     ("layernorm", ("ln_fwd_kernel", "ln_bwd_kernel")),
     ("softdot/shift/cand", ("scores_kernel", "apply_fwd_kernel", "apply_bwd_kernel", "attn_fwd_kernel",
                             "attn_bwd_apply_kernel", "attn_bwd_scores_kernel", "attn_bwd_dp_kernel",
-                            "attn_split_fwd_kernel", "attn_split_bwd_kernel")),
-    ("ada_gate", ("AdaFwdOp", "AdaBwdOp")),
+                            "attn_split_bwd_kernel", "attn_split_dots_kernel", "attn_split_ctx_kernel",
+                            "attn_rows_fwd_kernel", "attn_dot_rows_kernel")),
+    ("ada_gate", ("AdaFwdOp", "AdaBwdOp", "ada_gate_fwd_kernel", "ada_gate_bwd_kernel")),
     ("adain_musigma", ("adain_musigma",)),
+    ("gather", ("gather_rows_kernel",)),
+    ("lstm_cell", ("lstm_cell_fwd_kernel", "lstm_cell_bwd_kernel")),
     ("policy_head", ("policy_head_fwd_kernel", "policy_head_bwd_kernel")),
 ]
 
