@@ -21,36 +21,39 @@ class GradSync:
         self.flat = torch.empty(self.numel, dtype=torch.float32, device=dev)
         self.mask = torch.empty(len(self.params), dtype=torch.float32, device=dev)
         self.bucket = max(1, int(bucket_mb * 2**20 / 4))
+        self.sent = 0            # floats all-reduced by the last call
 
     def __call__(self):
-        off = 0
-        has = []
-        for p in self.params:
-            n = p.numel()
-            if p.grad is not None:
-                self.flat[off:off + n].copy_(p.grad.view(-1))
-                has.append(1.0)
-            else:
-                self.flat[off:off + n].zero_()
-                has.append(0.0)
-            off += n
-        self.mask.copy_(torch.tensor(has))
+        # which parameters received a gradient on ANY rank (one small all-reduce + host read): only
+        # those travel in the bucket — the 47.23 M floats of the README train config, not the 58 M
+        # trainable ones (the unused linear_out heads, encoder2decoder_*, never get one)
+        self.mask.copy_(torch.tensor([1.0 if p.grad is not None else 0.0 for p in self.params]))
         dist.all_reduce(self.mask)
-        # bucketed so that very large models keep several collectives in flight on RCCL's channels
-        for s in range(0, self.numel, self.bucket):
-            dist.all_reduce(self.flat[s:s + self.bucket])
-        self.flat.div_(self.world)
         m = self.mask.cpu().tolist()
         off = 0
         for p, any_rank in zip(self.params, m):
-            n = p.numel()
             if any_rank > 0:
+                n = p.numel()
+                if p.grad is not None:
+                    self.flat[off:off + n].copy_(p.grad.view(-1))
+                else:
+                    self.flat[off:off + n].zero_()
+                off += n
+        self.sent = off
+        # bucketed so that very large models keep several collectives in flight on RCCL's channels
+        for s in range(0, off, self.bucket):
+            dist.all_reduce(self.flat[s:min(off, s + self.bucket)])
+        self.flat[:off].div_(self.world)
+        off = 0
+        for p, any_rank in zip(self.params, m):
+            if any_rank > 0:
+                n = p.numel()
                 g = self.flat[off:off + n].view_as(p)
                 if p.grad is None:
                     p.grad = g.clone()
                 else:
                     p.grad.copy_(g)
-            off += n
+                off += n
 
 
 def broadcast_params(modules, src=0):
@@ -76,14 +79,15 @@ def _trainable(agent):
     return out
 
 
-def attach(agent):
+def attach(agent, force=False):
     """Broadcast rank 0's weights and install the gradient all-reduce in agent.optim_step().
+    `force` (test hook) installs it at world size 1 too, so the collective path runs on one GPU.
 
     Every rank of an unchanged train.py seeds torch identically (train.py:521), so the random streams
     are made rank-specific here: torch's generator (nn.Dropout, the env-drop noise) is re-seeded with
     seed + 7919 * rank, and the counter-RNG seed stream of the HIP kernels (dropout masks, Categorical
     draws) gets the rank as salt. Rank 0 keeps the single-GPU streams."""
-    if not dist.is_initialized() or dist.get_world_size() == 1:
+    if not dist.is_initialized() or (dist.get_world_size() == 1 and not force):
         return None
     from . import functional as DF
     rank = dist.get_rank()
