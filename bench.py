@@ -55,9 +55,10 @@ def parse():
     p.add_argument("--no-host-input", action="store_true", help="skip the host-input (PCIe-inclusive) leg")
     p.add_argument("--no-hoist", action="store_true", help="skip the --hoist_language (non-default mode) leg")
     p.add_argument("--cfg5-only", action="store_true", help="run only the configs[4] leg (tuning)")
-    p.add_argument("--only", choices=("cfg4", "cfg5"), default=None,
+    p.add_argument("--only", choices=("cfg4", "cfg5", "aug"), default=None,
                    help="run only that leg and print it (the per-workload rocprofv3 --pmc passes)")
     p.add_argument("--no-cfg4", action="store_true", help="skip the configs[3] (finetune, B=2, vl=3) leg")
+    p.add_argument("--no-aug", action="store_true", help="skip the full auglistener (GT + aug half) leg")
     p.add_argument("--cfg5-steps", type=int, default=6, help="decision steps per configs[4] rollout")
     p.add_argument("--backend", default="nccl", help="nccl (= RCCL on ROCm) | gloo (rehearsal only)")
     p.add_argument("--same-device", action="store_true",
@@ -213,6 +214,63 @@ def host_input_leg(a, steps=2):
             "note": "cfg2 training iteration with host-built observation features copied H2D (pinned) each step"}
 
 
+def aug_leg(a, steps=2):
+    """The WHOLE auglistener iteration of train.py:226-243 (the README --accumulateGrad loop): zero_grad;
+    GT half on the bench's env (ml_weight_org: teacher + sampled rollout); aug half on a second env
+    with the speaker back-translating each rollout's teacher path (speaker.py:265-350: decode word by
+    word, one host sync per word) and the shared env-drop noise (ml_weight_aug: teacher + sampled
+    rollout); then optim_step. The aug env holds 'goal' episodes (the speaker walks the teacher path to
+    its stop); the speaker is random-init (scaled x10 so rows decode different words), so it decodes
+    until <EOS> or maxDecode. Decisions = the four rollouts' batched steps x B. Beside `value`, never
+    as it."""
+    from dasa_amd.r2r import speaker as S
+    from dasa_amd.r2r import utils
+    from dasa_amd.r2r.param import args
+    from dasa_amd.synth import HashBTokenizer, SynthR2RBatch, init_params, speaker_vocab
+    agent, env = build_agent(a, 0, 1)
+    agent.tok = HashBTokenizer(80)
+    aug_env = SynthR2RBatch(env.world, a.batch, seed=3000, mode="goal", instr_len=80, lazy_features=True)
+    with contextlib.redirect_stdout(io.StringIO()):
+        spk = S.Speaker(aug_env, agent, utils.Tokenizer(vocab=speaker_vocab(), encoding_length=80))
+    for m, s in ((spk.encoder, 61), (spk.decoder, 62)):
+        init_params(m, s)
+        with torch.no_grad():
+            for p in m.parameters():
+                p.mul_(10.0)
+    words = []
+    infer = spk.infer_batch
+
+    def infer_rec(*x, **k):
+        r = infer(*x, **k)
+        words.append(r.shape[1])
+        return r
+    spk.infer_batch = infer_rec
+
+    def iteration():
+        agent.zero_grad()
+        agent.env = env
+        args.ml_weight = args.ml_weight_org
+        agent.accumulate_gradient("sample")
+        n = agent.logs["viewsteps/teacher"][-1] + agent.logs["viewsteps/sample"][-1]
+        agent.env = aug_env
+        args.ml_weight = args.ml_weight_aug
+        agent.accumulate_gradient("sample", speaker=spk)
+        n += agent.logs["viewsteps/teacher"][-1] + agent.logs["viewsteps/sample"][-1]
+        agent.optim_step()
+        args.ml_weight = args.ml_weight_org
+        return n * a.batch
+    iteration()
+    words.clear()
+    u, dt = timed(iteration, steps, 0, 1)
+    res = {"workload": "full auglistener iteration (train.py:226-243): GT half + aug half (speaker "
+                       "back-translation + env-drop noise, teacher + sampled rollout) + optim_step",
+           "value": round(u / dt, 2), "unit": "agent-decisions/s", "ms_per_step": round(1000 * dt / steps, 2),
+           "decisions_per_iteration": u / steps, "speaker_words_per_decode": words}
+    del agent, spk
+    torch.cuda.empty_cache()
+    return res
+
+
 def cfg4_leg(a, steps=3):
     """BASELINE configs[3] per rank: the README finetune iteration (README.md:104-116:
     --d_update_add_layer True, so the LXRT layers and the VisionEncoder train; d_vl_layers 3, batchSize 2,
@@ -296,6 +354,9 @@ def main():
     if a.only == "cfg4":
         print(json.dumps({"cfg4": cfg4_leg(a)}), flush=True)
         return
+    if a.only == "aug":
+        print(json.dumps({"aug": aug_leg(a)}), flush=True)
+        return
     agent, env = build_agent(a, rank, world)
     for _ in range(a.warmup):
         train_step(agent)
@@ -311,8 +372,10 @@ def main():
         "warmup": a.warmup, "ms_per_step": round(1000 * dt / a.steps, 2),
         "batched_steps_per_s": round(value / (a.batch * world), 2), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
-        "config": {"workload": "cfg2 auglistener training iteration (teacher + sample rollout, backward, "
-                               "grad all-reduce, RMSprop), README flags",
+        "config": {"workload": "cfg2 training iteration on the GT env: accumulate_gradient('sample') (teacher + "
+                               "sampled rollout) + optim_step (backward, " +
+                               ("RCCL grad all-reduce, " if world > 1 else "") + "clip, RMSprop), README flags; "
+                               "the GT half of train.py's auglistener loop (the full loop: `auglistener`)",
                    "global_batch": a.batch * world, "per_rank_batch": a.batch, "max_action": a.max_action,
                    "instr_len": 80, "vl_layers": a.vl, "la_layers": 9, "parallelism": f"dp{world}",
                    "world_size": world, "backend": (dist.get_backend() if world > 1 else None)},
@@ -343,6 +406,8 @@ def main():
         out["hoist_language"] = hoist_leg(agent)
     if rank == 0 and world == 1 and not a.no_host_input:
         out["host_input"] = host_input_leg(a)
+    if rank == 0 and world == 1 and not a.no_aug:
+        out["auglistener"] = aug_leg(a)
     if rank == 0 and world == 1 and not a.no_cfg4:
         out["cfg4"] = cfg4_leg(a)
     if rank == 0 and world == 1 and not a.no_cfg5:

@@ -508,3 +508,36 @@ def _device_input_feat_steps(self, obs_steps, device):
 
 SynthR2RBatch.device_input_feat = _device_input_feat
 SynthR2RBatch.device_input_feat_steps = _device_input_feat_steps
+
+
+# ---------------------------------------------------------------------------------- the aug half
+def speaker_vocab(n=991):
+    """A synthetic speaker word list of the R2R train_vocab.txt's size (991 entries; utils.py:22-24's
+    base vocabulary <PAD>, <UNK>, <EOS> first), for the bench's auglistener leg."""
+    return ["<PAD>", "<UNK>", "<EOS>"] + ["w%04d" % i for i in range(n - 3)]
+
+
+class HashBTokenizer:
+    """Stand-in for the listener's utils.BTokenizer (bert-base-uncased WordPiece, a name-based download
+    that is unavailable offline) with its contract: [CLS]=101 + one id per word + [SEP]=102, padded with
+    pad_token_id 0 to encoding_length, an over-long encoding cut with [SEP] last. Word ids are a CRC
+    of the word (tests/golden_inputs.py's WordHashBTokenizer is the same mapping)."""
+
+    class _T:
+        pad_token_id = 0
+        sep_token_id = 102
+
+    def __init__(self, encoding_length=80):
+        self.tokenizer = self._T()
+        self.encoding_length = encoding_length
+
+    def encode_sentence(self, sentence, seps=None):
+        import re
+        import zlib
+        words = [w for w in re.split(r"\s+", sentence.strip().lower()) if w]
+        enc = [101] + [1000 + zlib.crc32(w.encode()) % 29000 for w in words] + [102]
+        if len(enc) < self.encoding_length:
+            enc += [0] * (self.encoding_length - len(enc))
+        if len(enc) > self.encoding_length:
+            enc[self.encoding_length - 1] = 102
+        return np.array(enc[:self.encoding_length])

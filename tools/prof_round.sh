@@ -12,7 +12,7 @@ TAG=${TAG:-r03}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-BENCH_ARGS="--no-cfg5 --no-cfg4 --no-kbench --no-cpu-baseline --no-fwd --no-hoist --no-host-input"
+BENCH_ARGS="--no-cfg5 --no-cfg4 --no-aug --no-kbench --no-cpu-baseline --no-fwd --no-hoist --no-host-input"
 
 step() {   # step <name> <timeout> <log> cmd...
   local name=$1 t=$2 log=$3; shift 3
