@@ -38,6 +38,7 @@ struct PolicyFwd {
   float* ce_rows;           // [B] scratch
   int B, C, mode, ignore;
   uint64_t seed;
+  const uint64_t* seed_src; // device seed source of a graph-captured launch (eff_seed), or null
 };
 
 __global__ __launch_bounds__(1024) void policy_head_fwd_kernel(PolicyFwd a) {
@@ -100,7 +101,7 @@ __global__ __launch_bounds__(1024) void policy_head_fwd_kernel(PolicyFwd a) {
       }
       act = bi;
     } else if (a.mode == DASA_POLICY_SAMPLE) {   // inverse CDF over the masked softmax
-      const float u = dasa_uniform(a.seed, (uint64_t)b);
+      const float u = dasa_uniform(eff_seed(a.seed, a.seed_src), (uint64_t)b);
       float carry = 0.f;
       int pick = 0x7fffffff, last = -1;
 #pragma unroll
@@ -221,8 +222,10 @@ extern "C" int dasa_policy_head_fwd(const float* logit, int64_t ld, const int32_
       mode != DASA_POLICY_FORCED)
     return (int)hipErrorInvalidValue;
   if (mode != DASA_POLICY_TEACHER && !action) return (int)hipErrorInvalidValue;
+  // a captured sampled step draws fresh actions on every replay: the seed is re-keyed by the device
+  // seed source recorded at capture (dasa_set_seed_source), as the dropout kernels do
   PolicyFwd a{logit, (long)ld, cand_len, target, logp, ce_sum, ent, logp_a, action, ws, B, C, mode, ignore_index,
-              seed};
+              seed, mode == DASA_POLICY_SAMPLE ? dasa_seed_src_host() : nullptr};
   const int waves = B < 16 ? B : 16;
   hipLaunchKernelGGL(policy_head_fwd_kernel, dim3(1), dim3(64 * waves), 0, (hipStream_t)stream, a);
   DASA_CHECK_LAUNCH();

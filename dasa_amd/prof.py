@@ -135,7 +135,8 @@ def _pmc_traffic(workload):
 
 # the committed PMC summaries per workload the roofline's `traffic` / `mfma_busy` come from
 # (tools/prof_round.sh -> tools/pmc_summary.py); a workload without one reports no PMC values
-PMC_FILES = {"cfg2": "profiles/r03/prof_f/pmc_cfg2.json"}
+PMC_FILES = {"cfg2": "profiles/r04/prof_a/pmc_cfg2.json", "cfg5": "profiles/r04/prof_a/pmc_cfg5.json",
+             "cfg4": "profiles/r04/prof_a/pmc_cfg4.json"}
 
 
 def active():

@@ -30,6 +30,9 @@ step bench 400 $OUT/bench.log python bench.py --steps 3 --warmup 1 --shapes 40 $
 grep '^{"metric"' $OUT/bench.log | tail -1 > $OUT/bench.json
 step stats 500 $OUT/stats_run.log rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- \
   python3 bench.py --steps 2 --warmup 1 --no-profile $BENCH_ARGS
+# GPU busy / idle over the last timed iteration (union of kernel intervals; tools/timeline.py)
+TRACE=$(find $OUT/stats -name "*kernel_trace.csv" | head -1)
+[ -n "$TRACE" ] && python tools/timeline.py "$TRACE" ${ITER_MS:-420} > $OUT/timeline_last_iter.txt 2>&1
 find $OUT/stats \( -name "*kernel_trace*" -o -name "*.db" \) -delete 2>/dev/null
 STATS=$(find $OUT/stats -name "run_kernel_stats.csv" | head -1)
 [ -n "$STATS" ] && python tools/prof_compare.py "$STATS" $OUT/bench.json > $OUT/prof_compare.txt && cat $OUT/prof_compare.txt
