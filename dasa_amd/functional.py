@@ -2,6 +2,10 @@
 
 These are the differentiable building blocks of the reference-API modules in dasa_amd.r2r. Only
 the tensors a backward actually needs are saved, and nothing is saved when no input requires grad.
+Parameters are held as ctx attributes (ctx.params), not saved tensors: a captured training step
+(graph.AutogradGraphs) keeps its autograd graph across optimizer steps, whose in-place parameter
+updates would otherwise fail the saved-tensor version check; the backward reads the parameters as
+they are at backward time, which in every training loop here is before the optimizer step.
 """
 import contextlib
 
@@ -146,16 +150,17 @@ class LinearFn(torch.autograd.Function):
         if need and act == "gelu":
             z = ops.linear(x, W, b)
             y = ops.act_fwd(z, "gelu")
-            ctx.save_for_backward(x, W, z)
+            ctx.save_for_backward(x, z)
         else:
             y = ops.linear(x, W, b, act=act)
             if need:
-                ctx.save_for_backward(x, W, y if act is not None else None)
+                ctx.save_for_backward(x, y if act is not None else None)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, W, s = ctx.saved_tensors
+        x, s = ctx.saved_tensors
+        W = ctx.params[0]
         N = W.shape[0]
         dz = _flat(dy.contiguous())
         if ctx.act is not None:
@@ -318,14 +323,15 @@ class ShiftAttnFn(torch.autograd.Function):
         z = ops.linear(h, W_s, b_s)
         wctx, attn, shifted, wsm = ops.shift_attn_fwd(q, feat, z)
         if any(ctx.needs_input_grad):
-            ctx.save_for_backward(h, feat, q, attn, shifted, wsm, W_in, W_s)
+            ctx.save_for_backward(h, feat, q, attn, shifted, wsm)
             ctx.params = (W_in, W_s, b_s)
         ctx.mark_non_differentiable(attn)
         return wctx, attn
 
     @staticmethod
     def backward(ctx, dwctx, _dattn):
-        h, feat, q, attn, shifted, wsm, W_in, W_s = ctx.saved_tensors
+        h, feat, q, attn, shifted, wsm = ctx.saved_tensors
+        W_in, W_s = ctx.params[0], ctx.params[1]
         dq, dfeat, dz = ops.shift_attn_bwd(q, feat.contiguous(), attn, shifted, wsm, dwctx.contiguous(),
                                            want_dctx=ctx.needs_input_grad[1])
         dh = dWin = dWs = dbs = None
@@ -354,14 +360,15 @@ class SoftDotTildeFn(torch.autograd.Function):
         ops.copy2d(h, cat[:, D:])
         y = ops.linear(cat, W_out, act="tanh")
         if any(ctx.needs_input_grad):
-            ctx.save_for_backward(h, c, q, probs, cat, y, W_in, W_out)
+            ctx.save_for_backward(h, c, q, probs, cat, y)
             ctx.params = (W_in, W_out)
         ctx.mark_non_differentiable(probs)
         return y, probs
 
     @staticmethod
     def backward(ctx, dy, _dalpha):
-        h, c, q, probs, cat, y, W_in, W_out = ctx.saved_tensors
+        h, c, q, probs, cat, y = ctx.saved_tensors
+        W_in, W_out = ctx.params
         dz = ops.act_bwd(y, dy.contiguous(), "tanh")
         D = c.shape[2]
         dh = dc = dWin = dWout = None
@@ -387,13 +394,14 @@ class CandLogitFn(torch.autograd.Function):
         q = ops.linear(h, W_in)
         scores, _, _ = ops.softdot_fwd(q, cand, None, want_probs=False, want_wctx=False)
         if any(ctx.needs_input_grad):
-            ctx.save_for_backward(h, cand, q, scores, W_in)
+            ctx.save_for_backward(h, cand, q, scores)
             ctx.params = (W_in,)
         return scores
 
     @staticmethod
     def backward(ctx, dlogit):
-        h, cand, q, scores, W_in = ctx.saved_tensors
+        h, cand, q, scores = ctx.saved_tensors
+        W_in = ctx.params[0]
         # ds = dscores exactly when no dwctx flows (probs operand unused)
         dq, dcand = ops.softdot_bwd(q, cand.contiguous(), scores, dscores=dlogit.contiguous(),
                                     want_dctx=ctx.needs_input_grad[1])
@@ -453,14 +461,15 @@ class LSTMCellFn(torch.autograd.Function):
         need = any(ctx.needs_input_grad)
         h1, c1, act = ops.lstm_cell_fwd(gates, c, save=need)
         if need:
-            ctx.save_for_backward(xcat, h, c, c1, act, W_ih, W_hh)
+            ctx.save_for_backward(xcat, h, c, c1, act)
             ctx.params = (W_ih, W_hh, b_ih, b_hh)
         ctx.E = E
         return h1, c1
 
     @staticmethod
     def backward(ctx, dh1, dc1):
-        xcat, h, c, c1, act, W_ih, W_hh = ctx.saved_tensors
+        xcat, h, c, c1, act = ctx.saved_tensors
+        W_ih, W_hh = ctx.params[0], ctx.params[1]
         dgates, dc_prev = ops.lstm_cell_bwd(act, c, c1, dh1, dc1)
         E = ctx.E
         n = ctx.needs_input_grad

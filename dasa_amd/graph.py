@@ -123,3 +123,162 @@ class StepGraphs:
 
     def clear(self):
         self.entries.clear()
+
+
+# ------------------------------------------------------------------ training-mode (autograd) regions
+class _Slot:
+    __slots__ = ("graph", "static_in", "static_out", "counter", "pkey")
+
+
+def _lead(t, shape):
+    """The leading sub-block of `t` with `shape` (a padded static input holds its input there)."""
+    if tuple(t.shape) == tuple(shape):
+        return t
+    return t[tuple(slice(0, n) for n in shape)]
+
+
+class _BridgeFn(torch.autograd.Function):
+    """One replay of a captured training region, linked into the caller's autograd graph: forward
+    copies the inputs into the slot's static inputs (through .data: no version bump, the captured
+    autograd graph saved some of them), replays the graph and returns copies of the outputs; backward
+    runs the slot's own autograd graph (recorded at capture, retained) eagerly with the slot's seed
+    counter as the device seed source — so every dropout backward regenerates the masks this replay drew
+    — and hands the static inputs' gradients back. Parameter gradients accumulate (or are deferred,
+    functional.defer_weight_grads) inside that nested backward exactly as in an eager step."""
+
+    @staticmethod
+    def forward(ctx, slot, *inputs):
+        with torch.no_grad():
+            for s, x in zip(slot.static_in, inputs):
+                if s is not None:
+                    _lead(s.data, x.shape).copy_(x)
+        slot.graph.replay()
+        ctx.slot = slot
+        ctx.shapes = [x.shape if x is not None else None for x in inputs]
+        outs = tuple(o.detach().clone() if o is not None else None for o in slot.static_out)
+        nd = [o for o in outs if o is not None and not o.is_floating_point()]
+        if nd:
+            ctx.mark_non_differentiable(*nd)
+        return outs
+
+    @staticmethod
+    def backward(ctx, *gouts):
+        slot = ctx.slot
+        outs, grads = [], []
+        for o, g in zip(slot.static_out, gouts):
+            if o is not None and o.requires_grad and g is not None:
+                outs.append(o)
+                grads.append(g)
+        if outs:
+            L = _lib.lib()
+            L.dasa_set_seed_source(ctypes.c_void_p(slot.counter.data_ptr()))
+            try:
+                torch.autograd.backward(outs, grads, retain_graph=True)
+            finally:
+                L.dasa_set_seed_source(None)
+        res = []
+        for s, shape in zip(slot.static_in, ctx.shapes):
+            g = None
+            if s is not None and s.requires_grad and s.grad is not None:
+                g = _lead(s.grad, shape)
+                s.grad = None
+            res.append(g)
+        return (None,) + tuple(res)
+
+
+class AutogradGraphs:
+    """Training-mode decision steps (agent_dg.py:725-936 with autograd on) as hipGraph
+    replays. A region — e.g. the decoder step + the one-kernel policy head — is captured once per slot
+    key WITH autograd recording: the capture builds the region's autograd graph over static input
+    leaves, and that graph is kept. Each replay rewrites the graph-pool tensors the graph saved, so a
+    slot serves ONE live step: the caller keys slots by step index, and `run` adds an occurrence
+    number for keys used again before new_iteration() (the auglistener loop's GT and aug halves each
+    run a teacher and a sampled rollout before one backward). Dropout / Categorical draws stay fresh
+    per replay (a per-slot device seed counter, bumped by the graph's first node) and their backward
+    regenerates the same masks (_BridgeFn). Parameters are read in place by the replay (optimizer
+    updates need no re-capture); a re-assigned parameter (new storage) re-captures. Host cost of a
+    step: the input copies and one graph launch instead of ~30 Python-level launches."""
+
+    def __init__(self, modules):
+        self.modules = list(modules)
+        self._params = None
+        self.slots = {}
+        self.uses = {}
+        self.stream = None
+        self.pool = None
+        self.captures = 0
+        self.replays = 0
+
+    def _param_key(self):
+        if self._params is None:
+            self._params = [p for m in self.modules for p in m.parameters()]
+        return tuple((id(p), p.data_ptr()) for p in self._params)
+
+    def new_iteration(self):
+        """Every slot replayed since the last call has had its backward (or will never get one)."""
+        self.uses.clear()
+
+    def _capture(self, fn, inputs, pads):
+        dev = next(x for x in inputs if x is not None).device
+        if self.stream is None:
+            self.stream = torch.cuda.Stream(device=dev)
+            self.pool = torch.cuda.graph_pool_handle()
+        slot = _Slot()
+        slot.counter = torch.zeros(1, dtype=torch.int64, device=dev)
+        static_in = []
+        for i, x in enumerate(inputs):
+            if x is None:
+                static_in.append(None)
+                continue
+            shape, fill = pads.get(i, (x.shape, 0))
+            s = torch.full(shape, fill, dtype=x.dtype, device=dev)    # the padding keeps its fill value
+            _lead(s, x.shape).copy_(x)
+            static_in.append(s.requires_grad_(x.requires_grad))
+        self.stream.wait_stream(torch.cuda.current_stream())
+        _NESTED[0] += 1
+        try:
+            # warm-up on the capture stream (lazily built workspaces / caches outside the capture); its
+            # autograd graph is dropped
+            with torch.cuda.stream(self.stream), torch.enable_grad():
+                fn(*static_in)
+            torch.cuda.current_stream().wait_stream(self.stream)
+            torch.cuda.synchronize(dev)
+            g = torch.cuda.CUDAGraph()
+            L = _lib.lib()
+            ctr = ctypes.c_void_p(slot.counter.data_ptr())
+            L.dasa_set_seed_source(ctr)
+            try:
+                with torch.cuda.graph(g, pool=self.pool, stream=self.stream), torch.enable_grad():
+                    _lib.check(L.dasa_seed_bump(ctr, ctypes.c_void_p(self.stream.cuda_stream)), "dasa_seed_bump")
+                    out = fn(*static_in)
+            finally:
+                L.dasa_set_seed_source(None)
+        finally:
+            _NESTED[0] -= 1
+        slot.graph, slot.static_in, slot.static_out = g, static_in, tuple(out)
+        slot.pkey = self._param_key()
+        self.captures += 1
+        return slot
+
+    def run(self, key, fn, inputs, pads=None):
+        """fn(*inputs) -> tuple of tensors / None, recorded with autograd; returns the outputs linked to
+        `inputs` for backward. pads: {input index: (static shape >= the input's, fill value of the
+        padding)}; the input is copied into the leading sub-block on every replay."""
+        from . import ops
+        key = (key, ops._BF16["on"], ops._EMU["on"], ops._EMU["min_rows"])
+        n = self.uses.get(key, 0)
+        self.uses[key] = n + 1
+        skey = (key, n)
+        slot = self.slots.get(skey)
+        if slot is not None and slot.pkey != self._param_key():
+            del self.slots[skey]
+            slot = None
+        if slot is None:
+            slot = self._capture(fn, inputs, pads or {})
+            self.slots[skey] = slot
+        self.replays += 1
+        return _BridgeFn.apply(slot, *inputs)
+
+    def clear(self):
+        self.slots.clear()
+        self.uses.clear()

@@ -588,6 +588,8 @@ def _attn_ws(device, B, N, D):
     key = (device.index, _stream())
     buf = _AWS.get(key)
     if buf is None or buf.numel() * 4 < need:
+        if buf is not None:
+            _WS_OLD.append(buf)      # kernels already queued / captured in a graph still point at it
         buf = torch.zeros(max(need, 1 << 20) // 4 + 4, dtype=torch.float32, device=device)
         _AWS[key] = buf
     return buf

@@ -266,6 +266,7 @@ class Seq2SeqAgent(BaseAgent):
         # rollout while the one-kernel policy head stays on (dasa_policy_head_fwd mode FORCED)
         self.force_action_fn = None
         self._step_graphs = None     # captured forward-only decision steps (_graph_step)
+        self._train_graphs = None    # captured training decoder steps (_decode, graph.AutogradGraphs)
         self.grad_sync = None        # data-parallel hook set by dasa_amd.dp
 
     def _load_pretrained_bert(self, path):
@@ -547,6 +548,47 @@ class Seq2SeqAgent(BaseAgent):
                                                                   c_t, ctx_mask, cand_lens, target, text))
         return leng, outs
 
+    def _train_graph_ok(self):
+        """A training decoder step (decoder + one-kernel policy head, with autograd) replays as a captured
+        graph (graph.AutogradGraphs) unless a per-step host decision or a caller-visible module hook
+        needs the eager calls, the profiler brackets every launch, or it is switched off
+        (DASA_TRAIN_GRAPH=0)."""
+        dec = self.decoder
+        return (graph.ENABLED and os.environ.get("DASA_TRAIN_GRAPH", "0") != "0" and torch.is_grad_enabled()
+                and dec.training and not prof.active() and not graph.capturing()
+                and not args.decoder_consistent_drop and not args.pred_back and not args.submit
+                and self.sample_fn is None and os.environ.get("DASA_FUSED_HEAD", "1") != "0"
+                and isinstance(dec.drop_env, nn.Dropout)
+                and "forward" not in dec.__dict__ and not dec._forward_hooks and not dec._forward_pre_hooks
+                and (self._train_graphs is None or len(self._train_graphs.slots) < 1024))
+
+    def _decode(self, t, mode, e, h0, prev_h1, c0, ctx_mask, cand_lens, target, forced, dropfeat):
+        """agent_dg.py:811-886 for one step: BAttnDecoderLSTM + the one-kernel policy head (mask, CE,
+        action, entropy / log-prob). Training steps replay a captured graph keyed by the step index;
+        the candidate block is zero-padded to a multiple of 8 (>= 16) and the instruction context to a
+        multiple of 16 tokens with the padding masked: the head masks padded candidates and the
+        instruction attention gives masked tokens weight 0, so every valid logit, loss and gradient is
+        unchanged while few shapes (slots) arise. Otherwise eager. Returns (h_t, c_t, logit, h1, ce,
+        entropy, log-prob of the action, action)."""
+        dec = self.decoder
+
+        def step(a, df, cand, h0, prev_h1, c0, ctx, ctx_mask, cand_lens, target, forced):
+            h_t, c_t, logit, h1, _ = dec(a, df, cand, h0, prev_h1, c0, ctx, ctx_mask, already_dropfeat=dropfeat)
+            ce, ent, lpa, act = DF.policy_head(logit, cand_lens, target, mode, forced=forced)
+            return h_t, c_t, logit, h1, ce, ent, lpa, act
+        inputs = (e["a"], e["df"], e["cand"], h0, prev_h1, c0, e["ctx"], ctx_mask, cand_lens, target, forced)
+        if not self._train_graph_ok():
+            return step(*inputs)
+        if self._train_graphs is None:
+            self._train_graphs = graph.AutogradGraphs([self.decoder])
+        B, C, F = e["cand"].shape
+        L, H2 = e["ctx"].shape[1:]
+        Cp, Lp = max(16, -(-C // 8) * 8), -(-L // 16) * 16
+        key = ("dec", mode, t, B, Cp, Lp, H2, bool(dropfeat))
+        out = self._train_graphs.run(key, step, inputs, pads={2: ((B, Cp, F), 0), 6: ((B, Lp, H2), 0),
+                                                              7: ((B, Lp), True)})
+        return out[:2] + (out[2][:, :C],) + out[3:]
+
     def _encode_steps(self, obs_steps, seq, seq_mask, lens_dev, noise, consistent_drop, inputs=None):
         """Feature stage of the step loop (agent_dg.py:725-805): features -> env drop -> AdaIN ->
         DicEncoder, for one or several steps' observations at once (every op in it is per row, so
@@ -685,6 +727,18 @@ class Seq2SeqAgent(BaseAgent):
                     nxt, perm_obs = self._teacher_plan(perm_obs, perm_idx, ended, last_dist, traj,
                                                        min(chunk, self.episode_len - t_next))
                 for i, (s, e) in enumerate(zip(plan, enc)):
+                    if self._fused_head(e["cand"][:, :, 0]):   # decoder + fused head (captured when training)
+                        h0, c0 = (e["en_ht"], e["en_ct"]) if t == 0 else (h_t, c_t)
+                        h_t, c_t, logit, h1, ce = self._decode(t, "teacher", e, h0, h0 if t == 0 else h1, c0, ctx_mask,
+                                                               self._lens_dev(e["leng"]), targets[i], None,
+                                                               consistent_drop)[:5]
+                        total_forth_loss += ce
+                        t += 1
+                        ctx = e["ctx"]
+                        hidden_states.append(h_t)
+                        rewards.append(s["reward"])
+                        masks.append(s["mask"])
+                        continue
                     if t == 0:
                         h_t, c_t, logit, h1, aux = self.decoder(e["a"], e["df"], e["cand"], e["en_ht"], e["en_ht"],
                                                                 e["en_ct"], e["ctx"], ctx_mask,
@@ -738,7 +792,18 @@ class Seq2SeqAgent(BaseAgent):
                 (e,) = self._encode_steps([perm_obs], *enc_args)
                 candidate_leng = e["leng"]
                 ctx = e["ctx"]
-                if t == 0:
+                fused = self._fused_head(e["cand"][:, :, 0])
+                if fused:          # decoder + mask / CE / action / entropy / log-prob in one kernel (policy.hip)
+                    mode, forced = self.feedback, None
+                    if mode == "sample" and self.force_action_fn is not None:
+                        mode = "forced"
+                        forced = self._to_dev(np.asarray(self.force_action_fn(t, list(candidate_leng)), np.int64))
+                    h0, c0 = (e["en_ht"], e["en_ct"]) if t == 0 else (h_t, c_t)
+                    h_t, c_t, logit, h1, ce, ent, lpa, a_dev = self._decode(
+                        t, mode, e, h0, h0 if t == 0 else h1, c0, ctx_mask, self._lens_dev(candidate_leng), target,
+                        forced, consistent_drop)
+                    aux_outputs = {}
+                elif t == 0:
                     h_t, c_t, logit, h1, aux_outputs = self.decoder(e["a"], e["df"], e["cand"], e["en_ht"],
                                                                     e["en_ht"], e["en_ct"], ctx, ctx_mask,
                                                                     already_dropfeat=consistent_drop)
@@ -746,14 +811,7 @@ class Seq2SeqAgent(BaseAgent):
                     h_t, c_t, logit, h1, aux_outputs = self.decoder(e["a"], e["df"], e["cand"], h_t, h1, c_t, ctx,
                                                                     ctx_mask, already_dropfeat=consistent_drop)
                 hidden_states.append(h_t)
-                fused = self._fused_head(logit)
-                if fused:          # mask + CE + action + entropy / log-prob in one kernel (policy.hip)
-                    mode, forced = self.feedback, None
-                    if mode == "sample" and self.force_action_fn is not None:
-                        mode = "forced"
-                        forced = self._to_dev(np.asarray(self.force_action_fn(t, list(candidate_leng)), np.int64))
-                    ce, ent, lpa, a_dev = DF.policy_head(logit, self._lens_dev(candidate_leng), target, mode,
-                                                         forced=forced)
+                if fused:
                     total_forth_loss += ce
                     if self.feedback == "argmax":
                         a_t = a_dev
@@ -907,6 +965,8 @@ class Seq2SeqAgent(BaseAgent):
     def zero_grad(self):
         self.loss = 0.0
         self.losses = []
+        if self._train_graphs is not None:
+            self._train_graphs.new_iteration()
         for m, opt in zip(self.models, self.optimizers):
             m.train()
             opt.zero_grad()
@@ -941,6 +1001,8 @@ class Seq2SeqAgent(BaseAgent):
             self.loss.backward()
         DF.flush_bilstm_backward()
         DF.flush_weight_grads()
+        if self._train_graphs is not None:
+            self._train_graphs.new_iteration()     # every replayed step has had its backward
         # every kernel with a bounded inter-workgroup barrier (persistent bi-LSTM BPTT, D-split attention
         # backward) NaN-poisons its outputs and sets an error bit when the barrier times out: read the
         # error word (one host sync) before the gradients reach grad_sync, clipping and the optimizers

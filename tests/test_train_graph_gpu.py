@@ -1,0 +1,133 @@
+"""Captured training decision steps (dasa_amd.graph.AutogradGraphs): the decoder step +
+one-kernel policy head of a training rollout replays as a hipGraph recorded with autograd, and its
+backward runs the recorded autograd graph.
+
+* dropout / Categorical draws inside a replay are fresh per replay, and the backward regenerates the
+  forward's masks (the slot's device seed counter is the seed source of both);
+* a cfg2 training iteration (B=20, vl=3, 4 + 4 steps, dropout 0, forced draws) gives the same losses
+  and the same gradients with the capture as eagerly, over two iterations with RMSprop steps in
+  between (in-place parameter updates are read by the replays; no re-capture);
+* slots: one per (rollout, step) — captured in the first iteration, only replayed after.
+Reference: agent_dg.py:725-936 (the step loop), 1389-1405 (optim_step)."""
+import contextlib
+import io
+
+import numpy as np
+import pytest
+import torch
+
+from tests import golden_inputs as GI
+
+pytestmark = pytest.mark.gpu
+
+
+def test_autograd_graph_dropout_masks(dev):
+    from dasa_amd import functional as DF
+    from dasa_amd import graph
+    g = graph.AutogradGraphs([])
+    x = torch.ones(64, 1024, device=dev, requires_grad=True)
+
+    def fn(x):
+        return (DF.dropout(x, 0.5, True),)
+    outs = []
+    for it in range(3):
+        g.new_iteration()
+        (y,) = g.run("drop", fn, (x,))
+        y.backward(torch.ones_like(y))
+        outs.append(y.detach().clone())
+        # d/dx sum(mask / (1 - p) * x) = mask / (1 - p) = y (x = 1): the backward used the replay's mask
+        assert torch.equal(x.grad, y.detach()), it
+        x.grad = None
+    assert g.captures == 1 and g.replays == 3
+    assert not torch.equal(outs[0], outs[1]) and not torch.equal(outs[1], outs[2])   # fresh masks per replay
+    keep = (outs[0] != 0).float().mean().item()
+    assert 0.45 < keep < 0.55
+
+
+def test_autograd_graph_sampling_fresh_per_replay(dev):
+    from dasa_amd import functional as DF
+    from dasa_amd import graph
+    g = graph.AutogradGraphs([])
+    logit = torch.zeros(256, 16, device=dev, requires_grad=True)
+    lens = torch.full((256,), 16, dtype=torch.int32, device=dev)
+
+    def fn(logit, lens):
+        return DF.policy_head(logit, lens, None, "sample")
+    acts = []
+    for _ in range(2):
+        g.new_iteration()
+        ce, ent, lpa, act = g.run("head", fn, (logit, lens))
+        acts.append(act.cpu())
+        lpa.sum().backward()
+        # uniform logits: d log p(a) / dz_j = onehot_a - 1/16, summed over rows
+        want = torch.zeros(256, 16)
+        want[torch.arange(256), act.cpu()] = 1.0
+        want -= 1.0 / 16
+        assert torch.allclose(logit.grad.cpu(), want, atol=1e-6)
+        logit.grad = None
+    assert not torch.equal(acts[0], acts[1])
+
+
+def _agent(seed_env):
+    from dasa_amd.r2r import param
+    from dasa_amd.r2r.agent_dg import Seq2SeqAgent
+    from dasa_amd.synth import SynthR2RBatch, SynthWorld, init_params
+    env = SynthR2RBatch(SynthWorld(32, 0, 5), 20, seed=seed_env, mode="wander", instr_len=80, variable_len=True)
+    with contextlib.redirect_stdout(io.StringIO()):
+        ag = Seq2SeqAgent(env, "", None, 4, "Dic")
+    for m, s in ((ag.encoder, 1), (ag.decoder, 2), (ag.critic, 3), (ag.adaIn, 4)):
+        init_params(m, s)
+        for sub in m.modules():
+            if isinstance(sub, torch.nn.Dropout):
+                sub.p = 0.0
+    param.args.ml_weight = param.args.ml_weight_org
+    return ag
+
+
+def _iteration(ag, it):
+    from dasa_amd import functional as DF
+    table = GI.forced_table(4, 20, seed=GI.FORCED_SEED + it)
+    ag.force_action_fn = lambda t, lens: GI.forced_actions(table, t, lens, no_stop=True)
+    ag.zero_grad()
+    ag.accumulate_gradient("sample")
+    loss = ag.loss.item()
+    with DF.defer_bilstm_backward(), DF.defer_weight_grads():
+        ag.loss.backward()
+    DF.flush_bilstm_backward()
+    DF.flush_weight_grads()
+    grads = {f"{i}.{k}": p.grad.detach().clone() for i, m in enumerate(ag.models) for k, p in m.named_parameters()
+             if p.grad is not None}
+    for opt in ag.optimizers:
+        opt.step()
+    if ag._train_graphs is not None:
+        ag._train_graphs.new_iteration()
+    return loss, list(ag.logs["entropy"][-4:]), grads
+
+
+def test_train_graph_matches_eager(dev, monkeypatch):
+    from dasa_amd.r2r import param
+    param.readme_train(["--d_vl_layers", "3", "--batchSize", "20", "--maxAction", "4"])
+    try:
+        res = {}
+        for mode in ("0", "1"):
+            monkeypatch.setenv("DASA_TRAIN_GRAPH", mode)
+            torch.manual_seed(3)
+            ag = _agent(700)
+            res[mode] = [_iteration(ag, it) for it in range(2)]
+            if mode == "1":
+                tg = ag._train_graphs
+                assert tg is not None and tg.captures == 8 and len(tg.slots) == 8, (tg and tg.captures)
+                assert tg.replays == 16
+            else:
+                assert ag._train_graphs is None
+            del ag
+        for it in range(2):
+            (l0, e0, g0), (l1, e1, g1) = res["0"][it], res["1"][it]
+            assert abs(l0 - l1) <= 1e-6 * max(1.0, abs(l0)), (it, l0, l1)
+            assert np.allclose(e0, e1, rtol=1e-6, atol=0), (it, e0, e1)
+            assert sorted(g0) == sorted(g1)
+            for k in g0:
+                err = (g0[k] - g1[k]).abs().max().item()
+                assert err <= 1e-5 * max(1e-30, g0[k].abs().max().item()), (it, k, err)
+    finally:
+        param.readme_train(["--d_vl_layers", "1", "--batchSize", "2", "--maxAction", "5"])
