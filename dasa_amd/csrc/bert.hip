@@ -268,7 +268,8 @@ struct MhaArgs {
   const float* Q; long ldq; const float* K; long ldk; const float* V; long ldv;
   const float* mask; float* out; long ldo; float* probs;
   int B, heads, Lq, Lk; float scale; float p; uint64_t seed;
-  const uint64_t* seed_src;   // graph-captured forward only (eff_seed); the backward uses plain seeds
+  const uint64_t* seed_src;   // device seed source of a graph-captured launch (eff_seed), or null: the
+                              // backward of a captured training step re-keys with the same source
 };
 
 // Forward on matrix cores (v_mfma_f32_32x32x2_f32): one workgroup per (batch, head), one wave per
@@ -433,8 +434,9 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(MhaArgs a, const float* dO
     float p0 = lane < Lk ? a.probs[prow + lane] : 0.f;
     float p1 = lane + 64 < Lk ? a.probs[prow + lane + 64] : 0.f;
     // attention-probs dropout (train mode): the same counter-RNG mask as the forward
-    const float k0 = a.p > 0.f ? dasa_dropout_scale(a.p, a.seed, (uint64_t)prow + lane) : 1.f;
-    const float k1 = a.p > 0.f ? dasa_dropout_scale(a.p, a.seed, (uint64_t)prow + lane + 64) : 1.f;
+    const uint64_t sd = a.p > 0.f ? eff_seed(a.seed, a.seed_src) : 0;
+    const float k0 = a.p > 0.f ? dasa_dropout_scale(a.p, sd, (uint64_t)prow + lane) : 1.f;
+    const float k1 = a.p > 0.f ? dasa_dropout_scale(a.p, sd, (uint64_t)prow + lane + 64) : 1.f;
     float dp0 = 0.f, dp1 = 0.f;
     if (lane < Lk)
       for (int d = 0; d < kDh; ++d) dp0 = fmaf(dos[w][d], Vs[lane][d], dp0);
@@ -513,6 +515,7 @@ __global__ __launch_bounds__(256) void mha_bwd_lds_kernel(MhaArgs a, const float
   __shared__ float sdS[kBwdBufL];    // dP, then dS [Lq][Lk]
   __shared__ float sdST[kBwdBufL];   // dS^T [Lk][Lq]
   __shared__ float rowdot[kBwdMaxL];
+  const uint64_t sdk = a.p > 0.f ? eff_seed(a.seed, a.seed_src) : 0;   // dropout seed of this launch
   const int bh = blockIdx.x, b = bh / a.heads, h = bh % a.heads, t = threadIdx.x;
   const int Lq = a.Lq, Lk = a.Lk, Lq4 = (Lq + 3) & ~3, Lk4 = (Lk + 3) & ~3;
   const long pbase = ((long)b * a.heads + h) * Lq * Lk;
@@ -541,7 +544,7 @@ __global__ __launch_bounds__(256) void mha_bwd_lds_kernel(MhaArgs a, const float
         const int i = m0 + r, j = n0 + c;
         float v = 0.f;
         if (i < Lq && j < Lk)
-          v = drop ? acc[r][c] * dasa_dropout_scale(a.p, a.seed, (uint64_t)(pbase + (long)i * Lk + j)) : acc[r][c];
+          v = drop ? acc[r][c] * dasa_dropout_scale(a.p, sdk, (uint64_t)(pbase + (long)i * Lk + j)) : acc[r][c];
         sdS[i * kBwdLd + j] = v;
       }
   });
@@ -564,7 +567,7 @@ __global__ __launch_bounds__(256) void mha_bwd_lds_kernel(MhaArgs a, const float
   if (drop)
     for (int idx = t; idx < Lq * Lk; idx += blockDim.x) {
       const int i = idx / Lk, j = idx % Lk;
-      sP[i * kBwdLd + j] *= dasa_dropout_scale(a.p, a.seed, (uint64_t)(pbase + idx));
+      sP[i * kBwdLd + j] *= dasa_dropout_scale(a.p, sdk, (uint64_t)(pbase + idx));
     }
   for (int idx = t; idx < Lq4 * kDh; idx += blockDim.x) {
     const int i = idx / kDh, d = idx % kDh;
@@ -831,7 +834,7 @@ extern "C" int dasa_mha_bwd(const float* Q, int64_t ldq, const float* K, int64_t
   if (B <= 0 || Lq <= 0) return 0;
   if (dh != kDh || Lk <= 0 || Lk > kMaxLk || !probs) return (int)hipErrorInvalidValue;
   MhaArgs a{Q, ldq, K, ldk, V, ldv, nullptr, nullptr, 0, const_cast<float*>(probs), B, heads, Lq, Lk, scale, drop_p,
-            seed, nullptr};
+            seed, drop_p > 0.f ? dasa_seed_src_host() : nullptr};
   const bool vec = ((ldq | ldk | ldv) & 3) == 0 && (((uintptr_t)dQ | (uintptr_t)dK | (uintptr_t)dV) & 15) == 0;
   if (Lq <= kBwdMaxL && Lk <= kBwdMaxL && vec)
     hipLaunchKernelGGL(mha_bwd_lds_kernel, dim3(B * heads), dim3(256), 0, (hipStream_t)stream, a, dout, (long)lddo, dQ,

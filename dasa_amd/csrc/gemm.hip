@@ -1176,6 +1176,11 @@ void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
     const int rows = min(gm, (int)gridDim.y - grp * gm), r = wgid - grp * per;
     m0 = (grp * gm + r % rows) * BM;
     n0 = (r / rows) * BN;
+  } else if (p.group_m < -1) {   // grouped along N: -group_m column panels of W stay in L2, A streams
+    const int gn = -p.group_m, per = gn * gridDim.y, grp = wgid / per;
+    const int cols = min(gn, (int)gridDim.x - grp * gn), r = wgid - grp * per;
+    n0 = (grp * gn + r % cols) * BN;
+    m0 = (r / cols) * BM;
   } else {
     n0 = (wgid % gridDim.x) * BN;
     m0 = (wgid / gridDim.x) * BM;
@@ -2111,6 +2116,17 @@ static int x6_form_override() {
   return g_x6_form;
 }
 
+// DASA_X6_GROUP=<g>: A/B of the bf16x6 tile order (g > 1: g row panels per L2 group, walked column by
+// column — the default 4; g < -1: -g column panels per group, walked row by row; 1: plain row-major)
+static int g_x6_group = 0x7fffffff;
+static int x6_group_override() {
+  if (g_x6_group == 0x7fffffff) {
+    const char* e = getenv("DASA_X6_GROUP");
+    g_x6_group = e ? atoi(e) : 0;
+  }
+  return g_x6_group;
+}
+
 // DASA_X6_BALANCE: 0 = no split-K on many-tile problems (default), 1 = 2- or 3-way, 2 = 2-way only. Off:
 // measured slower in isolation on every shape but 12800 x 768 x 3072 (+4 %; 1600 x 4096 x 768 -23 %,
 // 720 x 3072 x 768 -20 %) and within run-to-run noise in the training iteration (3359-3604 on vs
@@ -2390,6 +2406,7 @@ extern "C" int dasa_gemm_f32x6_ws(const dasa_gemm_desc* d, int64_t plane, void* 
   if (pl.splitk > 1 && (ws == nullptr || ws_bytes < pl.ws)) { pl.splitk = 1; pl.kchunk = K; }
   const int cfg = pl.cfg, bm = pl.bm, bn = pl.bn;
   p.group_m = cdiv(M, bm) >= 8 ? 4 : 1;
+  if (x6_group_override() != 0) p.group_m = x6_group_override();   // A/B: DASA_X6_GROUP (< -1: along N)
   X6Split xs{};
   hipStream_t st = (hipStream_t)stream;
   if (pl.splitk > 1) {

@@ -232,7 +232,8 @@ class AutogradGraphs:
                 continue
             shape, fill = pads.get(i, (x.shape, 0))
             s = torch.full(shape, fill, dtype=x.dtype, device=dev)    # the padding keeps its fill value
-            _lead(s, x.shape).copy_(x)
+            with torch.no_grad():       # a LEAF: recorded, the copy would link the slot to x's graph
+                _lead(s, x.shape).copy_(x)
             static_in.append(s.requires_grad_(x.requires_grad))
         self.stream.wait_stream(torch.cuda.current_stream())
         _NESTED[0] += 1
