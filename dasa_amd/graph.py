@@ -236,7 +236,9 @@ class AutogradGraphs:
                 _lead(s, x.shape).copy_(x)
             static_in.append(s.requires_grad_(x.requires_grad))
         self.stream.wait_stream(torch.cuda.current_stream())
+        from . import ops
         _NESTED[0] += 1
+        ops._FRESH_PLANES[0] += 1
         try:
             # warm-up on the capture stream (lazily built workspaces / caches outside the capture); its
             # autograd graph is dropped
@@ -256,6 +258,7 @@ class AutogradGraphs:
                 L.dasa_set_seed_source(None)
         finally:
             _NESTED[0] -= 1
+            ops._FRESH_PLANES[0] -= 1
         slot.graph, slot.static_in, slot.static_out = g, static_in, tuple(out)
         slot.pkey = self._param_key()
         self.captures += 1

@@ -248,8 +248,16 @@ def split3_bf16(W):
     return planes
 
 
+_FRESH_PLANES = [0]   # > 0 while a training region is captured (graph.AutogradGraphs): see _x6_weight
+
+
 def _x6_weight(W):
-    """The cached bf16 planes of W for this weight version (recomputed after in-place updates)."""
+    """The cached bf16 planes of W for this weight version (recomputed after in-place updates). Inside a
+    captured TRAINING region the split is recorded into the graph instead (fresh planes on every replay):
+    the region's weights change in place with every optimizer step, which a cached plane buffer baked
+    into the graph would not see."""
+    if _FRESH_PLANES[0]:
+        return split3_bf16(W)
     wid = id(W)
     e = _X6.get(wid)
     if e is not None and e[0]() is W and e[1] == W._version and e[2] == W.data_ptr():

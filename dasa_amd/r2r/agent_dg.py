@@ -589,6 +589,51 @@ class Seq2SeqAgent(BaseAgent):
                                                               7: ((B, Lp), True)})
         return out[:2] + (out[2][:, :C],) + out[3:]
 
+    def _step_region_ok(self, consistent_drop, noise):
+        """The per-step loop's AdaIN joins the captured decoder region (_adain_decode) in the README
+        configuration: the channel AdaIN as one fused gate, no --ctx_v, and the shared env-drop noise
+        (aug half) only after AdaIN (agent_dg.py:764-785)."""
+        use_noise = consistent_drop and noise is not None
+        return (self._train_graph_ok() and args.adaIn_type == "channel" and self.adaIn.fused_ok() and not args.ctx_v
+                and (not use_noise or args.env_drop_stage == "after_adain"))
+
+    def _adain_decode(self, t, mode, inputs, seq, seq_mask, lens_dev, noise, consistent_drop, h_t, h1, c_t, ctx_mask,
+                      target, forced_fn):
+        """One decision step of the per-step loop (agent_dg.py:725-886) with AdaIN, the decoder and the
+        policy head as ONE captured training region: the observation gather and the DicEncoder (its
+        language stack comes from the side-stream pipe, the bi-LSTM needs the whole chip) run eagerly
+        around it. Same values as _encode_steps + _decode. Returns (leng, ctx, h_t, c_t, logit, h1, ce,
+        entropy, log-prob, action)."""
+        a, f, d, cf, cd, cinfo = inputs
+        _, C, leng = cinfo[0]
+        B = a.shape[0]
+        use_noise = consistent_drop and noise is not None
+        img = self._noise_mult(f, noise) if (use_noise and args.use_dropout_vision) else f   # agent_dg.py:780-797
+        ctx, en_ht, en_ct, _, _ = self.encoder(seq, mask=seq_mask, lengths=lens_dev, f_t_all=img, want_vision=False)
+        h0, c0, prev = (en_ht, en_ct, en_ht) if t == 0 else (h_t, c_t, h1)
+        forced = forced_fn(leng) if forced_fn is not None else None
+        cand_lens = self._lens_dev(leng)
+        dec, ada, depth_drop = self.decoder, self.adaIn, args.depth_drop
+
+        def step(a, f, d, cf, cd, noise, h0, prev_h1, c0, ctx, ctx_mask, cand_lens, target, forced):
+            df = ada.feature(f, d, noise if (noise is not None and depth_drop) else None)
+            cand = ada.feature(cf, cd, noise)
+            h_t, c_t, logit, h1, _ = dec(a, df, cand, h0, prev_h1, c0, ctx, ctx_mask, already_dropfeat=consistent_drop)
+            ce, ent, lpa, act = DF.policy_head(logit, cand_lens, target, mode, forced=forced)
+            return h_t, c_t, logit, h1, ce, ent, lpa, act
+        cf3, cd3 = cf.view(B, C, -1), cd.view(B, C, -1)
+        step_in = (a, f, d, cf3, cd3, noise if use_noise else None, h0, prev, c0, ctx, ctx_mask, cand_lens, target,
+                   forced)
+        if self._train_graphs is None:
+            self._train_graphs = graph.AutogradGraphs([self.decoder, self.adaIn])
+        F = cf3.shape[2]
+        L, H2 = ctx.shape[1:]
+        Cp, Lp = max(16, -(-C // 8) * 8), -(-L // 16) * 16
+        key = ("step", mode, t, B, Cp, Lp, H2, bool(consistent_drop), bool(use_noise))
+        out = self._train_graphs.run(key, step, step_in, pads={3: ((B, Cp, F), 0), 4: ((B, Cp, F), 0),
+                                                               9: ((B, Lp, H2), 0), 10: ((B, Lp), True)})
+        return (leng, ctx) + out[:2] + (out[2][:, :C],) + out[3:]
+
     def _encode_steps(self, obs_steps, seq, seq_mask, lens_dev, noise, consistent_drop, inputs=None):
         """Feature stage of the step loop (agent_dg.py:725-805): features -> env drop -> AdaIN ->
         DicEncoder, for one or several steps' observations at once (every op in it is per row, so
@@ -776,6 +821,46 @@ class Seq2SeqAgent(BaseAgent):
                     total_forth_loss += ce
                     policy_log_probs.append(lpa.unsqueeze(1))
                     cpu_a_t = a_t.cpu().numpy().copy()      # the step's one device->host sync
+                    for i, next_id in enumerate(cpu_a_t):
+                        if next_id == (candidate_leng[i] - 1) or next_id == args.ignoreid:
+                            cpu_a_t[i] = -1
+                    self.make_equiv_action(cpu_a_t, perm_obs, perm_idx, traj)
+                    obs = np.array(self.env._get_obs())
+                    perm_obs = obs[perm_idx]
+                    reward, mask = self._step_reward(perm_obs, cpu_a_t, ended, last_dist)
+                    rewards.append(reward)
+                    masks.append(mask)
+                    ended[:] = np.logical_or(ended, (cpu_a_t == -1))
+                    if ended.all():
+                        break
+                    continue
+                if self._step_region_ok(consistent_drop, noise):
+                    # AdaIN + decoder + one-kernel policy head replayed as one captured training region
+                    mode = self.feedback
+                    forced_fn = None
+                    if mode == "sample" and self.force_action_fn is not None:
+                        mode = "forced"
+                        forced_fn = (lambda leng, t=t: self._to_dev(
+                            np.asarray(self.force_action_fn(t, list(leng)), np.int64)))
+                    candidate_leng, ctx, h_t, c_t, logit, h1, ce, ent, lpa, a_dev = self._adain_decode(
+                        t, mode, self._step_inputs([perm_obs]), *enc_args, h_t, h1, c_t, ctx_mask, target, forced_fn)
+                    fused, aux_outputs = True, {}
+                    hidden_states.append(h_t)
+                    total_forth_loss += ce
+                    if self.feedback == "argmax":
+                        a_t = a_dev
+                        policy_log_probs.append(lpa.unsqueeze(1))
+                    elif self.feedback == "sample":
+                        deferred["entropy"].append(ent.sum().detach())
+                        entropys.append(ent)
+                        a_t = a_dev
+                        policy_log_probs.append(lpa)
+                    else:
+                        a_t = target
+                    if self.feedback == "teacher":
+                        cpu_a_t = target_np.copy()
+                    else:
+                        cpu_a_t = a_t.cpu().numpy().copy()  # the step's one device->host sync
                     for i, next_id in enumerate(cpu_a_t):
                         if next_id == (candidate_leng[i] - 1) or next_id == args.ignoreid:
                             cpu_a_t[i] = -1
