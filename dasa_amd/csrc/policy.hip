@@ -59,7 +59,8 @@ __global__ __launch_bounds__(1024) void policy_head_fwd_kernel(PolicyFwd a) {
     for (int k = 0; k < kVpl; ++k) s += (z[k] == -INFINITY) ? 0.f : __expf(z[k] - m);
     s = wave_sum(s);
     const float lse = m + __logf(s);
-    const bool cat = a.mode == DASA_POLICY_SAMPLE || a.mode == DASA_POLICY_FORCED;   // Categorical semantics
+    const bool cat = a.mode == DASA_POLICY_SAMPLE || a.mode == DASA_POLICY_FORCED ||
+                     a.mode == DASA_POLICY_SAMPLE_ARGMAX;   // Categorical semantics
     float lp[kVpl], lc[kVpl], h = 0.f;
 #pragma unroll
     for (int k = 0; k < kVpl; ++k) {
@@ -85,7 +86,7 @@ __global__ __launch_bounds__(1024) void policy_head_fwd_kernel(PolicyFwd a) {
     }
     // action
     int act = -1;
-    if (a.mode == DASA_POLICY_ARGMAX) {   // first index of the max, as torch.max over the masked logits
+    if (a.mode == DASA_POLICY_ARGMAX || a.mode == DASA_POLICY_SAMPLE_ARGMAX) {   // first index of the max (torch.max)
       float best = -INFINITY;
       int bi = 0x7fffffff;
 #pragma unroll
@@ -165,7 +166,7 @@ struct PolicyBwd {
 // with g_c = dH / dp_c = -(l_c + u_c). Argmax / teacher: u = 1 and l = log p (the exact log-softmax).
 __global__ __launch_bounds__(1024) void policy_head_bwd_kernel(PolicyBwd a) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const bool cat = a.mode == DASA_POLICY_SAMPLE || a.mode == DASA_POLICY_FORCED;
+  const bool cat = a.mode == DASA_POLICY_SAMPLE || a.mode == DASA_POLICY_FORCED || a.mode == DASA_POLICY_SAMPLE_ARGMAX;
   for (int b = blockIdx.x * nw + w; b < a.B; b += gridDim.x * nw) {
     const int L = a.len[b];
     float p[kVpl], gh[kVpl];
@@ -219,7 +220,7 @@ extern "C" int dasa_policy_head_fwd(const float* logit, int64_t ld, const int32_
   if (C <= 0 || C > 64 * kVpl || ld < C || !logit || !cand_len || !logp || !ce_sum || !ws)
     return (int)hipErrorInvalidValue;
   if (mode != DASA_POLICY_TEACHER && mode != DASA_POLICY_ARGMAX && mode != DASA_POLICY_SAMPLE &&
-      mode != DASA_POLICY_FORCED)
+      mode != DASA_POLICY_FORCED && mode != DASA_POLICY_SAMPLE_ARGMAX)
     return (int)hipErrorInvalidValue;
   if (mode != DASA_POLICY_TEACHER && !action) return (int)hipErrorInvalidValue;
   // a captured sampled step draws fresh actions on every replay: the seed is re-keyed by the device
@@ -238,7 +239,7 @@ extern "C" int dasa_policy_head_bwd(const float* logp, const int32_t* cand_len, 
                                     int32_t B, int32_t C, int32_t mode, int32_t ignore_index, void* stream) {
   if (B <= 0 || C <= 0) return 0;
   if (C > 64 * kVpl || ldd < C || !logp || !cand_len || !dlogit || (d_ent && !ent)) return (int)hipErrorInvalidValue;
-  if (mode < DASA_POLICY_TEACHER || mode > DASA_POLICY_FORCED) return (int)hipErrorInvalidValue;
+  if (mode < DASA_POLICY_TEACHER || mode > DASA_POLICY_SAMPLE_ARGMAX) return (int)hipErrorInvalidValue;
   PolicyBwd a{logp, cand_len, target, action, ent, d_ce, d_logp_a, d_ent, dlogit, (long)ldd, B, C, ignore_index,
               mode};
   const int waves = B < 16 ? B : 16;

@@ -385,6 +385,43 @@ class SoftDotTildeFn(torch.autograd.Function):
         return dh, dc, None, dWin, dWout
 
 
+class SoftDotFn(torch.autograd.Function):
+    """SoftDotAttention with output_tilde=False in general (model.py:268-296): the weighted context and
+    the attention — the masked softmax, or with want_scores the raw scores with -inf where masked (the
+    reference's aliased `logit`, masked in place). wctx and the scores are differentiable (dasa_softdot_bwd
+    takes dwctx and dscores); the softmax output is returned detached (no caller differentiates it)."""
+
+    @staticmethod
+    def forward(ctx, h, c, mask, W_in, want_scores):
+        q = ops.linear(h, W_in)
+        scores, probs, wctx = ops.softdot_fwd(q, c, mask)
+        if mask is not None and want_scores:
+            scores = scores.masked_fill(mask.bool(), -float("inf"))
+        if any(ctx.needs_input_grad):
+            ctx.save_for_backward(h, c, q, probs, mask.bool() if mask is not None else None)
+            ctx.params = (W_in,)
+        ctx.want_scores = want_scores
+        if not want_scores:
+            ctx.mark_non_differentiable(probs)
+        return wctx, (scores if want_scores else probs)
+
+    @staticmethod
+    def backward(ctx, dwctx, dattn):
+        h, c, q, probs, mask = ctx.saved_tensors
+        W_in = ctx.params[0]
+        ds = None
+        if ctx.want_scores and dattn is not None:
+            ds = dattn.masked_fill(mask, 0.0) if mask is not None else dattn
+        if dwctx is None:
+            dwctx = torch.zeros_like(q)
+        dq, dc = ops.softdot_bwd(q, c.contiguous(), probs, dwctx=dwctx.contiguous(),
+                                 dscores=ds.contiguous() if ds is not None else None,
+                                 want_dctx=ctx.needs_input_grad[1])
+        dh = ops.matmul_nn(dq, W_in) if ctx.needs_input_grad[0] else None
+        dW = _wgrad(W_in, dq, h) if ctx.needs_input_grad[3] else None
+        return dh, dc, None, dW, None
+
+
 class CandLogitFn(torch.autograd.Function):
     """SoftDotAttention with output_prob=False, output_tilde=False: the raw candidate logits
     (model.py:276-280, 289-290; used as the policy logits at model.py:559)."""

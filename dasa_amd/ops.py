@@ -537,7 +537,7 @@ def mha_bwd(Q, K, V, probs, dout, heads, scale, drop_p=0.0, seed=0):
 
 
 # ------------------------------------------------------------------------------ policy head
-POLICY_MODES = {"teacher": 0, "argmax": 1, "sample": 2, "forced": 3}
+POLICY_MODES = {"teacher": 0, "argmax": 1, "sample": 2, "forced": 3, "sample_argmax": 4}
 
 
 def policy_head_fwd(logit, cand_len_i32, target, mode, seed, ignore_index=-100, forced=None):

@@ -20,7 +20,6 @@ from collections import defaultdict
 import numpy as np
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
 from .. import functional as DF
 from .. import graph
@@ -261,7 +260,7 @@ class Seq2SeqAgent(BaseAgent):
         self.losses = []
         self.criterion = nn.CrossEntropyLoss(ignore_index=args.ignoreid, reduction="sum")
         self.logs = defaultdict(list)
-        self.sample_fn = None        # test hook: probs -> actions, replaces Categorical sampling (torch head)
+        self.sample_fn = None        # test hook: "argmax" replaces the sampled rollout's Categorical draw by the argmax
         # test hook: (step, candidate lengths) -> int64 [B] actions replacing the draw of the sampled
         # rollout while the one-kernel policy head stays on (dasa_policy_head_fwd mode FORCED)
         self.force_action_fn = None
@@ -295,10 +294,41 @@ class Seq2SeqAgent(BaseAgent):
                 list(perm_idx), progresses)
 
     def _fused_head(self, logit):
-        """The one-kernel policy head (dasa_policy_head_fwd) applies unless a host-side mask edit
-        (--submit), the back-prediction head (its mask is reused) or the sampling test hook is on."""
-        return (not args.submit and not args.pred_back and self.sample_fn is None and logit.shape[1] <= 256
-                and os.environ.get("DASA_FUSED_HEAD", "1") != "0")
+        """Every decision step's loss / action stage is the one-kernel policy head (dasa_policy_head_fwd,
+        C <= 256 candidates); --submit's visited candidates and the back-prediction head (--pred_back) are
+        fed to it as an extra mask / a second teacher-mode call."""
+        if logit.shape[1] > 256:
+            raise NotImplementedError("more than 256 candidates per viewpoint")
+        return True
+
+    def _head_mode(self):
+        """The policy head's mode for this rollout's feedback (agent_dg.py:862-886): teacher, argmax,
+        sample (a Categorical draw on the device RNG), forced (force_action_fn: a caller's action table)
+        or sample_argmax (sample_fn == "argmax": Categorical semantics with the draw replaced by the
+        argmax, the golden fixtures' sampled rollouts)."""
+        fb = self.feedback
+        if fb == "sample":
+            if self.force_action_fn is not None:
+                return "forced"
+            if self.sample_fn is None:
+                return "sample"
+            if self.sample_fn == "argmax":
+                return "sample_argmax"
+            raise NotImplementedError("sample_fn: None or 'argmax' (the policy head draws on the device)")
+        if fb in ("teacher", "argmax"):
+            return fb
+        sys.exit("Invalid feedback option")
+
+    def _visited_mask(self, perm_obs, visited, C):
+        """--submit (agent_dg.py:852-858): a candidate whose viewpoint the agent already visited is masked
+        like a padding candidate; updates `visited` with this step's viewpoints."""
+        m = np.zeros((len(perm_obs), C), dtype=bool)
+        for i, ob in enumerate(perm_obs):
+            visited[i].add(ob["viewpoint"])
+            for c_id, c in enumerate(ob["candidate"]):
+                if c["viewpointId"] in visited[i]:
+                    m[i, c_id] = True
+        return self._to_dev(m)
 
     def _lens_dev(self, leng):
         return self._to_dev(np.asarray(leng, dtype=np.int32))
@@ -510,8 +540,7 @@ class Seq2SeqAgent(BaseAgent):
         return (graph.ENABLED and t > 0 and self.feedback == "argmax" and not torch.is_grad_enabled()
                 and not enc.training and not self.decoder.training and speaker is None
                 and not (consistent_drop and noise is not None) and not args.submit and not args.pred_back
-                and self.sample_fn is None and os.environ.get("DASA_FUSED_HEAD", "1") != "0"
-                and os.environ.get("DASA_STEP_GRAPH", "1") != "0"
+                and self.sample_fn is None and os.environ.get("DASA_STEP_GRAPH", "1") != "0"
                 and enc._lang_cache_on and enc._lang_cache is not None and not prof.active()
                 # a caller that wraps or hooks the modules observes every per-step call: run eagerly
                 and all("forward" not in m.__dict__ and not m._forward_hooks and not m._forward_pre_hooks
@@ -557,28 +586,40 @@ class Seq2SeqAgent(BaseAgent):
         return (graph.ENABLED and os.environ.get("DASA_TRAIN_GRAPH", "0") != "0" and torch.is_grad_enabled()
                 and dec.training and not prof.active() and not graph.capturing()
                 and not args.decoder_consistent_drop and not args.pred_back and not args.submit
-                and self.sample_fn is None and os.environ.get("DASA_FUSED_HEAD", "1") != "0"
                 and isinstance(dec.drop_env, nn.Dropout)
                 and "forward" not in dec.__dict__ and not dec._forward_hooks and not dec._forward_pre_hooks
                 and (self._train_graphs is None or len(self._train_graphs.slots) < 1024))
 
-    def _decode(self, t, mode, e, h0, prev_h1, c0, ctx_mask, cand_lens, target, forced, dropfeat):
+    def _decode(self, t, mode, e, h0, prev_h1, c0, ctx_mask, cand_lens, target, forced, dropfeat, extra_mask=None,
+                back_target=None):
         """agent_dg.py:811-886 for one step: BAttnDecoderLSTM + the one-kernel policy head (mask, CE,
         action, entropy / log-prob). Training steps replay a captured graph keyed by the step index;
         the candidate block is zero-padded to a multiple of 8 (>= 16) and the instruction context to a
         multiple of 16 tokens with the padding masked: the head masks padded candidates and the
         instruction attention gives masked tokens weight 0, so every valid logit, loss and gradient is
-        unchanged while few shapes (slots) arise. Otherwise eager. Returns (h_t, c_t, logit, h1, ce,
-        entropy, log-prob of the action, action)."""
+        unchanged while few shapes (slots) arise. Otherwise eager, with --submit's extra mask and the
+        --pred_back CE (a second teacher-mode head call on the back logits, agent_dg.py:872-876).
+        Returns (h_t, c_t, logit, h1, ce, entropy, log-prob of the action, action, back CE or None)."""
         dec = self.decoder
 
         def step(a, df, cand, h0, prev_h1, c0, ctx, ctx_mask, cand_lens, target, forced):
             h_t, c_t, logit, h1, _ = dec(a, df, cand, h0, prev_h1, c0, ctx, ctx_mask, already_dropfeat=dropfeat)
             ce, ent, lpa, act = DF.policy_head(logit, cand_lens, target, mode, forced=forced)
             return h_t, c_t, logit, h1, ce, ent, lpa, act
+        if extra_mask is not None or args.pred_back or not self._train_graph_ok():
+            h_t, c_t, logit, h1, aux = dec(e["a"], e["df"], e["cand"], h0, prev_h1, c0, e["ctx"], ctx_mask,
+                                           already_dropfeat=dropfeat)
+            if extra_mask is not None:
+                logit = logit.masked_fill(extra_mask, -float("inf"))
+            ce, ent, lpa, act = DF.policy_head(logit, cand_lens, target, mode, forced=forced)
+            back = None
+            if args.pred_back:
+                bl = aux["back_logit"]
+                if extra_mask is not None:
+                    bl = bl.masked_fill(extra_mask, -float("inf"))
+                back = DF.policy_head(bl, cand_lens, back_target, "teacher")[0]
+            return h_t, c_t, logit, h1, ce, ent, lpa, act, back
         inputs = (e["a"], e["df"], e["cand"], h0, prev_h1, c0, e["ctx"], ctx_mask, cand_lens, target, forced)
-        if not self._train_graph_ok():
-            return step(*inputs)
         if self._train_graphs is None:
             self._train_graphs = graph.AutogradGraphs([self.decoder])
         B, C, F = e["cand"].shape
@@ -587,7 +628,7 @@ class Seq2SeqAgent(BaseAgent):
         key = ("dec", mode, t, B, Cp, Lp, H2, bool(dropfeat))
         out = self._train_graphs.run(key, step, inputs, pads={2: ((B, Cp, F), 0), 6: ((B, Lp, H2), 0),
                                                               7: ((B, Lp), True)})
-        return out[:2] + (out[2][:, :C],) + out[3:]
+        return out[:2] + (out[2][:, :C],) + out[3:] + (None,)
 
     def _step_region_ok(self, consistent_drop, noise):
         """The per-step loop's AdaIN joins the captured decoder region (_adain_decode) in the README
@@ -772,38 +813,18 @@ class Seq2SeqAgent(BaseAgent):
                     nxt, perm_obs = self._teacher_plan(perm_obs, perm_idx, ended, last_dist, traj,
                                                        min(chunk, self.episode_len - t_next))
                 for i, (s, e) in enumerate(zip(plan, enc)):
-                    if self._fused_head(e["cand"][:, :, 0]):   # decoder + fused head (captured when training)
-                        h0, c0 = (e["en_ht"], e["en_ct"]) if t == 0 else (h_t, c_t)
-                        h_t, c_t, logit, h1, ce = self._decode(t, "teacher", e, h0, h0 if t == 0 else h1, c0, ctx_mask,
-                                                               self._lens_dev(e["leng"]), targets[i], None,
-                                                               consistent_drop)[:5]
-                        total_forth_loss += ce
-                        t += 1
-                        ctx = e["ctx"]
-                        hidden_states.append(h_t)
-                        rewards.append(s["reward"])
-                        masks.append(s["mask"])
-                        continue
-                    if t == 0:
-                        h_t, c_t, logit, h1, aux = self.decoder(e["a"], e["df"], e["cand"], e["en_ht"], e["en_ht"],
-                                                                e["en_ct"], e["ctx"], ctx_mask,
-                                                                already_dropfeat=consistent_drop)
-                    else:
-                        h_t, c_t, logit, h1, aux = self.decoder(e["a"], e["df"], e["cand"], h_t, h1, c_t, e["ctx"],
-                                                                ctx_mask, already_dropfeat=consistent_drop)
+                    self._fused_head(e["cand"][:, :, 0])
+                    h0, c0 = (e["en_ht"], e["en_ct"]) if t == 0 else (h_t, c_t)
+                    back_target = self._back_teacher_action(s["obs"], s["ended"]) if args.pred_back else None
+                    h_t, c_t, logit, h1, ce, _, _, _, back = self._decode(
+                        t, "teacher", e, h0, h0 if t == 0 else h1, c0, ctx_mask, self._lens_dev(e["leng"]),
+                        targets[i], None, consistent_drop, None, back_target)
+                    total_forth_loss += ce
+                    if back is not None:
+                        total_back_loss += back
                     t += 1
                     ctx = e["ctx"]
                     hidden_states.append(h_t)
-                    if self._fused_head(logit):
-                        total_forth_loss += DF.policy_head(logit, self._lens_dev(e["leng"]), targets[i], "teacher")[0]
-                    else:
-                        candidate_mask = utils.length2mask(e["leng"], device=self.device)
-                        logit = logit.masked_fill(candidate_mask, -float("inf"))
-                        total_forth_loss += self.criterion(logit, targets[i])
-                    if args.pred_back:
-                        back_logit = aux["back_logit"].masked_fill(candidate_mask, -float("inf"))
-                        total_back_loss += self.criterion(back_logit,
-                                                          self._back_teacher_action(s["obs"], s["ended"]))
                     rewards.append(s["reward"])
                     masks.append(s["mask"])
                 plan = nxt
@@ -834,115 +855,41 @@ class Seq2SeqAgent(BaseAgent):
                     if ended.all():
                         break
                     continue
+                mode = self._head_mode()
+                forced_fn = None
+                if mode == "forced":
+                    forced_fn = (lambda leng, t=t: self._to_dev(
+                        np.asarray(self.force_action_fn(t, list(leng)), np.int64)))
+                back = None
                 if self._step_region_ok(consistent_drop, noise):
                     # AdaIN + decoder + one-kernel policy head replayed as one captured training region
-                    mode = self.feedback
-                    forced_fn = None
-                    if mode == "sample" and self.force_action_fn is not None:
-                        mode = "forced"
-                        forced_fn = (lambda leng, t=t: self._to_dev(
-                            np.asarray(self.force_action_fn(t, list(leng)), np.int64)))
                     candidate_leng, ctx, h_t, c_t, logit, h1, ce, ent, lpa, a_dev = self._adain_decode(
                         t, mode, self._step_inputs([perm_obs]), *enc_args, h_t, h1, c_t, ctx_mask, target, forced_fn)
-                    fused, aux_outputs = True, {}
-                    hidden_states.append(h_t)
-                    total_forth_loss += ce
-                    if self.feedback == "argmax":
-                        a_t = a_dev
-                        policy_log_probs.append(lpa.unsqueeze(1))
-                    elif self.feedback == "sample":
-                        deferred["entropy"].append(ent.sum().detach())
-                        entropys.append(ent)
-                        a_t = a_dev
-                        policy_log_probs.append(lpa)
-                    else:
-                        a_t = target
-                    if self.feedback == "teacher":
-                        cpu_a_t = target_np.copy()
-                    else:
-                        cpu_a_t = a_t.cpu().numpy().copy()  # the step's one device->host sync
-                    for i, next_id in enumerate(cpu_a_t):
-                        if next_id == (candidate_leng[i] - 1) or next_id == args.ignoreid:
-                            cpu_a_t[i] = -1
-                    self.make_equiv_action(cpu_a_t, perm_obs, perm_idx, traj)
-                    obs = np.array(self.env._get_obs())
-                    perm_obs = obs[perm_idx]
-                    reward, mask = self._step_reward(perm_obs, cpu_a_t, ended, last_dist)
-                    rewards.append(reward)
-                    masks.append(mask)
-                    ended[:] = np.logical_or(ended, (cpu_a_t == -1))
-                    if ended.all():
-                        break
-                    continue
-                (e,) = self._encode_steps([perm_obs], *enc_args)
-                candidate_leng = e["leng"]
-                ctx = e["ctx"]
-                fused = self._fused_head(e["cand"][:, :, 0])
-                if fused:          # decoder + mask / CE / action / entropy / log-prob in one kernel (policy.hip)
-                    mode, forced = self.feedback, None
-                    if mode == "sample" and self.force_action_fn is not None:
-                        mode = "forced"
-                        forced = self._to_dev(np.asarray(self.force_action_fn(t, list(candidate_leng)), np.int64))
+                else:
+                    (e,) = self._encode_steps([perm_obs], *enc_args)
+                    candidate_leng, ctx = e["leng"], e["ctx"]
+                    self._fused_head(e["cand"][:, :, 0])
                     h0, c0 = (e["en_ht"], e["en_ct"]) if t == 0 else (h_t, c_t)
-                    h_t, c_t, logit, h1, ce, ent, lpa, a_dev = self._decode(
+                    extra = self._visited_mask(perm_obs, visited, e["cand"].shape[1]) if args.submit else None
+                    back_target = self._back_teacher_action(perm_obs, ended) if args.pred_back else None
+                    h_t, c_t, logit, h1, ce, ent, lpa, a_dev, back = self._decode(
                         t, mode, e, h0, h0 if t == 0 else h1, c0, ctx_mask, self._lens_dev(candidate_leng), target,
-                        forced, consistent_drop)
-                    aux_outputs = {}
-                elif t == 0:
-                    h_t, c_t, logit, h1, aux_outputs = self.decoder(e["a"], e["df"], e["cand"], e["en_ht"],
-                                                                    e["en_ht"], e["en_ct"], ctx, ctx_mask,
-                                                                    already_dropfeat=consistent_drop)
-                else:
-                    h_t, c_t, logit, h1, aux_outputs = self.decoder(e["a"], e["df"], e["cand"], h_t, h1, c_t, ctx,
-                                                                    ctx_mask, already_dropfeat=consistent_drop)
+                        forced_fn(candidate_leng) if forced_fn is not None else None, consistent_drop, extra,
+                        back_target)
                 hidden_states.append(h_t)
-                if fused:
-                    total_forth_loss += ce
-                    if self.feedback == "argmax":
-                        a_t = a_dev
-                        policy_log_probs.append(lpa.unsqueeze(1))
-                    elif self.feedback == "sample":
-                        deferred["entropy"].append(ent.sum().detach())
-                        entropys.append(ent)
-                        a_t = a_dev
-                        policy_log_probs.append(lpa)
-                    else:
-                        a_t = target
-                else:
-                    candidate_mask = utils.length2mask(candidate_leng, device=self.device)
-                if not fused and args.submit:
-                    cm = candidate_mask.cpu()
-                    for ob_id, ob in enumerate(perm_obs):
-                        visited[ob_id].add(ob["viewpoint"])
-                        for c_id, c in enumerate(ob["candidate"]):
-                            if c["viewpointId"] in visited[ob_id]:
-                                cm[ob_id][c_id] = 1
-                    candidate_mask = cm.to(self.device)
-                if not fused:
-                    logit = logit.masked_fill(candidate_mask, -float("inf"))
-                    forth_loss = self.criterion(logit, target)
-                    total_forth_loss += forth_loss
-                if args.pred_back:
-                    back_logit = aux_outputs["back_logit"].masked_fill(candidate_mask, -float("inf"))
-                    total_back_loss += self.criterion(back_logit, self._back_teacher_action(perm_obs, ended))
-                if fused:
-                    pass
-                elif self.feedback == "teacher":
-                    a_t = target
-                elif self.feedback == "argmax":
-                    _, a_t = logit.max(1)
-                    a_t = a_t.detach()
-                    policy_log_probs.append(F.log_softmax(logit, 1).gather(1, a_t.unsqueeze(1)))
+                total_forth_loss += ce          # mask + CE + action + entropy / log-prob: one kernel (policy.hip)
+                if back is not None:
+                    total_back_loss += back
+                if self.feedback == "argmax":
+                    a_t = a_dev
+                    policy_log_probs.append(lpa.unsqueeze(1))
                 elif self.feedback == "sample":
-                    probs = F.softmax(logit, 1)
-                    c = torch.distributions.Categorical(probs, validate_args=False)   # (validation = a host sync)
-                    ent = c.entropy()
                     deferred["entropy"].append(ent.sum().detach())
                     entropys.append(ent)
-                    a_t = (self.sample_fn(probs) if self.sample_fn is not None else c.sample()).detach()
-                    policy_log_probs.append(c.log_prob(a_t))
+                    a_t = a_dev
+                    policy_log_probs.append(lpa)
                 else:
-                    sys.exit("Invalid feedback option")
+                    a_t = target
                 if self.feedback == "teacher":
                     cpu_a_t = target_np.copy()           # a_t is target: its host copy, no device round trip
                 else:
@@ -962,11 +909,8 @@ class Seq2SeqAgent(BaseAgent):
 
         if train_rl:
             input_a_t, f_t, d_t, candidate_feat, candidate_dfeat, candidate_leng = self.get_input_feat(perm_obs)
-            # host-side inputs of the step's loss/action stage, copied up front without a sync (the
-            # reference builds them after the decoder with blocking copies; same values)
-            target_np = self._teacher_action_np(perm_obs, ended)
-            target = self._to_dev(target_np)
-            candidate_mask = utils.length2mask(candidate_leng, device=self.device)
+            # (the reference also builds this step's teacher target and candidate mask, agent_dg.py:945-950;
+            # nothing reads them)
             if speaker is not None:
                 candidate_feat = self._noise_mult(candidate_feat, noise)
                 f_t = self._noise_mult(f_t, noise)

@@ -32,14 +32,8 @@ class SoftDotAttention(nn.Module):
             q = ops.linear(h.detach(), self.linear_in.weight.detach())
             wctx = ops.softdot_fwd(q, context.detach(), None)[2]     # unused by the decoder (model.py:559)
             return wctx, logit
-        # general combination (not on the README path)
-        q = DF.linear(h, self.linear_in.weight)
-        scores = torch.einsum("bnd,bd->bn", context, q)
-        if mask is not None:
-            scores = scores.masked_fill(mask.bool(), -float("inf"))
-        p = torch.softmax(scores, 1)
-        wctx = torch.einsum("bn,bnd->bd", p, context)
-        attn = p if output_prob else scores
+        # the other combinations (no README caller) on the same kernels: dasa_softdot_fwd / _bwd
+        wctx, attn = DF.SoftDotFn.apply(h, context, mask, self.linear_in.weight, not output_prob)
         if output_tilde:
             return DF.linear(torch.cat((wctx, h), 1), self.linear_out.weight, None, "tanh"), attn
         return wctx, attn
@@ -70,8 +64,9 @@ class ShiftSoftDotAttention(nn.Module):
             raise ValueError("ShiftSoftDotAttention expects the 36-view panorama (3 x 12)")
         wctx, attn = DF.ShiftAttnFn.apply(h, context.contiguous(), self.linear_in.weight, self.linear_shift.weight,
                                           self.linear_shift.bias)
-        if not output_prob:
-            attn = torch.einsum("bnd,bd->bn", context, ops.linear(h.detach(), self.linear_in.weight.detach()))
+        if not output_prob:   # the raw scores (model.py:346-347), detached: no caller differentiates them
+            q = ops.linear(h.detach(), self.linear_in.weight.detach())
+            attn = ops.softdot_fwd(q, context.detach(), None, want_probs=False, want_wctx=False)[0]
         if output_tilde:
             return DF.linear(torch.cat((wctx, h), 1), self.linear_out.weight, None, "tanh"), attn
         return wctx, attn

@@ -267,7 +267,7 @@ int dasa_reverse_valid(const float* x, const int32_t* lengths, float* out, int32
                        int32_t H, void* stream);
 /* ---- policy head (agent_dg.py:832-886) ------------------------------------------------------- */
 enum dasa_policy_mode { DASA_POLICY_TEACHER = 0, DASA_POLICY_ARGMAX = 1, DASA_POLICY_SAMPLE = 2,
-                        DASA_POLICY_FORCED = 3 };
+                        DASA_POLICY_FORCED = 3, DASA_POLICY_SAMPLE_ARGMAX = 4 };
 /* One decision step's loss/action stage on logit [B][C] (row stride ld): candidates c >= cand_len[b]
  * are masked (-inf); logp [B][C] = masked log-softmax (saved for backward); ce_sum[0] = sum over rows
  * with target != ignore_index of -logp[target] (CrossEntropyLoss(reduction='sum')); mode ARGMAX:
@@ -276,7 +276,9 @@ enum dasa_policy_mode { DASA_POLICY_TEACHER = 0, DASA_POLICY_ARGMAX = 1, DASA_PO
  * CE, ce_sum = 0). C <= 256. ws: B floats of scratch. One launch, deterministic.
  * Mode FORCED is mode SAMPLE with the draw replaced by the caller's action[b] (an INPUT, 0 <= action[b]
  * < cand_len[b]): entropy and logp_a as in SAMPLE. It pins the sampled rollout's loss stage against a
- * reference run whose Categorical.sample returns the same actions (tests/test_policy_gpu.py). */
+ * reference run whose Categorical.sample returns the same actions (tests/test_policy_gpu.py).
+ * Mode SAMPLE_ARGMAX is mode SAMPLE with the draw replaced by the first argmax (a reference run whose
+ * Categorical.sample is replaced by probs.argmax: the golden fixtures' sampled rollouts). */
 int dasa_policy_head_fwd(const float* logit, int64_t ld, const int32_t* cand_len, const int64_t* target,
                          int32_t B, int32_t C, int32_t mode, int32_t ignore_index, uint64_t seed,
                          float* logp, float* ce_sum, float* ent, float* logp_a, int64_t* action,
@@ -296,8 +298,11 @@ int dasa_policy_head_bwd(const float* logp, const int32_t* cand_len, const int64
 /* Device seed source for hipGraph capture. While a counter is set (dev_counter != NULL), every
  * forward dropout launch (layernorm, embeddings, attention probabilities, dropout) records it, and
  * its mask seed becomes seed ^ mix(*dev_counter) read at run time: a captured graph that starts with
- * dasa_seed_bump(dev_counter) draws fresh masks on every replay. Host-only setting, not thread-safe;
- * set it only around capture of forward-only (no-grad) work (backward kernels use plain seeds). */
+ * dasa_seed_bump(dev_counter) draws fresh masks on every replay; the Categorical draw of the policy
+ * head (mode SAMPLE) is keyed the same way. Backward dropout kernels (dropout, layernorm, attention
+ * probabilities) launched while the same counter is set regenerate the replay's masks: a captured
+ * TRAINING step runs its eager backward with its counter set (dasa_amd/graph.py AutogradGraphs).
+ * Host-only setting, not thread-safe. */
 int dasa_set_seed_source(const uint64_t* dev_counter);
 int dasa_seed_bump(uint64_t* dev_counter, void* stream);
 

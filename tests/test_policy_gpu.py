@@ -262,7 +262,7 @@ def test_train_iteration_grads(R, dev, deferred):
             if isinstance(sub, torch.nn.Dropout):
                 sub.p = 0.0
     param.args.ml_weight = param.args.ml_weight_org
-    ag.sample_fn = lambda p: p.argmax(-1)
+    ag.sample_fn = "argmax"
     ag.zero_grad()
     ag.accumulate_gradient("sample")
     assert abs(ag.loss.item() - float(G["train/loss"])) < TOL * max(1.0, abs(float(G["train/loss"])))
@@ -302,7 +302,7 @@ def test_hoist_language_train(R, dev):
                 for sub in m.modules():
                     if isinstance(sub, torch.nn.Dropout):
                         sub.p = 0.0
-        ag.sample_fn = lambda p: p.argmax(-1)
+        ag.sample_fn = "argmax"
         return ag
     param.args.ml_weight = param.args.ml_weight_org
     param.args.hoist_language = True
@@ -355,7 +355,7 @@ def test_finetune_train_iteration_grads(R, dev, monkeypatch, deferred):
             if isinstance(sub, torch.nn.Dropout):
                 sub.p = 0.0
     monkeypatch.setattr(param.args, "ml_weight", param.args.ml_weight_org)
-    ag.sample_fn = lambda p: p.argmax(-1)
+    ag.sample_fn = "argmax"
     ag.zero_grad()
     ag.accumulate_gradient("sample")
     assert abs(ag.loss.item() - float(G["ft/loss"])) < TOL * max(1.0, abs(float(G["ft/loss"])))
@@ -650,7 +650,7 @@ def test_cfg2_train_iteration_grads(R, dev, cfg2_args, deferred):
             if isinstance(sub, torch.nn.Dropout):
                 sub.p = 0.0
     param.args.ml_weight = param.args.ml_weight_org
-    ag.sample_fn = lambda p: p.argmax(-1)
+    ag.sample_fn = "argmax"
     ag.zero_grad()
     ag.accumulate_gradient("sample")
     ref = float(G["train/loss"])
