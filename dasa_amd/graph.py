@@ -127,7 +127,7 @@ class StepGraphs:
 
 # ------------------------------------------------------------------ training-mode (autograd) regions
 class _Slot:
-    __slots__ = ("graph", "static_in", "static_out", "counter", "pkey")
+    __slots__ = ("graph", "static_in", "static_out", "counter", "pkey", "fills", "shapes")
 
 
 def _lead(t, shape):
@@ -149,9 +149,15 @@ class _BridgeFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, slot, *inputs):
         with torch.no_grad():
-            for s, x in zip(slot.static_in, inputs):
-                if s is not None:
-                    _lead(s.data, x.shape).copy_(x)
+            for i, (s, x) in enumerate(zip(slot.static_in, inputs)):
+                if s is None:
+                    continue
+                if i in slot.fills and slot.shapes[i] != tuple(x.shape):
+                    # another extent than the last input of this padded slot: rows a larger one wrote
+                    # past the new extent go back to the padding value (e.g. True in a padded mask)
+                    s.data.fill_(slot.fills[i])
+                    slot.shapes[i] = tuple(x.shape)
+                _lead(s.data, x.shape).copy_(x)
         slot.graph.replay()
         ctx.slot = slot
         ctx.shapes = [x.shape if x is not None else None for x in inputs]
@@ -225,6 +231,7 @@ class AutogradGraphs:
             self.pool = torch.cuda.graph_pool_handle()
         slot = _Slot()
         slot.counter = torch.zeros(1, dtype=torch.int64, device=dev)
+        slot.fills, slot.shapes = {}, {}
         static_in = []
         for i, x in enumerate(inputs):
             if x is None:
@@ -232,6 +239,8 @@ class AutogradGraphs:
                 continue
             shape, fill = pads.get(i, (x.shape, 0))
             s = torch.full(shape, fill, dtype=x.dtype, device=dev)    # the padding keeps its fill value
+            if i in pads:
+                slot.fills[i], slot.shapes[i] = fill, tuple(x.shape)
             with torch.no_grad():       # a LEAF: recorded, the copy would link the slot to x's graph
                 _lead(s, x.shape).copy_(x)
             static_in.append(s.requires_grad_(x.requires_grad))

@@ -594,8 +594,8 @@ class Seq2SeqAgent(BaseAgent):
                 back_target=None):
         """agent_dg.py:811-886 for one step: BAttnDecoderLSTM + the one-kernel policy head (mask, CE,
         action, entropy / log-prob). Training steps replay a captured graph keyed by the step index;
-        the candidate block is zero-padded to a multiple of 8 (>= 16) and the instruction context to a
-        multiple of 16 tokens with the padding masked: the head masks padded candidates and the
+        the candidate block is zero-padded and the instruction context padded to --maxInput tokens with
+        the padding masked (_slot_pads): the head masks padded candidates and the
         instruction attention gives masked tokens weight 0, so every valid logit, loss and gradient is
         unchanged while few shapes (slots) arise. Otherwise eager, with --submit's extra mask and the
         --pred_back CE (a second teacher-mode head call on the back logits, agent_dg.py:872-876).
@@ -624,11 +624,24 @@ class Seq2SeqAgent(BaseAgent):
             self._train_graphs = graph.AutogradGraphs([self.decoder])
         B, C, F = e["cand"].shape
         L, H2 = e["ctx"].shape[1:]
-        Cp, Lp = max(16, -(-C // 8) * 8), -(-L // 16) * 16
+        Cp, Lp = self._slot_pads(C, L)
         key = ("dec", mode, t, B, Cp, Lp, H2, bool(dropfeat))
         out = self._train_graphs.run(key, step, inputs, pads={2: ((B, Cp, F), 0), 6: ((B, Lp, H2), 0),
                                                               7: ((B, Lp), True)})
         return out[:2] + (out[2][:, :C],) + out[3:] + (None,)
+
+    @staticmethod
+    def _slot_pads(C, L):
+        """Padded candidate / instruction extents of a captured training step: candidates to 16, 32, 64, ...
+        and the instruction context to the longest instruction the encoder admits (--maxInput, rounded
+        up to 16), so a slot serves every batch of its step index — at small B the batch's longest
+        instruction and candidate count vary from batch to batch, and per-extent slots would re-capture
+        for most steps. Padded tokens are masked, padded candidates lie past every row's length."""
+        Cp = 16
+        while Cp < C:
+            Cp *= 2
+        Lp = -(-max(L, args.maxInput) // 16) * 16
+        return Cp, Lp
 
     def _step_region_ok(self, consistent_drop, noise):
         """The per-step loop's AdaIN joins the captured decoder region (_adain_decode) in the README
@@ -669,7 +682,7 @@ class Seq2SeqAgent(BaseAgent):
             self._train_graphs = graph.AutogradGraphs([self.decoder, self.adaIn])
         F = cf3.shape[2]
         L, H2 = ctx.shape[1:]
-        Cp, Lp = max(16, -(-C // 8) * 8), -(-L // 16) * 16
+        Cp, Lp = self._slot_pads(C, L)
         key = ("step", mode, t, B, Cp, Lp, H2, bool(consistent_drop), bool(use_noise))
         out = self._train_graphs.run(key, step, step_in, pads={3: ((B, Cp, F), 0), 4: ((B, Cp, F), 0),
                                                                9: ((B, Lp, H2), 0), 10: ((B, Lp), True)})

@@ -439,6 +439,13 @@ class SynthR2RBatch:
         h = (item["wander_seed"] * 1000003 + sim.vp * 9176 + sim.step * 7919) % (1 << 31)
         return w.ids[nb[h % len(nb)][0]]
 
+    def _back_teacher(self, sim, item):
+        """env.py:348: the next viewpoint on the shortest path back to the episode start (the current one
+        once there; also when the start is unreachable on the directed synthetic graph)."""
+        w = self.world
+        hop = int(w.next_hop[sim.vp, w.index[item["path"][0]]])
+        return w.ids[hop if hop >= 0 else sim.vp]
+
     def _distance(self, sim, item):
         w = self.world
         if self.mode == "goal":
@@ -478,7 +485,7 @@ class SynthR2RBatch:
                 "navigableLocations": self._nav_locs(v),
                 "instructions": item["instructions"],
                 "teacher": self._teacher(sim, item),
-                "back_teacher": item["path"][0],
+                "back_teacher": self._back_teacher(sim, item),
                 "path_id": item["path_id"],
                 "instr_encoding": item["instr_encoding"],
                 "distance": self._distance(sim, item),
