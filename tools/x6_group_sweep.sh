@@ -5,9 +5,9 @@ set -o pipefail
 OUT=gpurun_out/x6group
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-for S in ${SHAPES:-"12800,3072,768 12800,2304,768 12800,768,3072"}; do
+for S in ${SHAPES:-12800,3072,768 12800,2304,768 12800,768,3072}; do
   IFS=, read M N K <<< "$S"
-  for G in ${X6_GROUP_LIST:-"4 8 16 1 -2 -4 -8"}; do
+  for G in ${X6_GROUP_LIST:-4 8 16 1 -2 -4 -8}; do
     DASA_X6_GROUP=$G timeout -k 10 60 python tools/x6_one.py $M $N $K 20 > $OUT/t_${M}_${N}_${K}_g$G.txt 2>&1 || exit 1
     DASA_X6_GROUP=$G timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "f32x6" --output-format csv -d $OUT/p_${M}_${N}_${K}_g$G -o run -- python3 tools/x6_one.py $M $N $K 10 > $OUT/r_${M}_${N}_${K}_g$G.log 2>&1
     rc=$?; [ $rc -ne 0 ] && { echo "pmc $S g$G rc=$rc"; exit $rc; }
