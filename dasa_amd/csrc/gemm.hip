@@ -2405,7 +2405,9 @@ extern "C" int dasa_gemm_f32x6_ws(const dasa_gemm_desc* d, int64_t plane, void* 
   X6Plan pl = x6_plan(d);
   if (pl.splitk > 1 && (ws == nullptr || ws_bytes < pl.ws)) { pl.splitk = 1; pl.kchunk = K; }
   const int cfg = pl.cfg, bm = pl.bm, bn = pl.bn;
-  p.group_m = cdiv(M, bm) >= 8 ? 4 : 1;
+  // tile order: groups of 8 W column panels, A streaming under them (r04 sweep, profiles/r04/x6_group_sweep.txt:
+  // 12800 x {3072, 2304} x 768 fetch 460 -> 332 MB / 367 -> 274 MB per launch, time within +-1 %)
+  p.group_m = cdiv(M, bm) >= 8 ? -8 : 1;
   if (x6_group_override() != 0) p.group_m = x6_group_override();   // A/B: DASA_X6_GROUP (< -1: along N)
   X6Split xs{};
   hipStream_t st = (hipStream_t)stream;
