@@ -768,8 +768,8 @@ __global__ __launch_bounds__(256) void attn_split_bwd_kernel(SplitArgs a) {
 //             also writes scores / probs / shifted / the tap weights.
 // Measured (profiles/r03/attn_forms_b.txt, B = 20): shift attention 8.55 us vs 8.89 for the row-split
 // kernel's in-launch merge, so the shift forward takes it; the instruction SoftDot (N = 80) ran 12.1 vs
-// 10.8 us and keeps the row-split kernel (reachable in attention mode 2, where the tests run it with
-// masks, strided rows and N up to 80).
+// 10.8 us on it, and r04 moved it here as well (dasa_softdot_fwd: the row-split kernel is not reproducible
+// beside bf16x6 form-20 GEMMs on another stream).
 template <int RPT>
 __global__ __launch_bounds__(256) void attn_split_dots_kernel(SplitArgs a) {
   const int g = blockIdx.x, b = blockIdx.y, t = threadIdx.x, col = t & 31, rl = t >> 5;
@@ -1061,7 +1061,11 @@ extern "C" int dasa_softdot_fwd(const float* q, const float* ctx, int64_t ldn, c
     DASA_CHECK_LAUNCH();
     return 0;
   }
-  if (g_attn_mode == 2 && split2_ok(B, N, D)) return launch_split2_fwd(a, B, ws, (hipStream_t)stream);
+  // B < 128: the two-launch D-split form. The row-split kernel (attn_fwd_kernel, 1.2 us faster per call)
+  // returned wrong row dots in 10-50 % of calls while bf16x6 form-20 GEMMs ran on another stream
+  // (tools/determinism_stress.py, profiles/r04/attn_rowsplit_concurrency.txt); every other kernel of the
+  // step, the D-split forms included, stayed bitwise reproducible under the same load.
+  if (split2_ok(B, N, D)) return launch_split2_fwd(a, B, ws, (hipStream_t)stream);
   return launch_fwd<16>(a, B, ws, (hipStream_t)stream);
 }
 

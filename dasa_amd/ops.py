@@ -581,8 +581,8 @@ _AWS = {}
 
 
 def attn_set_mode(mode):
-    """Attention implementation (include/dasa_hip.h dasa_attn_set_mode): 0 automatic, 1 row-split only,
-    2 automatic + the two-launch D-split SoftDot forward (tests)."""
+    """Attention implementation (include/dasa_hip.h dasa_attn_set_mode): 0 automatic (B < 128: the
+    two-launch D-split forms), 1 row-split only (tests), 2 = 0."""
     _lib.check(_lib.lib().dasa_attn_set_mode(int(mode)), "dasa_attn_set_mode")
 
 

@@ -145,9 +145,10 @@ int dasa_mha_bwd(const float* Q, int64_t ldq, const float* K, int64_t ldk, const
  * meet at a bounded group barrier; a timeout NaN-poisons the outputs and ORs 4 into the error word,
  * dasa_set_error_word); shift-attention forward with B < 128, and the candidate scores (no probs /
  * wctx) with B < 128: two-launch D-split (row-dot partials, then softmax + context per column chunk)
- * and one workgroup per row. dasa_attn_set_mode: 0 = automatic (the default; DASA_ATTN_SPLIT=0 in
- * the environment starts in mode 1), 1 = row-split only, 2 = automatic plus the two-launch D-split
- * forward for SoftDot with probs / wctx as well (tests). Host-only setting.                         */
+ * and one workgroup per row; SoftDot with probs / wctx at B < 128 (N <= 80, D % 128 == 0) on the same
+ * two-launch form (r04). dasa_attn_set_mode: 0 = automatic (the default; DASA_ATTN_SPLIT=0 in the
+ * environment starts in mode 1), 1 = row-split only, 2 = the same as 0 (kept for callers of r03).
+ * Host-only setting.                                                                                 */
 int64_t dasa_attn_workspace(int32_t B, int32_t N, int32_t D);
 int dasa_attn_set_mode(int32_t mode);
 int dasa_softdot_fwd(const float* q, const float* ctx, int64_t ldn, const uint8_t* mask,

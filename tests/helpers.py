@@ -112,5 +112,10 @@ def close(a, b, tol, what=""):
     b = torch.as_tensor(b).double().cpu()
     assert a.shape == b.shape, (what, a.shape, b.shape)
     err = (a - b).abs().max().item() if a.numel() else 0.0
-    assert err <= tol, f"{what}: max|diff| {err:.3e} > {tol:.1e}"
+    if err > tol:
+        d = (a - b).abs()
+        idx = tuple(int(i) for i in torch.nonzero(d == d.max())[0])
+        bad = int((d > tol).sum())
+        raise AssertionError(f"{what}: max|diff| {err:.3e} > {tol:.1e} at {idx} (got {a[idx].item():.6g}, want "
+                             f"{b[idx].item():.6g}; {bad} of {a.numel()} elements off)")
     return err

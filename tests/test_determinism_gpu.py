@@ -1,0 +1,41 @@
+"""Bitwise run-to-run reproducibility of the step's kernels with in-launch hand-offs (split-K and
+last-arriver merges, group barriers) while a bf16x6 GEMM runs on another stream — the training
+iteration's shape of concurrency (the language pipe's 12800-row GEMMs beside the decoder step).
+r04 found the row-split SoftDot kernel wrong in 10-50 % of calls under that load
+(profiles/r04/attn_rowsplit_concurrency.txt); the default path must stay reproducible."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _cases(dev):
+    from tools.determinism_stress import cases
+    g = torch.Generator(device=dev).manual_seed(0)
+    return [c for c in cases(dev, g) if not c[0].startswith("bilstm")]
+
+
+def test_handoff_kernels_reproducible_beside_x6_gemm(dev):
+    from dasa_amd import ops
+    bg = torch.cuda.Stream()
+    A, W = torch.randn(12800, 768, device=dev), torch.randn(3072, 768, device=dev) * 0.02
+    y = torch.empty(12800, 3072, device=dev)
+    bad = {}
+    for name, xs, fn in _cases(dev):
+        refs = [fn(x).clone() for x in xs]
+        torch.cuda.synchronize()
+        cnt = torch.zeros((), dtype=torch.int32, device=dev)
+        iters = 120 if name.startswith("softdot") else 24
+        for i in range(iters):
+            if i % 4 == 0:
+                bg.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(bg):
+                    ops.linear(A, W, out=y)
+            out = fn(xs[i & 1])
+            cnt += (~torch.eq(out, refs[i & 1])).any().int()
+        torch.cuda.current_stream().wait_stream(bg)
+        torch.cuda.synchronize()
+        if int(cnt):
+            bad[name] = int(cnt)
+    ops.check_device_errors()
+    assert not bad, bad
