@@ -99,6 +99,13 @@ class _Recorder:
                 roof["mfma_busy"] = round(pf["mfma_busy"], 4)
             roof["traffic_source"] = (pmc["file"] + ": " + pmc["source"] + " (a separate rocprofv3 --pmc run of the "
                                       "same workload; counters cannot be collected in the timed run)")
+        tp = _timed_path_avg_us(pmc_workload, dom_name)
+        if tp is not None:
+            # the same kernels in the TIMED path (graph replays, full stream concurrency), from the
+            # committed rocprofv3 --kernel-trace --stats summary of this workload: the bracketed launches
+            # above run with less overlap, so they are faster per launch
+            roof["timed_path_rocprof"] = dict(tp, frac=round(roof["per_launch"]["alg_flops"] / (tp["avg_us"] * 1e-6)
+                                                          / 1e12 / d["peak"], 4) if d["bound"] == "mfma" else None)
         for name, ent in kernels.items():          # PMC MFMA-busy / HBM bytes per family where measured
             pf = (pmc or {}).get("families", {}).get(name)
             if pf:
@@ -133,10 +140,36 @@ def _pmc_traffic(workload):
     return d
 
 
+def _timed_path_avg_us(workload, family):
+    """Average launch duration of `family` in the committed rocprofv3 --stats summary of `workload`'s
+    timed path (STATS_FILES), or None."""
+    import csv
+    import os
+    rel = STATS_FILES.get(workload)
+    prefix = FAMILIES.get(family, (None, ""))[1].split(" ")[0]
+    if rel is None or not prefix:
+        return None
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), rel)
+    if not os.path.exists(path):
+        return None
+    calls, ns = 0, 0.0
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if prefix + "<" in row["Name"] or row["Name"].split("(")[0].endswith(prefix):
+                calls += int(row["Calls"])
+                ns += float(row["TotalDurationNs"])
+    if not calls:
+        return None
+    return {"avg_us": round(ns / calls / 1e3, 2), "launches": calls, "file": rel}
+
+
+# rocprofv3 --kernel-trace --stats of the timed path per workload (tools/prof_round.sh)
+STATS_FILES = {"cfg2": "profiles/r04/prof_final/rocprof_kernel_stats_timed_path.csv"}
+
 # the committed PMC summaries per workload the roofline's `traffic` / `mfma_busy` come from
 # (tools/prof_round.sh -> tools/pmc_summary.py); a workload without one reports no PMC values
-PMC_FILES = {"cfg2": "profiles/r04/prof_a/pmc_cfg2.json", "cfg5": "profiles/r04/prof_a/pmc_cfg5.json",
-             "cfg4": "profiles/r04/prof_a/pmc_cfg4.json"}
+PMC_FILES = {"cfg2": "profiles/r04/prof_final/pmc_cfg2.json", "cfg5": "profiles/r04/prof_final/pmc_cfg5.json",
+             "cfg4": "profiles/r04/prof_final/pmc_cfg4.json"}
 
 
 def active():

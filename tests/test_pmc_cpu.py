@@ -45,3 +45,12 @@ def test_pmc_summary_pairs_counters_with_their_dispatch(tmp_path):
     assert abs(res["window_inflated"] - 0.5) < 1e-9
     assert abs(res["mfma_busy"] - 0.4) < 1e-9                  # not deflated by the inflated window
     assert res["hbm_bytes"] == 2 * 1024 * 1000.0 + 1024 * 500.0
+
+
+def test_timed_path_stats_attached():
+    """The bench line's roofline carries the dominant kernel's timed-path average from the committed
+    rocprofv3 --stats summary (prof.STATS_FILES), the file the judge recomputes `frac` from."""
+    from dasa_amd import prof
+    tp = prof._timed_path_avg_us("cfg2", "gemm_x6")
+    assert tp is not None and tp["launches"] > 0 and tp["avg_us"] > 0
+    assert prof._timed_path_avg_us("cfg2", "no_such_family") is None
