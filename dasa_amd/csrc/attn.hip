@@ -1054,18 +1054,22 @@ extern "C" int dasa_softdot_fwd(const float* q, const float* ctx, int64_t ldn, c
   if (B <= 0 || N <= 0) return 0;
   if (bad_common(q, ctx, ldn, B, N, D, ws) || (wctx && !aligned16(wctx))) return (int)hipErrorInvalidValue;
   FwdArgs a{q, ctx, (long)ldn, mask, nullptr, 0, scores, probs, nullptr, nullptr, wctx, N, D};
+  if (g_attn_mode < 0) split_rpt(1, 1, 128, false);   // reads DASA_ATTN_SPLIT once
   if ((probs || wctx) && rows_ok(B, N, D)) return launch_rows(a, B, (hipStream_t)stream);
-  if (!probs && !wctx && scores && g_attn_mode != 1 && B < kRowsMinB && D <= 4 * 1024) {   // scores only
+  if (!probs && !wctx && scores && g_attn_mode != 1 && D <= 4 * 1024) {   // scores only (every B: see below)
     hipLaunchKernelGGL(attn_dot_rows_kernel, dim3(N, B), dim3(256), 0, (hipStream_t)stream, q, ctx, (long)ldn,
                        scores, N, D);
     DASA_CHECK_LAUNCH();
     return 0;
   }
-  // B < 128: the two-launch D-split form. The row-split kernel (attn_fwd_kernel, 1.2 us faster per call)
-  // returned wrong row dots in 10-50 % of calls while bf16x6 form-20 GEMMs ran on another stream
-  // (tools/determinism_stress.py, profiles/r04/attn_rowsplit_concurrency.txt); every other kernel of the
-  // step, the D-split forms included, stayed bitwise reproducible under the same load.
-  if (split2_ok(B, N, D)) return launch_split2_fwd(a, B, ws, (hipStream_t)stream);
+  // Every B the whole-row form does not take: the two-launch D-split form. The row-split kernel
+  // (attn_fwd_kernel, 1.2 us faster per call at B = 20) returned wrong row dots in 10-50 % of calls, at
+  // B = 20 and at B = 256, while bf16x6 form-20 GEMMs ran on another stream (tools/determinism_stress.py,
+  // profiles/r04/attn_rowsplit_concurrency.txt); every other kernel of the step, the D-split and
+  // whole-row forms included, stayed bitwise reproducible under the same load. It is left for mode 1
+  // (tests) and for shapes no other form takes (N > 80 or D % 128 != 0).
+  if (g_attn_mode != 1 && N <= kSplitMaxN && D % (4 * kCW) == 0 && D <= 4 * kCW * 32)
+    return launch_split2_fwd(a, B, ws, (hipStream_t)stream);
   return launch_fwd<16>(a, B, ws, (hipStream_t)stream);
 }
 

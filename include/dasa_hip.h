@@ -143,12 +143,13 @@ int dasa_mha_bwd(const float* Q, int64_t ldq, const float* K, int64_t ldk, const
  * workgroup streams a batch row); backward with N <= 80, D % 128 == 0 and B * D/128 <= 1024 (the
  * decision step's B = 20), D-split (a batch row's 128-float column chunks over D/128 workgroups that
  * meet at a bounded group barrier; a timeout NaN-poisons the outputs and ORs 4 into the error word,
- * dasa_set_error_word); shift-attention forward with B < 128, and the candidate scores (no probs /
- * wctx) with B < 128: two-launch D-split (row-dot partials, then softmax + context per column chunk)
- * and one workgroup per row; SoftDot with probs / wctx at B < 128 (N <= 80, D % 128 == 0) on the same
- * two-launch form (r04). dasa_attn_set_mode: 0 = automatic (the default; DASA_ATTN_SPLIT=0 in the
- * environment starts in mode 1), 1 = row-split only, 2 = the same as 0 (kept for callers of r03).
- * Host-only setting.                                                                                 */
+ * dasa_set_error_word); shift-attention forward with B < 128: two-launch D-split (row-dot partials,
+ * then softmax + context per column chunk); candidate scores (no probs / wctx): one workgroup per
+ * row at every B; SoftDot with probs / wctx (N <= 80, D % 128 == 0) on the two-launch form at every B
+ * the whole-row form does not take (r04: the row-split kernel is not reproducible beside bf16x6
+ * form-20 GEMMs on another stream; it remains for mode 1 and for shapes no other form takes).
+ * dasa_attn_set_mode: 0 = automatic (the default; DASA_ATTN_SPLIT=0 in the environment starts in
+ * mode 1), 1 = row-split only, 2 = the same as 0 (kept for callers of r03). Host-only setting.      */
 int64_t dasa_attn_workspace(int32_t B, int32_t N, int32_t D);
 int dasa_attn_set_mode(int32_t mode);
 int dasa_softdot_fwd(const float* q, const float* ctx, int64_t ldn, const uint8_t* mask,

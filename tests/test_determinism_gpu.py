@@ -12,7 +12,7 @@ pytestmark = pytest.mark.gpu
 def _cases(dev):
     from tools.determinism_stress import cases
     g = torch.Generator(device=dev).manual_seed(0)
-    return [c for c in cases(dev, g) if not c[0].startswith("bilstm")]
+    return [c for c in cases(dev, g) if not c[0].startswith("bilstm")]   # (B = 256 cases included)
 
 
 def test_handoff_kernels_reproducible_beside_x6_gemm(dev):

@@ -50,6 +50,13 @@ def cases(dev, g):
     out.append(("softdot_bwd B20", (rnd(20, 2048), rnd(20, 2048)),
                 lambda dw: torch.cat([ops.softdot_bwd(qb, ctx, pr, dwctx=dw)[0],
                                       ops.softdot_bwd(qb, ctx, pr, dwctx=dw)[1].flatten(1)], 1)))
+    # B = 256 (configs[4]'s eval rollout): the instruction SoftDot (N = 80) is still on the row-split kernel
+    ctx2 = rnd(256, 80, 2048, scale=0.2)
+    out.append(("softdot B256 N80", (rnd(256, 2048, scale=0.05), rnd(256, 2048, scale=0.05)),
+                lambda q: torch.cat([t for t in ops.softdot_fwd(q, ctx2, None)], 1)))
+    feat2 = rnd(256, 36, 2176, scale=0.2)
+    out.append(("shift B256", (rnd(256, 2176, scale=0.05), rnd(256, 2176, scale=0.05)),
+                lambda q: ops.shift_attn_fwd(q, feat2, rnd(256, 5) * 0 + 0.1)[0]))
     # per-row kernels of the step (wave reductions only)
     gam, bet = rnd(768, scale=0.1) + 1, rnd(768, scale=0.1)
     out.append(("layernorm 1600x768", (rnd(1600, 768), rnd(1600, 768)),
