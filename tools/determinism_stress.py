@@ -85,6 +85,8 @@ def main():
     iters = int(sys.argv[1]) if len(sys.argv) > 1 else 200
     only = sys.argv[2] if len(sys.argv) > 2 else None          # substring of the case names to run
     bgk = sys.argv[3] if len(sys.argv) > 3 else "x6"   # side-stream load: x6 | f32 | ew | nobg
+    phase = int(sys.argv[4]) if len(sys.argv) > 4 else 0   # the side GEMM is launched before calls i % period == phase
+    period = int(sys.argv[5]) if len(sys.argv) > 5 else 4
     use_bg = bgk != "nobg"
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
@@ -101,7 +103,7 @@ def main():
         bad = torch.zeros(2, dtype=torch.int32, device=dev)
         shown = 0
         for i in range(iters):
-            if use_bg and i % 4 == 0 and not name.startswith("bilstm"):   # (the persistent kernel needs the whole chip)
+            if use_bg and i % period == phase and not name.startswith("bilstm"):   # (the persistent kernel needs the whole chip)
                 bg.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(bg):
                     if bgk == "x6":
