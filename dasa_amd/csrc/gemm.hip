@@ -1154,11 +1154,7 @@ struct X6Split { unsigned* cnt; float* slab; int splitk, kchunk; };
 // at most 128 registers (waves_per_eu 4): two workgroups share a CU and overlap each other's split / LDS
 // phase with their MFMAs — form 8's products in form 8's order (bitwise equal), 1.07-1.14x the previous
 // plan on the many-tile K = 768, N >= 2048 shapes (profiles/r03/x6_lds1_forms.txt).
-// APRE (sweep forms 22 / 23, r04 probe): A arrives pre-split too — p.A points at bf16 planes [3][M][lda]
-// (dasa_f32_split3_bf16 of A) and is staged exactly like W: no split VALU in the stage phase, 1.5x the
-// A bytes. Bitwise the same products as the in-kernel split.
-template <int BM, int BN, int WAVES_M, int WAVES_N, bool SEP, int PF = 1, bool SPL = false, int PRIO = 0,
-          bool APRE = false>
+template <int BM, int BN, int WAVES_M, int WAVES_N, bool SEP, int PF = 1, bool SPL = false, int PRIO = 0>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N)
 __attribute__((amdgpu_waves_per_eu(PF < 0 ? 4 : 1, PF < 0 ? 4 : 2)))
 void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
@@ -1193,8 +1189,6 @@ void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
   const int kb = SPL ? split * xs.kchunk : 0;
   const float* A = p.A + (long)b * p.sA + kb;
   const unsigned short* W = reinterpret_cast<const unsigned short*>(p.B) + (long)b * p.sB + kb;
-  const unsigned short* Ab = reinterpret_cast<const unsigned short*>(p.A) + (long)b * p.sA + kb;   // APRE
-  const long aplane = (long)p.M * p.lda;
 
   floatx4 big[TM][TN], small[SEP ? TM : 1][SEP ? TN : 1];
 #pragma unroll
@@ -1211,29 +1205,21 @@ void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
   // unit u -> (row, quad): 8 consecutive lanes take 8 consecutive rows of one quad (coalesced 128-B
   // row segments per 4 x 8 lanes on the global side, conflict-free ds_write_b128 groups on the LDS side)
   struct Stage {
-    u32x4 a[NA][APRE ? 3 : 2];   // 8 fp32 of A as bit patterns (integer vectors keep the stages out of
-                                 // scratch), or its three bf16 planes (APRE)
+    u32x4 a[NA][2];   // 8 fp32 of A as bit patterns (integer vectors keep the stages out of scratch)
     u32x4 w[3][NB];
     __device__ __forceinline__ static void unit(int u, int& row, int& q) {
       q = (u >> 3) & 3;
       row = (u & 7) + 8 * (u >> 5);
     }
     __device__ __forceinline__ void load(const GemmP& p, const float* A, const unsigned short* W, long plane, int m0,
-                                         int n0, int k0, int tid, const unsigned short* Ab = nullptr,
-                                         long aplane = 0) {
+                                         int n0, int k0, int tid) {
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
         int row, q;
         unit(tid + NT * i, row, q);
-        if constexpr (APRE) {
-          const unsigned short* src = Ab + (long)min(m0 + row, p.M - 1) * p.lda + k0 + 8 * q;
-#pragma unroll
-          for (int pl = 0; pl < 3; ++pl) a[i][pl] = *reinterpret_cast<const u32x4*>(src + pl * aplane);
-        } else {
-          const float* src = A + (long)min(m0 + row, p.M - 1) * p.lda + k0 + 8 * q;
-          a[i][0] = *reinterpret_cast<const u32x4*>(src);
-          a[i][1] = *reinterpret_cast<const u32x4*>(src + 4);
-        }
+        const float* src = A + (long)min(m0 + row, p.M - 1) * p.lda + k0 + 8 * q;
+        a[i][0] = *reinterpret_cast<const u32x4*>(src);
+        a[i][1] = *reinterpret_cast<const u32x4*>(src + 4);
       }
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
@@ -1249,16 +1235,11 @@ void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
       for (int i = 0; i < NA; ++i) {
         int row, q;
         unit(tid + NT * i, row, q);
-        if constexpr (APRE) {
-#pragma unroll
-          for (int pl = 0; pl < 3; ++pl) S[pl * PA + q * BM + row] = __builtin_bit_cast(uint4, a[i][pl]);
-        } else {
-          uint4 h, m, l;
-          split3_quad(__builtin_bit_cast(float4, a[i][0]), __builtin_bit_cast(float4, a[i][APRE ? 0 : 1]), h, m, l);
-          S[0 * PA + q * BM + row] = h;
-          S[1 * PA + q * BM + row] = m;
-          S[2 * PA + q * BM + row] = l;
-        }
+        uint4 h, m, l;
+        split3_quad(__builtin_bit_cast(float4, a[i][0]), __builtin_bit_cast(float4, a[i][1]), h, m, l);
+        S[0 * PA + q * BM + row] = h;
+        S[1 * PA + q * BM + row] = m;
+        S[2 * PA + q * BM + row] = l;
       }
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
@@ -1300,12 +1281,12 @@ void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
   };
 
   const int nk = (SPL ? min(xs.kchunk, p.K - kb) : p.K) / 32;
-  stg.load(p, A, W, plane, m0, n0, 0, tid, Ab, aplane);
+  stg.load(p, A, W, plane, m0, n0, 0, tid);
   if (PF < 0) {
     stg.store(smem, tid);
     __syncthreads();
     for (int t = 0; t < nk; ++t) {
-      stg.load(p, A, W, plane, m0, n0, 32 * min(t + 1, nk - 1), tid, Ab, aplane);   // unconditional (clamped re-read)
+      stg.load(p, A, W, plane, m0, n0, 32 * min(t + 1, nk - 1), tid);   // unconditional (clamped re-read)
       compute(smem);
       __syncthreads();
       stg.store(smem, tid);
@@ -1315,29 +1296,29 @@ void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
     stg.store(smem, tid);
     __syncthreads();
     for (int t = 0; t < nk; ++t) {
-      stg.load(p, A, W, plane, m0, n0, 32 * min(t + 1, nk - 1), tid, Ab, aplane);   // unconditional (clamped re-read)
+      stg.load(p, A, W, plane, m0, n0, 32 * min(t + 1, nk - 1), tid);   // unconditional (clamped re-read)
       compute(smem + (t & 1) * STAGE);
       stg.store(smem + ((t + 1) & 1) * STAGE, tid);
       __syncthreads();
     }
   } else if (PF == 3) {
     // three register stages: tile t + 3's loads issued before tile t's MFMAs
-    stg2.load(p, A, W, plane, m0, n0, 32 * min(1, nk - 1), tid, Ab, aplane);
-    stg3.load(p, A, W, plane, m0, n0, 32 * min(2, nk - 1), tid, Ab, aplane);
+    stg2.load(p, A, W, plane, m0, n0, 32 * min(1, nk - 1), tid);
+    stg3.load(p, A, W, plane, m0, n0, 32 * min(2, nk - 1), tid);
     stg.store(smem, tid);
     __syncthreads();
     for (int t = 0; t < nk; t += 3) {
-      stg.load(p, A, W, plane, m0, n0, 32 * min(t + 3, nk - 1), tid, Ab, aplane);
+      stg.load(p, A, W, plane, m0, n0, 32 * min(t + 3, nk - 1), tid);
       compute(smem + (t & 1) * STAGE);
       stg2.store(smem + ((t + 1) & 1) * STAGE, tid);
       __syncthreads();
       if (t + 1 >= nk) break;
-      stg2.load(p, A, W, plane, m0, n0, 32 * min(t + 4, nk - 1), tid, Ab, aplane);
+      stg2.load(p, A, W, plane, m0, n0, 32 * min(t + 4, nk - 1), tid);
       compute(smem + ((t + 1) & 1) * STAGE);
       stg3.store(smem + (t & 1) * STAGE, tid);
       __syncthreads();
       if (t + 2 >= nk) break;
-      stg3.load(p, A, W, plane, m0, n0, 32 * min(t + 5, nk - 1), tid, Ab, aplane);
+      stg3.load(p, A, W, plane, m0, n0, 32 * min(t + 5, nk - 1), tid);
       compute(smem + (t & 1) * STAGE);
       stg.store(smem + ((t + 1) & 1) * STAGE, tid);
       __syncthreads();
@@ -1345,16 +1326,16 @@ void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
   } else {
     // two register stages: the loads of tile t + 2 are issued before tile t's MFMAs, so each tile's
     // global reads have two K steps of compute to land in (the L2 / MALL latency under full load)
-    stg2.load(p, A, W, plane, m0, n0, 32 * min(1, nk - 1), tid, Ab, aplane);
+    stg2.load(p, A, W, plane, m0, n0, 32 * min(1, nk - 1), tid);
         stg.store(smem, tid);
     __syncthreads();
     for (int t = 0; t < nk; t += 2) {
-      stg.load(p, A, W, plane, m0, n0, 32 * min(t + 2, nk - 1), tid, Ab, aplane);
+      stg.load(p, A, W, plane, m0, n0, 32 * min(t + 2, nk - 1), tid);
       compute(smem);
             stg2.store(smem + STAGE, tid);
       __syncthreads();
       if (t + 1 >= nk) break;
-      stg2.load(p, A, W, plane, m0, n0, 32 * min(t + 3, nk - 1), tid, Ab, aplane);
+      stg2.load(p, A, W, plane, m0, n0, 32 * min(t + 3, nk - 1), tid);
       compute(smem + STAGE);
             stg.store(smem, tid);
       __syncthreads();
@@ -2463,9 +2444,6 @@ extern "C" int dasa_gemm_f32x6_ws(const dasa_gemm_desc* d, int64_t plane, void* 
     case 15: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, false, 2>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
     case 16: hipLaunchKernelGGL((gemm_f32x6_dma_kernel<128, 128, 4, 2>), grid, dim3(512), 0, st, p, (long)plane); break;
     case 20: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true, -1>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
-    // r04 probe (forced only): A pre-split into bf16 planes by the caller (d->A = the planes)
-    case 22: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true, -1, false, 0, true>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
-    case 23: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true, 2, false, 0, true>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
     default: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
   }
   DASA_CHECK_LAUNCH();
