@@ -24,9 +24,9 @@ FAMILIES = {
     "bilstm_bptt": ("mfma", "bilstm_bptt_step_kernel"),
     "shift_attn": ("hbm", "attn_split_dots_kernel<5> + attn_split_ctx_kernel<5> (B < 128) / attn_rows_fwd_kernel<3>"),
     "shift_attn_bwd": ("hbm", "attn_split_bwd_kernel<5> (B*17 <= 1024) / attn_bwd_dp_kernel<12>+attn_bwd_apply_kernel<12>"),
-    "softdot": ("hbm", "attn_fwd_kernel<16> (B < 128) / attn_rows_fwd_kernel<N/12>"),
+    "softdot": ("hbm", "attn_split_dots_kernel<10> + attn_split_ctx_kernel<10> / attn_rows_fwd_kernel<N/12>"),
     "softdot_bwd": ("hbm", "attn_split_bwd_kernel<10> / attn_bwd_dp_kernel<16>+attn_bwd_apply_kernel<16>"),
-    "cand_logit": ("hbm", "attn_dot_rows_kernel (B < 128) / attn_fwd_kernel<16>"),
+    "cand_logit": ("hbm", "attn_dot_rows_kernel"),
     "cand_logit_bwd": ("hbm", "attn_split_bwd_kernel<2> / attn_bwd_apply_kernel<16>"),
     "mha": ("mfma", "mha_fwd_kernel"),
     "mha_bwd": ("mfma", "mha_bwd_kernel / mha_bwd_lds_kernel"),
