@@ -1,9 +1,12 @@
-"""Host-side (Python) cost of one bench training iteration: cProfile of train_step, top functions."""
+"""Host-side (Python) profile of the bench training iteration's phases: cProfile over
+accumulate_gradient (both rollouts) and optim_step (backward + RMSprop) after warm-up, top functions by
+own time. Shows where the host spends the ~15 ms per iteration the GPU idles in the backward phase.
+    python tools/host_prof.py"""
 import cProfile
+import io
 import os
 import pstats
 import sys
-import time
 
 import torch
 
@@ -12,25 +15,23 @@ import bench  # noqa: E402
 
 
 def main():
+    sys.argv = sys.argv[:1]
     a = bench.parse()
-    rank, world = bench.setup_dist(a)
-    from dasa_amd import functional as DF
-    DF.reseed(1234)
-    agent, env = bench.build_agent(a, rank, world)
-    bench.train_step(agent)
+    agent, _ = bench.build_agent(a, 0, 1)
+    for _ in range(2):
+        bench.train_step(agent)
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    bench.train_step(agent)
-    torch.cuda.synchronize()
-    print(f"wall {1e3 * (time.perf_counter() - t0):.1f} ms")
-    pr = cProfile.Profile()
-    pr.enable()
-    bench.train_step(agent)
-    torch.cuda.synchronize()
-    pr.disable()
-    st = pstats.Stats(pr)
-    st.sort_stats("tottime").print_stats(35)
-    st.sort_stats("cumtime").print_stats(30)
+    for name, fn in (("rollouts", lambda: (agent.zero_grad(), agent.accumulate_gradient("sample"))),
+                     ("optim_step", lambda: agent.optim_step())):
+        pr = cProfile.Profile()
+        pr.enable()
+        fn()
+        torch.cuda.synchronize()
+        pr.disable()
+        s = io.StringIO()
+        pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(25)
+        print(f"==== {name}")
+        print(s.getvalue()[:6000])
 
 
 if __name__ == "__main__":
