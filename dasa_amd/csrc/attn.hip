@@ -345,10 +345,20 @@ __global__ __launch_bounds__(576) void attn_rows_fwd_kernel(FwdArgs a) {
     }
     __syncthreads();   // red / swt are rewritten by the next slice
   };
+  // slices s = 0 .. NS-1 alternate between the two register buffers; the buffer a slice has just
+  // been folded from is reloaded with slice s + 2 (NS <= 7: N <= 84, the instruction SoftDot's 80 rows)
   slice(xa, 0);
   if (NS > 2) load(xa, 24);
   if (NS > 1) slice(xb, 12);
+  if (NS > 3) load(xb, 36);
   if (NS > 2) slice(xa, 24);
+  if (NS > 4) load(xa, 48);
+  if (NS > 3) slice(xb, 36);
+  if (NS > 5) load(xb, 60);
+  if (NS > 4) slice(xa, 48);
+  if (NS > 6) load(xa, 72);
+  if (NS > 5) slice(xb, 60);
+  if (NS > 6) slice(xa, 72);
   if (t < 64) {   // the exact softmax / shifted weights from the saved scores
     const float M = m_run, inv = 1.f / z_run;
     if (lane == 0) sscale = inv;
@@ -970,9 +980,10 @@ void split_launch(const SplitArgs& a, int B, hipStream_t st) {
 // pays at large B — B = 256: shift 0.44 -> 0.57 of HBM peak — and loses at B = 20, where the row-split
 // kernel's 60 workgroups win despite their merge (9.2 vs 10.6 us; profiles/r03/attn_forms.txt).
 constexpr int kRowsMinB = 128;
-bool rows_ok(int B, int N, int D) {
+bool rows_ok(int B, int N, int D, bool shift = true) {
   if (g_attn_mode < 0) split_rpt(1, 1, 128, false);   // reads DASA_ATTN_SPLIT once
-  return g_attn_mode != 1 && B >= kRowsMinB && N >= 1 && N <= 36 && D <= 4 * 576;
+  // the shift attention's rings need N <= 36; SoftDot takes up to seven 12-row slices (N <= 84)
+  return g_attn_mode != 1 && B >= kRowsMinB && N >= 1 && N <= (shift ? 36 : 84) && D <= 4 * 576;
 }
 
 int launch_rows(const FwdArgs& a, int B, hipStream_t st) {
@@ -981,7 +992,11 @@ int launch_rows(const FwdArgs& a, int B, hipStream_t st) {
   switch (ns) {
     case 1: hipLaunchKernelGGL(attn_rows_fwd_kernel<1>, grid, block, 0, st, a); break;
     case 2: hipLaunchKernelGGL(attn_rows_fwd_kernel<2>, grid, block, 0, st, a); break;
-    default: hipLaunchKernelGGL(attn_rows_fwd_kernel<3>, grid, block, 0, st, a); break;
+    case 3: hipLaunchKernelGGL(attn_rows_fwd_kernel<3>, grid, block, 0, st, a); break;
+    case 4: hipLaunchKernelGGL(attn_rows_fwd_kernel<4>, grid, block, 0, st, a); break;
+    case 5: hipLaunchKernelGGL(attn_rows_fwd_kernel<5>, grid, block, 0, st, a); break;
+    case 6: hipLaunchKernelGGL(attn_rows_fwd_kernel<6>, grid, block, 0, st, a); break;
+    default: hipLaunchKernelGGL(attn_rows_fwd_kernel<7>, grid, block, 0, st, a); break;
   }
   DASA_CHECK_LAUNCH();
   return 0;
@@ -1055,7 +1070,7 @@ extern "C" int dasa_softdot_fwd(const float* q, const float* ctx, int64_t ldn, c
   if (bad_common(q, ctx, ldn, B, N, D, ws) || (wctx && !aligned16(wctx))) return (int)hipErrorInvalidValue;
   FwdArgs a{q, ctx, (long)ldn, mask, nullptr, 0, scores, probs, nullptr, nullptr, wctx, N, D};
   if (g_attn_mode < 0) split_rpt(1, 1, 128, false);   // reads DASA_ATTN_SPLIT once
-  if ((probs || wctx) && rows_ok(B, N, D)) return launch_rows(a, B, (hipStream_t)stream);
+  if ((probs || wctx) && rows_ok(B, N, D, false)) return launch_rows(a, B, (hipStream_t)stream);
   if (!probs && !wctx && scores && g_attn_mode != 1 && D <= 4 * 1024) {   // scores only (every B: see below)
     hipLaunchKernelGGL(attn_dot_rows_kernel, dim3(N, B), dim3(256), 0, (hipStream_t)stream, q, ctx, (long)ldn,
                        scores, N, D);

@@ -139,7 +139,8 @@ int dasa_mha_bwd(const float* Q, int64_t ldq, const float* K, int64_t ldk, const
  * zero) and the next 33 x 1024 are monotonic group-barrier counters (zero once), so a caller zeroes
  * the buffer once and reuses it on one stream for calls of any shape.
  * Implementations, same results to fp32 rounding: row-split (a batch row's rows over workgroups,
- * online-softmax merge by the last workgroup); forward with N <= 36 and B >= 128, whole-row (one
+ * online-softmax merge by the last workgroup); forward with B >= 128 and N <= 36 (shift) / N <= 84
+ * (SoftDot), whole-row (one
  * workgroup streams a batch row); backward with N <= 80, D % 128 == 0 and B * D/128 <= 1024 (the
  * decision step's B = 20), D-split (a batch row's 128-float column chunks over D/128 workgroups that
  * meet at a bounded group barrier; a timeout NaN-poisons the outputs and ORs 4 into the error word,

@@ -325,11 +325,13 @@ def test_softdot_fused_shapes(dev, B, N, D, ldn, attn_mode):
     assert (sc2.cpu().double() - s.detach()).abs().max() < 1e-4
 
 
-@pytest.mark.parametrize("N,D,ldn", [(36, 2176, 2176), (20, 2048, 2176), (7, 2176, 2176)])
+@pytest.mark.parametrize("N,D,ldn", [(36, 2176, 2176), (20, 2048, 2176), (7, 2176, 2176), (80, 2048, 2048),
+                                     (80, 2048, 2176), (49, 2176, 2176), (84, 1024, 1024)])
 def test_attention_whole_row_forward(dev, N, D, ldn):
     """The whole-row forward (B >= 128: one workgroup per batch row, rows streamed 12 at a time with an
-    online softmax) against fp64 host math: SoftDot with a mask at N = 36 / 20 / 7 (strided rows), and
-    the K=5 shift attention over the 36-view panorama."""
+    online softmax) against fp64 host math: SoftDot with a mask at N = 7 ... 84 (up to seven 12-row
+    slices, the last one partial; strided rows: configs[4]'s N = 80 instruction attention), and the K=5
+    shift attention over the 36-view panorama."""
     from dasa_amd import ops
     ops.attn_set_mode(0)
     g = torch.Generator().manual_seed(N + D)
