@@ -16,6 +16,12 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from dasa_amd import ops  # noqa: E402
 
 
+def _native(x, W):
+    y = torch.empty(x.shape[0], W.shape[0], device=x.device)
+    ops.gemm(x, W, y, M=x.shape[0], N=W.shape[0], K=x.shape[1], lda=x.shape[1], ldb=W.shape[1], ldc=W.shape[0])
+    return y
+
+
 def cases(dev, g):
     def rnd(*s, scale=1.0):
         return torch.randn(*s, device=dev, generator=g) * scale
@@ -57,6 +63,14 @@ def cases(dev, g):
     feat2 = rnd(256, 36, 2176, scale=0.2)
     out.append(("shift B256", (rnd(256, 2176, scale=0.05), rnd(256, 2176, scale=0.05)),
                 lambda q: ops.shift_attn_fwd(q, feat2, rnd(256, 5) * 0 + 0.1)[0]))
+    # LXRT / language attention core (mha_fwd: LDS-staged K / V, MFMA), B = 20 x 12 heads, L = 80
+    qkv = rnd(20, 80, 3 * 768)
+    out.append(("mha B20 L80", (rnd(20, 80, 768), rnd(20, 80, 768)),
+                lambda q: ops.mha(q, qkv[..., 768:1536], qkv[..., 1536:], None, 12, 0.125)))
+    # the native fp32 MFMA GEMM as a victim (LXRT short-K projection shape)
+    Wn2 = rnd(768, 768, scale=0.02)
+    out.append(("gemm_f32 1600x768x768", (rnd(1600, 768), rnd(1600, 768)),
+                lambda x: _native(x, Wn2)))
     # per-row kernels of the step (wave reductions only)
     gam, bet = rnd(768, scale=0.1) + 1, rnd(768, scale=0.1)
     out.append(("layernorm 1600x768", (rnd(1600, 768), rnd(1600, 768)),
