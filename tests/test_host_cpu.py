@@ -235,3 +235,18 @@ def test_teacher_plan_matches_stepwise_oracle(mode, seed):
     assert len(plan) == t + 1
     np.testing.assert_array_equal(ended, ended2)
     assert [ob["viewpoint"] for ob in final_obs] == [ob["viewpoint"] for ob in po]
+
+
+def test_train_graph_slot_pads():
+    """Captured training steps pad their static inputs so one slot serves every batch of a step index:
+    candidates to 16, 32, 64, ...; the instruction context to --maxInput tokens rounded up to 16
+    (agent_dg.Seq2SeqAgent._slot_pads)."""
+    from dasa_amd.r2r import param
+    param.readme_train(["--d_vl_layers", "1", "--batchSize", "2", "--maxAction", "5"])
+    from dasa_amd.r2r.agent_dg import Seq2SeqAgent
+    L0 = -(-param.args.maxInput // 16) * 16
+    assert Seq2SeqAgent._slot_pads(3, 7) == (16, L0)
+    assert Seq2SeqAgent._slot_pads(16, L0) == (16, L0)
+    assert Seq2SeqAgent._slot_pads(17, 1) == (32, L0)
+    assert Seq2SeqAgent._slot_pads(33, 1) == (64, L0)
+    assert Seq2SeqAgent._slot_pads(5, L0 + 3)[1] == L0 + 16      # longer than --maxInput: its own extent
