@@ -250,3 +250,22 @@ def test_train_graph_slot_pads():
     assert Seq2SeqAgent._slot_pads(17, 1) == (32, L0)
     assert Seq2SeqAgent._slot_pads(33, 1) == (64, L0)
     assert Seq2SeqAgent._slot_pads(5, L0 + 3)[1] == L0 + 16      # longer than --maxInput: its own extent
+
+
+def test_synth_back_teacher_is_a_candidate_or_here():
+    """env.py:348: back_teacher is the next viewpoint on the shortest path back to the episode start,
+    so --pred_back's target (agent_dg._back_teacher_action) is always a candidate or the current
+    viewpoint, wherever the agent stands."""
+    import numpy as np
+    from dasa_amd.r2r import param
+    param.readme_train(["--d_vl_layers", "1", "--batchSize", "4", "--maxAction", "5"])
+    from dasa_amd.synth import SynthR2RBatch, SynthWorld
+    env = SynthR2RBatch(SynthWorld(16, 0, 3), 4, seed=33, mode="goal", instr_len=80, variable_len=True)
+    env.reset()
+    rng = np.random.default_rng(0)
+    for _ in range(8):
+        for sim in env.env.sims:
+            sim.vp = int(rng.integers(16))
+        for ob in env._get_obs():
+            assert ob["back_teacher"] == ob["viewpoint"] or any(
+                c["viewpointId"] == ob["back_teacher"] for c in ob["candidate"]), ob["viewpoint"]
