@@ -10,7 +10,8 @@ stops when the policy says so, exactly as the reference. value = decisions / s w
 sum over rollouts of (batched steps x B), summed over all ranks.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 20] [--max-action 35] [--vl 3]
-    torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU, RCCL)
+        (N > 1: bench.py starts the N rank processes itself, one per GPU, RCCL)
+    torchrun --nproc-per-node N bench.py --gpus N ...      (the same under an external launcher)
 """
 import argparse
 import contextlib
@@ -63,24 +64,94 @@ def parse():
     p.add_argument("--backend", default="nccl", help="nccl (= RCCL on ROCm) | gloo (rehearsal only)")
     p.add_argument("--same-device", action="store_true",
                    help="map every rank to cuda:0 (rehearsing the DP path on a one-GPU box with gloo)")
+    p.add_argument("--dist-check", action="store_true",
+                   help="launch the ranks, build the process group, all-reduce once, print the world; no model")
     return p.parse_args()
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(a):
+    """`--gpus N` (N > 1) without a launcher environment: start the N ranks here, one process per GPU,
+    as torch.distributed.run would (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT),
+    each re-running this script with the same arguments. The parent never touches the GPU (it only
+    waits), rank 0 prints the JSON line, and the exit code is the first failing rank's (the others are
+    stopped). Reference DP launch: tasks/R2R/nav_dic_pretrain.py:252,765 (one process per GPU, NCCL)."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus), LOCAL_WORLD_SIZE=str(a.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                code = p.poll()
+                if code is None:
+                    continue
+                pending.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    for q in pending:          # a failed rank leaves the others in a collective: stop them
+                        q.terminate()
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
 
 
 def setup_dist(a):
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but the launcher's WORLD_SIZE is {world}", file=sys.stderr)
+        sys.exit(3)
+    cpu = a.dist_check and a.backend == "gloo" and not torch.cuda.is_available()
     if world > 1:
         dev = 0 if a.same_device else local
-        torch.cuda.set_device(dev)
+        if not cpu:
+            torch.cuda.set_device(dev)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if a.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group(a.backend)
-    else:
+        if dist.get_world_size() != a.gpus:
+            print(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus {a.gpus}", file=sys.stderr)
+            sys.exit(3)
+    elif not cpu:
         torch.cuda.set_device(0)
     return rank, world
+
+
+def dist_check(a, rank, world):
+    """`--dist-check`: the launch path alone (rank processes, process group, one all-reduce), no model:
+    prints {"world_size", "backend", "rank_sum"} from rank 0 (tests rehearse it with gloo on the CPU)."""
+    dev = "cpu" if (a.backend == "gloo" and not torch.cuda.is_available()) else "cuda"
+    t = torch.tensor([float(rank)], device=dev)
+    if world > 1:
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"world_size": world, "n_gpus": a.gpus,
+                          "backend": dist.get_backend() if world > 1 else None, "rank_sum": float(t.item())}),
+              flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def build_agent(a, rank, world, finetune=False):
@@ -344,7 +415,12 @@ def cfg5_leg(a):
 
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(a))        # before any GPU call in this process
     rank, world = setup_dist(a)
+    if a.dist_check:
+        dist_check(a, rank, world)
+        return
     torch.manual_seed(1 + rank)
     from dasa_amd import functional as DF
     DF.reseed(1234 + rank)

@@ -13,6 +13,15 @@ import torch.distributed as dist
 
 
 class GradSync:
+    """One flat-bucket all-reduce of the gradient-receiving parameters per optimizer step.
+
+    Which parameters received a gradient on ANY rank is agreed every step (a small mask all-reduce), so a
+    mode switch (e.g. teacher-only iterations, where the critic gets none) stays exact. The mask
+    all-reduce is enqueued by `prepare()` before optim_step's device-error-word read, and its host read
+    in `__call__` comes after it: the step's one host sync (the error-word check, which must precede
+    clipping and the optimizers anyway) covers both — no second sync per step. The host-side local mask
+    is cached per gradient set, so no host->device copy is made either."""
+
     def __init__(self, params, bucket_mb=256):
         self.params = [p for p in params if p.requires_grad]
         self.world = dist.get_world_size()
@@ -22,13 +31,27 @@ class GradSync:
         self.mask = torch.empty(len(self.params), dtype=torch.float32, device=dev)
         self.bucket = max(1, int(bucket_mb * 2**20 / 4))
         self.sent = 0            # floats all-reduced by the last call
+        self._local = {}         # gradient set (tuple of bools) -> its mask on the device
+        self._prepared = False
+
+    def prepare(self):
+        """Enqueue the mask all-reduce (no host sync). Call after backward, before the host sync that
+        precedes __call__; __call__ does it itself when it was not called."""
+        local = tuple(p.grad is not None for p in self.params)
+        m = self._local.get(local)
+        if m is None:
+            m = self._local[local] = self.mask.new_tensor([1.0 if g else 0.0 for g in local])
+        self.mask.copy_(m)
+        dist.all_reduce(self.mask)
+        self._prepared = True
 
     def __call__(self):
-        # which parameters received a gradient on ANY rank (one small all-reduce + host read): only
-        # those travel in the bucket — the 47.23 M floats of the README train config, not the 58 M
-        # trainable ones (the unused linear_out heads, encoder2decoder_*, never get one)
-        self.mask.copy_(torch.tensor([1.0 if p.grad is not None else 0.0 for p in self.params]))
-        dist.all_reduce(self.mask)
+        # which parameters received a gradient on ANY rank: only those travel in the bucket — the
+        # 47.23 M floats of the README train config, not the 58 M trainable ones (the unused linear_out
+        # heads, encoder2decoder_*, never get one)
+        if not self._prepared:
+            self.prepare()
+        self._prepared = False
         m = self.mask.cpu().tolist()
         off = 0
         for p, any_rank in zip(self.params, m):

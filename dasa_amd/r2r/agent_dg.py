@@ -1047,7 +1047,11 @@ class Seq2SeqAgent(BaseAgent):
             self._train_graphs.new_iteration()     # every replayed step has had its backward
         # every kernel with a bounded inter-workgroup barrier (persistent bi-LSTM BPTT, D-split attention
         # backward) NaN-poisons its outputs and sets an error bit when the barrier times out: read the
-        # error word (one host sync) before the gradients reach grad_sync, clipping and the optimizers
+        # error word (one host sync) before the gradients reach grad_sync, clipping and the optimizers;
+        # the data-parallel mask all-reduce is enqueued first, so that one sync covers its host read too
+        prep = getattr(self.grad_sync, "prepare", None)
+        if prep is not None:
+            prep()
         ops.check_device_errors()
         if self.grad_sync is not None:
             self.grad_sync()

@@ -32,6 +32,7 @@ def _worker(rank, world, port, q):
     m[2].bias.grad = None if rank == 1 else m[2].bias.grad     # a grad present on one rank only
     m[0].weight.grad = None                                   # ... and a grad present on no rank
     local = {k: (p.grad.clone() if p.grad is not None else None) for k, p in m.named_parameters()}
+    sync.prepare()                           # mask all-reduce enqueued ahead of the step's host sync
     sync()
     out = {k: (p.grad.clone() if p.grad is not None else None) for k, p in m.named_parameters()}
     weights = {k: p.detach().clone() for k, p in m.named_parameters()}
