@@ -60,6 +60,8 @@ SIGNATURES = {
     "dasa_softdot_fwd": (i32, [vp, vp, i64, vp, vp, vp, vp, i32, i32, i32, vp, vp]),
     "dasa_attn_workspace": (i64, [i32, i32, i32]),
     "dasa_attn_set_mode": (i32, [i32]),
+    "dasa_attn_debug_buffer": (i32, [vp, i64]),
+    "dasa_attn_debug_record_floats": (i64, []),
     "dasa_softdot_bwd": (i32, [vp, vp, i64, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp, vp]),
     "dasa_shift_attn_fwd": (i32, [vp, vp, i64, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp]),
     "dasa_shift_attn_bwd": (i32, [vp, vp, i64, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp, vp]),

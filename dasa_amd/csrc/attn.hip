@@ -107,27 +107,49 @@ __device__ __forceinline__ void lds_wave_sync() {
 // Row dots of the workgroup's rows with vec, summed over the workgroup: returns on lane r < nr of
 // wave 0 (valid after the internal __syncthreads) the dot of row r; thread t < D/4 keeps its float4
 // of each row in x (D <= 4096, so one column per thread).
-template <int RB>
+// Diagnosis dump (dasa_attn_debug_buffer; r05): per workgroup a record of kDbgRec floats —
+// [0] HW_ID, [1] XCC_ID, [2] blockIdx.x, [3] blockIdx.y (as raw bits), then per thread its 16 row
+// partials v[] (blockDim x 16), a checksum of its q float4 (blockDim), the 16 x 16 wave partials as
+// written to red[w][r], and the 16 row dots wave 0 summed. Diagnosis only: written beside, never read.
+constexpr int kDbgHdr = 4, kDbgMaxT = 1024;
+constexpr int kDbgRec = kDbgHdr + kDbgMaxT * 16 + kDbgMaxT + kMaxW * 16 + 16;
+
+template <int RB, bool DBG = false>
 __device__ __forceinline__ float block_row_dots(const float* rows, long ldn, int nr, const float* vec, int D4,
-                                                float4 (&x)[RB], float (*red)[16]) {
+                                                float4 (&x)[RB], float (*red)[16], float* dbg = nullptr) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, W = blockDim.x >> 6;
   float v[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) v[i] = 0.f;
+  float qsum = 0.f;
   if (t < D4) {   // D4 <= blockDim: one float4 column per thread
     const float4 qv = reinterpret_cast<const float4*>(vec)[t];
 #pragma unroll
     for (int i = 0; i < RB; ++i) x[i] = reinterpret_cast<const float4*>(rows + (long)min(i, nr - 1) * ldn)[t];
 #pragma unroll
     for (int i = 0; i < RB; ++i) v[i] = dot4(x[i], qv);
+    if (DBG) qsum = (qv.x + qv.y) + (qv.z + qv.w);
+  }
+  if (DBG) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dbg[kDbgHdr + t * 16 + i] = v[i];
+    dbg[kDbgHdr + kDbgMaxT * 16 + t] = qsum;
+    if (t == 0) {
+      dbg[0] = __uint_as_float(__builtin_amdgcn_s_getreg(0xF804));   // HW_REG_HW_ID, 32 bits
+      dbg[1] = __uint_as_float(__builtin_amdgcn_s_getreg(0xF814));   // HW_REG_XCC_ID
+      dbg[2] = __uint_as_float(blockIdx.x);
+      dbg[3] = __uint_as_float(blockIdx.y);
+    }
   }
   const float s = reduce_scatter16(v, lane);
   const int r = (lane >> 2) & 15;
   if ((lane & 3) == 0 && r < RB) red[w][r] = s;
+  if (DBG && (lane & 3) == 0) dbg[kDbgHdr + kDbgMaxT * 17 + w * 16 + r] = s;
   __syncthreads();
   float tot = 0.f;
   if (t < 64 && lane < nr)
     for (int i = 0; i < W; ++i) tot += red[i][lane];
+  if (DBG && t < 16) dbg[kDbgHdr + kDbgMaxT * 17 + kMaxW * 16 + t] = tot;
   return tot;
 }
 
@@ -161,9 +183,10 @@ struct FwdArgs {
   float* scores; float* probs; float* shifted; float* wsm; float* wctx;
   int N, D, nblk;
   unsigned* cnt; float* ws; int o_part, o_ml, o_ee;   // workspace: counters + byte offsets of partials
+  float* dbg;                                          // row-split diagnosis dump (DBG instantiation only)
 };
 
-template <int RB>
+template <int RB, bool DBG = false>
 __global__ __launch_bounds__(1024) void attn_fwd_kernel(FwdArgs a) {
   __shared__ float red[kMaxW][16];
   __shared__ float se[16], sep[16], sw[kMaxK + 1], ssc[kMaxBlk];
@@ -173,7 +196,8 @@ __global__ __launch_bounds__(1024) void attn_fwd_kernel(FwdArgs a) {
   const bool shift = a.shift_logits != nullptr;
   const float* rows = a.ctx + ((long)b * N + r0) * a.ldn;
   float4 x[RB];
-  const float s = block_row_dots<RB>(rows, a.ldn, nr, a.q + (long)b * a.D, D4, x, red);
+  const float s = block_row_dots<RB, DBG>(rows, a.ldn, nr, a.q + (long)b * a.D, D4, x, red,
+                                          DBG ? a.dbg + (long)(b * nblk + j) * kDbgRec : nullptr);
   const bool combine = a.wctx || a.probs || a.shifted;
   const __amdgpu_buffer_rsrc_t wr = ws_rsrc(a.ws);
   if (t < 64) {
@@ -929,12 +953,21 @@ inline WsLayout ws_layout(void* ws, int B, int N, int D) {
   return L;
 }
 
+float* g_attn_dbg = nullptr;   // dasa_attn_debug_buffer: the next row-split forward dumps here
+int64_t g_attn_dbg_bytes = 0;
+
 template <int RB>
 int launch_fwd(FwdArgs a, int B, void* ws, hipStream_t st) {
   a.nblk = (a.N + RB - 1) / RB;
   WsLayout L = ws_layout(ws, B, a.N, a.D);
   a.cnt = L.cnt1; a.ws = (float*)ws; a.o_part = L.o_part; a.o_ml = L.o_ml; a.o_ee = L.o_ee;
-  hipLaunchKernelGGL(attn_fwd_kernel<RB>, dim3(a.nblk, B), dim3(block_threads(a.D)), 0, st, a);
+  if (g_attn_dbg && (int64_t)a.nblk * B * kDbgRec * 4 <= g_attn_dbg_bytes) {
+    a.dbg = g_attn_dbg;
+    g_attn_dbg = nullptr;   // one launch per armed buffer
+    hipLaunchKernelGGL((attn_fwd_kernel<RB, true>), dim3(a.nblk, B), dim3(block_threads(a.D)), 0, st, a);
+  } else {
+    hipLaunchKernelGGL(attn_fwd_kernel<RB>, dim3(a.nblk, B), dim3(block_threads(a.D)), 0, st, a);
+  }
   DASA_CHECK_LAUNCH();
   return 0;
 }
@@ -1057,6 +1090,15 @@ extern "C" int dasa_attn_set_mode(int32_t mode) {
   g_attn_mode = mode;
   return 0;
 }
+
+extern "C" int dasa_attn_debug_buffer(float* buf, int64_t bytes) {
+  if (buf && (bytes < (int64_t)kDbgRec * 4 || ((uintptr_t)buf & 15))) return (int)hipErrorInvalidValue;
+  g_attn_dbg = buf;
+  g_attn_dbg_bytes = buf ? bytes : 0;
+  return 0;
+}
+
+extern "C" int64_t dasa_attn_debug_record_floats() { return kDbgRec; }
 
 extern "C" int64_t dasa_attn_workspace(int32_t B, int32_t N, int32_t D) {
   if (B <= 0 || N <= 0 || D <= 0) return 16;

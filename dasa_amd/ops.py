@@ -586,6 +586,17 @@ def attn_set_mode(mode):
     _lib.check(_lib.lib().dasa_attn_set_mode(int(mode)), "dasa_attn_set_mode")
 
 
+def attn_debug_buffer(buf):
+    """Diagnosis hook (include/dasa_hip.h dasa_attn_debug_buffer): the next row-split forward launch dumps
+    its per-workgroup records into `buf` (float32, device; None disarms). Returns the record size in
+    floats."""
+    if buf is None:
+        _lib.check(_lib.lib().dasa_attn_debug_buffer(None, 0), "dasa_attn_debug_buffer")
+    else:
+        _lib.check(_lib.lib().dasa_attn_debug_buffer(_p(buf), buf.numel() * 4), "dasa_attn_debug_buffer")
+    return int(_lib.lib().dasa_attn_debug_record_floats())
+
+
 def _attn_ws(device, B, N, D):
     """Attention workspace (include/dasa_hip.h dasa_attn_workspace): one zero-initialised buffer per
     (device, stream), grown on demand. Its leading arrival counters are left zero by every call, so

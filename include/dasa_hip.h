@@ -153,6 +153,13 @@ int dasa_mha_bwd(const float* Q, int64_t ldq, const float* K, int64_t ldk, const
  * mode 1), 1 = row-split only, 2 = the same as 0 (kept for callers of r03). Host-only setting.      */
 int64_t dasa_attn_workspace(int32_t B, int32_t N, int32_t D);
 int dasa_attn_set_mode(int32_t mode);
+/* Diagnosis hook (r05, tools/rowsplit_diag.py): arm a device buffer of `bytes` (16-B aligned) that the
+ * NEXT row-split forward launch (attn_fwd_kernel, mode 1) fills with one record of
+ * dasa_attn_debug_record_floats() floats per workgroup — HW_ID / XCC_ID / block index, every thread's 16
+ * row partials, its q checksum, the wave partials as written to LDS and the summed row dots — and then
+ * disarms. buf = NULL disarms. Host-only setting; not capture-safe; not used by the product path.   */
+int dasa_attn_debug_buffer(float* buf, int64_t bytes);
+int64_t dasa_attn_debug_record_floats(void);
 int dasa_softdot_fwd(const float* q, const float* ctx, int64_t ldn, const uint8_t* mask,
                      float* scores, float* probs, float* wctx,
                      int32_t B, int32_t N, int32_t D, float* ws, void* stream);
