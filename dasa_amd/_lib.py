@@ -8,7 +8,9 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdasa_hip.so")
+# DASA_DEBUG=1: the debug library (device input checks compiled in; dasa_amd/build.py --debug)
+LIB_PATH = os.path.join(_HERE, "libdasa_hip_debug.so" if os.environ.get("DASA_DEBUG", "0") not in ("", "0")
+                        else "libdasa_hip.so")
 
 f32p = C.c_void_p  # device pointers travel as integers
 i64 = C.c_int64

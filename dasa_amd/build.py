@@ -19,6 +19,78 @@ FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-pass-fail
          "-I" + os.path.join(os.path.dirname(HERE), "include")]
 
 
+# Debug builds (SURVEY.md §5 "race detection / sanitizers"):
+#  * `python -m dasa_amd.build --debug` -> libdasa_hip_debug.so, loaded instead of the release library when
+#    DASA_DEBUG=1: device code with the DASA_DCHECK input checks compiled in (common.h; a failed check sets
+#    a bit in the error word that ops.check_device_errors() raises on), host code at -O1 -g. It carries no
+#    host ASan: a python process would need the ASan runtime preloaded, and GPU-side ASan / xnack builds are
+#    not available on the GPU pool.
+#  * `python -m dasa_amd.build --debug --host-only` -> a HOST-ONLY (--cuda-host-only: no device code, so
+#    seconds to build, kernels never launched) copy of the same sources under AddressSanitizer +
+#    UndefinedBehaviorSanitizer, driven by tools/asan_host_check.cpp — an executable built with
+#    -fsanitize=address, so the runtime comes first — through every host-side entry point (argument
+#    validation, workspace sizing, the GEMM / attention / bi-LSTM planners): tests/test_debug_cpu.py.
+#  * DASA_CHECK_FINITE=1 (dasa_amd/debug.py): NaN / +Inf check of every op's outputs (release or debug lib).
+OUT_DEBUG = os.path.join(HERE, "libdasa_hip_debug.so")
+SAN = ["-Xarch_host", "-fsanitize=address,undefined", "-Xarch_host", "-fno-omit-frame-pointer",
+       "-Xarch_host", "-fno-sanitize-recover=undefined"]
+_INC = ["-I" + os.path.join(os.path.dirname(HERE), "include")]
+DEBUG_FLAGS = ["-O3", "-Xarch_host", "-O1", "-g", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}",
+               "-Wno-pass-failed", "-Wno-inline-asm", "-DDASA_DEBUG=1"] + _INC
+HOSTSAN_FLAGS = ["-O1", "-g", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "--cuda-host-only",
+                 "-Wno-pass-failed", "-Wno-inline-asm", "-DDASA_DEBUG=1"] + _INC + SAN
+HOSTSAN_OUT = os.path.join(BUILD_DIR, "hostsan", "libdasa_hip_hostsan.so")
+
+
+def build_variant(out, flags, build_dir, link_extra=(), jobs=8):
+    """Compile every source with `flags` into `build_dir` and link `out` (no up-to-date checks)."""
+    os.makedirs(build_dir, exist_ok=True)
+
+    def compile_one(src):
+        obj = os.path.join(build_dir, os.path.basename(src) + ".o")
+        r = subprocess.run([HIPCC] + list(flags) + ["-c", src, "-o", obj], capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
+        return obj
+
+    with ThreadPoolExecutor(max_workers=min(jobs, os.cpu_count() or 1)) as ex:
+        objs = list(ex.map(compile_one, sources()))
+    if "--cuda-host-only" in flags:
+        objs.append(_fatbin_stub(objs, build_dir))
+    cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", out] + list(link_extra) + objs
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stderr}")
+    return out
+
+
+def _fatbin_stub(objs, build_dir):
+    """A host-only object still references each translation unit's device image (__hip_fatbin_<hash>);
+    define each as an empty offload bundle (the magic string, no entries) so the host code links and
+    loads. Nothing in the host-sanitizer run launches a kernel."""
+    names = set()
+    for o in objs:
+        r = subprocess.run(["nm", o], capture_output=True, text=True)
+        names.update(ln.split()[-1] for ln in r.stdout.splitlines() if ln.split()[-1].startswith("__hip_fatbin_")
+                     and ln.split()[0] == "U")
+    src = os.path.join(build_dir, "fatbin_stub.c")
+    with open(src, "w") as f:
+        for n in sorted(names):
+            f.write(f'__attribute__((aligned(4096))) const char {n}[32] = "__CLANG_OFFLOAD_BUNDLE__";\n')
+    obj = src[:-2] + ".o"
+    r = subprocess.run(["gcc", "-c", "-fPIC", src, "-o", obj], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(r.stderr)
+    return obj
+
+
+def build_debug(host_only=False):
+    """The debug library (device DCHECKs), or with host_only=True the host-sanitizer copy."""
+    if host_only:
+        return build_variant(HOSTSAN_OUT, HOSTSAN_FLAGS, os.path.join(BUILD_DIR, "hostsan"), link_extra=SAN[:2])
+    return build_variant(OUT_DEBUG, DEBUG_FLAGS, os.path.join(BUILD_DIR, "debug"))
+
+
 def sources():
     return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
 
@@ -66,4 +138,7 @@ def build(force=False, verbose=True):
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    if "--debug" in sys.argv:
+        print(build_debug(host_only="--host-only" in sys.argv), file=sys.stderr)
+    else:
+        build(force="--force" in sys.argv)

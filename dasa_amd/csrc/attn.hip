@@ -193,6 +193,7 @@ __global__ __launch_bounds__(1024) void attn_fwd_kernel(FwdArgs a) {
   __shared__ int s_flag;
   const int j = blockIdx.x, b = blockIdx.y, t = threadIdx.x, lane = t & 63;
   const int N = a.N, D4 = a.D >> 2, r0 = j * RB, nr = min(RB, N - r0), nblk = a.nblk;
+  DASA_DCHECK((int)blockDim.x >= D4 && nr >= 1 && (int)gridDim.x == nblk, 128);   // one column per thread
   const bool shift = a.shift_logits != nullptr;
   const float* rows = a.ctx + ((long)b * N + r0) * a.ldn;
   float4 x[RB];
@@ -306,6 +307,7 @@ __global__ __launch_bounds__(576) void attn_rows_fwd_kernel(FwdArgs a) {
   __shared__ float ssc[12 * NS], swt[12], sw[kMaxK + 1], sscale;
   const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6, W = blockDim.x >> 6;
   const int N = a.N, D4 = a.D >> 2;
+  DASA_DCHECK((int)blockDim.x >= D4 && N <= 12 * NS, 128);   // one column per thread, N rows in NS slices
   const bool shift = a.shift_logits != nullptr, col = t < D4;
   const float* rows = a.ctx + (long)b * N * a.ldn;
   float4 xa[12], xb[12];
@@ -947,8 +949,10 @@ inline WsLayout ws_layout(void* ws, int B, int N, int D) {
   const long o1 = take(kMaxB), o2 = take(kMaxB), ob = take(kBarSlots * kSplitMaxWG), o3 = take((long)B * N),
              o4 = take((long)B * N), o5 = take((long)B * N), o6 = take((long)B * nblk * 2), o7 = take((long)B * N * 2),
              o8 = take((long)B * nblk * D);
+  // pointers only into a real buffer (a size query passes ws = nullptr: no arithmetic on a null pointer)
   float* f = (float*)ws;
-  WsLayout L{(unsigned*)(f + o1), (unsigned*)(f + o2), (unsigned*)(f + ob), f + o4, f + o5, (int)(o3 * 4),
+  auto at = [&](long o) { return f ? f + o : nullptr; };
+  WsLayout L{(unsigned*)at(o1), (unsigned*)at(o2), (unsigned*)at(ob), at(o4), at(o5), (int)(o3 * 4),
              (int)(o6 * 4), (int)(o7 * 4), (int)(o8 * 4), (int64_t)off * 4};
   return L;
 }

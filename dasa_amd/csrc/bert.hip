@@ -613,6 +613,7 @@ __global__ void reverse_valid_kernel(const float* __restrict__ x, const int* __r
     const long rt = idx / (H / 4);
     const int t = (int)(rt % L), b = (int)(rt / L);
     const int n = len[b];
+    DASA_DCHECK(n >= 0 && n <= L, 64);
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (t < n) v = reinterpret_cast<const float4*>(x + ((long)b * L + (n - 1 - t)) * H)[c];
     reinterpret_cast<float4*>(out + ((long)b * L + t) * H)[c] = v;

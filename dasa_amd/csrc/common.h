@@ -73,6 +73,36 @@ __attribute__((visibility("hidden"))) const uint64_t* dasa_seed_src_host();
 __attribute__((visibility("hidden"))) unsigned* dasa_err_word_host();
 __attribute__((visibility("hidden"))) int dasa_force_timeout_host();
 
+// ---- debug build (dasa_amd/build.py --debug: -DDASA_DEBUG, host ASan + UBSan) ----------------------
+// DASA_DCHECK(cond, bit): a device-side check of an input invariant the kernel relies on (an index in
+// range, a launch shape the kernel assumes). In the debug library a failed check ORs `bit` into the
+// library's error word (dasa_set_error_word; the host raises at its next ops.check_device_errors()) and
+// the thread leaves the kernel — no trap, no fault. `cond` must be uniform over a workgroup wherever the
+// kernel has a barrier after the check. Compiled out of the release library. Bits: 16 policy head
+// target / forced action, 32 gather index, 64 sequence length, 128 attention launch shape.
+#ifdef DASA_DEBUG
+namespace {
+__device__ unsigned* g_dbg_err = nullptr;   // per translation unit, set by dasa_set_error_word
+}
+__attribute__((visibility("hidden"))) void dasa_dbg_register(void (*setter)(unsigned*));
+namespace {
+inline void dasa_dbg_set_err(unsigned* p) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_err), &p, sizeof(p)); }
+[[maybe_unused]] const int dasa_dbg_registered = (dasa_dbg_register(dasa_dbg_set_err), 0);
+}
+#define DASA_DCHECK(cond, bit)                          \
+  do {                                                  \
+    if (!(cond)) {                                      \
+      unsigned* _w = g_dbg_err;                         \
+      if (_w) atomicOr(_w, (unsigned)(bit));            \
+      return;                                           \
+    }                                                   \
+  } while (0)
+#else
+#define DASA_DCHECK(cond, bit) \
+  do {                         \
+  } while (0)
+#endif
+
 __device__ __forceinline__ float dasa_dropout_scale(float p, uint64_t seed, uint64_t idx) {
   if (p <= 0.f) return 1.f;
   return dasa_uniform(seed, idx) >= p ? 1.f / (1.f - p) : 0.f;

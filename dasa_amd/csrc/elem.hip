@@ -204,6 +204,7 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const float* __restric
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (r >= R) return;
   const int a = ia[r], b = ib ? ib[r] : -1;
+  DASA_DCHECK(a >= -1 && b >= -1, 32);
   float4* o = reinterpret_cast<float4*>(out + (long)r * (Fa + Fb));
   const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
   const float4* pa = a >= 0 ? reinterpret_cast<const float4*>(ta + (long)a * Fa) : nullptr;

@@ -483,8 +483,23 @@ __global__ __launch_bounds__(1024) void bilstm_persist_bwd_kernel(PBwd a) {
 static unsigned* g_err_word = nullptr;
 static int g_force_tmo = 0;
 static unsigned long long* g_stamps = nullptr;
+#ifdef DASA_DEBUG
+// debug build: every translation unit registers the setter of its DASA_DCHECK error-word pointer
+static void (*(&dbg_setters())[16])(unsigned*) {
+  static void (*s[16])(unsigned*) = {};
+  return s;
+}
+void dasa_dbg_register(void (*setter)(unsigned*)) {
+  for (auto& f : dbg_setters())
+    if (!f || f == setter) { f = setter; return; }
+}
+#endif
 extern "C" int dasa_set_error_word(uint32_t* dev_word) {
   g_err_word = reinterpret_cast<unsigned*>(dev_word);
+#ifdef DASA_DEBUG
+  for (auto f : dbg_setters())
+    if (f) f(g_err_word);
+#endif
   return 0;
 }
 // Diagnostic hook: when buf != NULL, workgroup 0 of every persistent forward launch writes s_memtime

@@ -45,6 +45,9 @@ __global__ __launch_bounds__(1024) void policy_head_fwd_kernel(PolicyFwd a) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
   for (int b = w; b < a.B; b += nw) {
     const int L = a.len[b];
+    DASA_DCHECK(L >= 0 && L <= a.C, 16);
+    DASA_DCHECK(!a.target || a.target[b] == a.ignore || (a.target[b] >= 0 && a.target[b] < a.C), 16);
+    DASA_DCHECK(a.mode != DASA_POLICY_FORCED || (a.action[b] >= 0 && a.action[b] < L), 16);
     float z[kVpl];
     float m = -INFINITY;
 #pragma unroll

@@ -26,7 +26,9 @@ import torch
 from . import _lib
 from . import prof
 
-ENABLED = os.environ.get("DASA_GRAPH", "1") != "0"
+from . import debug as _debug
+# DASA_CHECK_FINITE (dasa_amd/debug.py) synchronises after every op: no capture / replay then
+ENABLED = os.environ.get("DASA_GRAPH", "1") != "0" and not _debug.active()
 _NESTED = [0]    # > 0 while an enclosing region is being warmed up / captured: inner regions run inline
 
 

@@ -851,3 +851,10 @@ def gather_rows(ta, ia, tb, ib, out):
     _call("dasa_gather_rows", "gather", _lib.lib().dasa_gather_rows, _p(ta), _p(ia), Fa, _p(tb), _p(ib), Fb, _p(out),
           R, _stream(), nbytes=8.0 * R * (Fa + Fb))
     return out
+
+
+# DASA_CHECK_FINITE=1|strict: every tensor-producing entry point above checks its outputs (dasa_amd/debug.py)
+from . import debug as _debug  # noqa: E402
+if _debug.active():
+    import sys as _sys
+    _debug.install(_sys.modules[__name__])

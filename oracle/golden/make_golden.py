@@ -559,6 +559,57 @@ def cfg5(R):
     return out
 
 
+def cfg5_b256(R):
+    """configs[4] at its own batch (GI.CFG5_B256: B=256, vl=6, L<=80 variable): a 2-step teacher-forced
+    eval rollout, fp32 — per-step raw logits, critic values and the last step's states."""
+    A = R.args
+    cfg = GI.CFG5_B256
+    A.d_vl_layers, A.batchSize, A.views, A.maxAction = cfg["vl_layers"], cfg["batch"], 36, cfg["max_action"]
+    world = SynthWorld(n_viewpoints=cfg["viewpoints"], feat_seed=0, graph_seed=cfg["graph_seed"])
+    env = SynthR2RBatch(world, cfg["batch"], seed=cfg["seed"], mode="wander", instr_len=cfg["instr_len"],
+                        variable_len=True)
+    agent = make_agent(R, env, cfg["max_action"])
+    out = {}
+    _eval_rollout(agent, "teacher", out, "b256/")
+    return out
+
+
+def cfg4_full(R):
+    """The README finetune iteration at its real length (GI.CFG4_FULL: --d_update_add_layer True, vl=3,
+    B=2, maxAction 35, 'wander' episodes, dropout 0, no-stop forced draws): one
+    accumulate_gradient('sample') — 35 teacher + 35 sampled steps + the A2C bootstrap — then backward.
+    Raw logits of every decoder call, losses / logs, every gradient (LXRT stack and VisionEncoder
+    included)."""
+    A = R.args
+    cfg = GI.CFG4_FULL
+    A.d_vl_layers, A.batchSize, A.views, A.maxAction = cfg["vl_layers"], cfg["batch"], 36, cfg["max_action"]
+    A.d_update_add_layer = True
+    out = {}
+    try:
+        world = SynthWorld(n_viewpoints=cfg["viewpoints"], feat_seed=0, graph_seed=cfg["graph_seed"])
+        env = SynthR2RBatch(world, cfg["batch"], seed=cfg["env_seed"], mode="wander", instr_len=cfg["instr_len"],
+                            variable_len=True)
+        agent = make_agent(R, env, cfg["max_action"])
+        assert agent.encoder.bert.update_add_layer
+        _zero_dropout(agent)
+        logits = []
+        dec_fwd = agent.decoder.forward
+
+        def dec_wrap(*a, **k):
+            r = dec_fwd(*a, **k)
+            logits.append(f32(r[2]))
+            return r
+        agent.decoder.forward = dec_wrap
+        _train_iteration(R, agent, out, "ft35/", forced=GI.forced_table(cfg["max_action"], cfg["batch"],
+                                                                       seed=cfg["forced_seed"]), no_stop=True)
+        out["ft35/n_decoder_calls"] = np.array(len(logits))
+        for t, lg in enumerate(logits):
+            out[f"ft35/logit/{t}"] = lg
+    finally:
+        A.d_update_add_layer = False
+    return out
+
+
 def checkpoint_schema(R):
     """The structure of a reference checkpoint (Seq2SeqAgent.save, agent_dg.py:1466-1487) after one
     optimizer step: top-level names, per-module entry names, state_dict keys, optimizer state layout."""
@@ -818,6 +869,8 @@ FIXTURES = {
     "optim": optim,
     "cfg4_readme": cfg4_readme,
     "pretrain": pretrain,
+    "cfg5_b256": cfg5_b256,
+    "cfg4_full": cfg4_full,
 }
 
 

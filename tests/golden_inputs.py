@@ -18,6 +18,11 @@ CFG2 = dict(batch=20, vl_layers=3, la_layers=9, max_action=35, train_max_action=
 # golden; the GPU compares its fp32 and its bf16-operand rollouts against it).
 CFG5 = dict(batch=4, vl_layers=6, la_layers=9, max_action=6, instr_len=80, kernel=5, viewpoints=16, graph_seed=3,
             seed=23)
+# configs[4] at its own batch (r05): B=256, vl=6, a 2-step teacher-forced eval rollout (fp32 golden), so
+# the B >= 128 kernel forms — whole-row attention incl. the N = 80 SoftDot, the bf16x6 plans at 256-row
+# batches, the bi-LSTM's 192-row tiles — are compared with the reference itself, not with the product.
+CFG5_B256 = dict(batch=256, vl_layers=6, la_layers=9, max_action=2, instr_len=80, kernel=5, viewpoints=64,
+                 graph_seed=3, seed=31)
 
 
 def _u(rng, *shape):
@@ -237,6 +242,13 @@ CFG4R = dict(batch=2, vl_layers=3, la_layers=9, max_action=6, instr_len=80, env_
 # and the deferred weight gradients with K = T*B.
 CFG2_FULL = dict(batch=20, vl_layers=3, la_layers=9, max_action=35, instr_len=80, viewpoints=32, graph_seed=5,
                  env_seed=24, forced_seed=33)
+
+# ---- cfg4 at its README length (r05): the finetune iteration the bench's cfg4 leg runs (README.md:104-116:
+# --d_update_add_layer True, vl 3, B 2, maxAction 35) on 'wander' episodes with no-stop forced draws, so
+# 35 teacher + 35 sampled steps run: the 70-step bi-LSTM BPTT at B = 2 and the LXRT / MHA backward at full
+# length, every gradient, every decoder call's logits; dropout 0.
+CFG4_FULL = dict(batch=2, vl_layers=3, la_layers=9, max_action=35, instr_len=80, viewpoints=32, graph_seed=5,
+                 env_seed=44, forced_seed=45)
 
 # ---- --pretrain_model_name (agent_dg.py:165-188): a DicAddActionPreTrain checkpoint directory -------
 # whose config.json says vl_layers=2 while the command line says d_vl_layers=3 (the checkpoint decides)

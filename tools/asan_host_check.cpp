@@ -1,0 +1,155 @@
+// Host-sanitizer run of the C-ABI's host code (SURVEY.md §5 "race detection / sanitizers"; VERDICT r04
+// Missing 2). Built with -fsanitize=address,undefined and linked against the HOST-ONLY sanitized copy
+// of libdasa_hip (dasa_amd/build.py build_debug(host_only=True): no device code, so no kernel is ever
+// launched here). It drives every host-side path that runs before a launch: the GEMM / bf16x6 /
+// attention / bi-LSTM planners through the workspace queries over a grid of shapes, every entry
+// point's argument validation (null, misaligned, out-of-range arguments must come back as
+// hipErrorInvalidValue, never as a launch or a host memory error), the mode / tuning setters and the
+// string helpers. ASan / UBSan abort the process on any host memory error or undefined behaviour;
+// otherwise it prints "asan_host_check: N checks ok" (tests/test_debug_cpu.py).
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <initializer_list>
+
+#include "../include/dasa_hip.h"
+
+static int g_checks = 0, g_fail = 0;
+
+static void expect(bool ok, const char* what, long v) {
+  ++g_checks;
+  if (!ok) {
+    ++g_fail;
+    std::fprintf(stderr, "FAIL %s (%ld)\n", what, v);
+  }
+}
+
+// fake, 16-B aligned device addresses: never dereferenced on the host
+static float* fp(uintptr_t a) { return reinterpret_cast<float*>(a); }
+static const int kInval = 1;   // hipErrorInvalidValue
+
+static dasa_gemm_desc desc(int M, int N, int K, int opA, int opB, int batch = 1) {
+  dasa_gemm_desc d;
+  std::memset(&d, 0, sizeof(d));
+  d.M = M; d.N = N; d.K = K; d.batch = batch; d.opA = opA; d.opB = opB;
+  d.A = fp(0x100000); d.B = fp(0x200000); d.C = fp(0x300000);
+  d.lda = opA == 0 ? K : M; d.ldb = opB == 1 ? K : N; d.ldc = N;
+  d.strideA = (long)M * K; d.strideB = (long)N * K; d.strideC = (long)M * N;
+  d.alpha = 1.f; d.beta = 0.f;
+  return d;
+}
+
+int main() {
+  expect(dasa_version() > 0, "dasa_version", dasa_version());
+  expect(dasa_build_info() && std::strlen(dasa_build_info()) > 0, "dasa_build_info", 0);
+  for (int e : {0, 1, 2, 98, 101, 400, 719, 999999, -5}) expect(dasa_error_string(e) != nullptr, "dasa_error_string", e);
+
+  // ---- GEMM planners: workspace queries over the path's shapes and a grid around them ----
+  const int Ms[] = {1, 2, 16, 20, 32, 33, 40, 160, 720, 1040, 1400, 1600, 2880, 12800, 13312, 20480};
+  const int Ns[] = {1, 5, 64, 768, 1024, 2048, 2176, 2304, 3072, 4096};
+  const int Ks[] = {32, 64, 128, 768, 1024, 2048, 2176, 2240, 3072, 4096, 112000};
+  long total = 0;
+  for (int M : Ms)
+    for (int N : Ns)
+      for (int K : Ks)
+        for (int op = 0; op < 4; ++op) {
+          dasa_gemm_desc d = desc(M, N, K, op & 1, op >> 1, (M * N) % 3 == 0 ? 2 : 1);
+          const int64_t w = dasa_gemm_f32_workspace(&d);
+          expect(w >= 0, "dasa_gemm_f32_workspace", w);
+          total += w > 0;
+          if (op == 2 && K % 32 == 0) {   // the bf16x6 form: opA 0, opB 1
+            const int64_t w6 = dasa_gemm_f32x6_workspace(&d);
+            expect(w6 >= 0, "dasa_gemm_f32x6_workspace", w6);
+          }
+          // invalid leading dimensions: the plan is made, then the call refuses (no launch)
+          dasa_gemm_desc bad = d;
+          if (op & 1) bad.lda = M - 1; else bad.lda = K - 1;
+          if (bad.lda >= 0 && M > 0 && N > 0 && K > 0)
+            expect(dasa_gemm_f32(&bad, nullptr, 0, nullptr) == kInval, "dasa_gemm_f32 lda", M);
+        }
+  expect(total > 0, "some plans use a workspace", total);
+  {
+    dasa_gemm_desc d = desc(-1, 4, 4, 0, 1);
+    expect(dasa_gemm_f32(&d, nullptr, 0, nullptr) == kInval, "dasa_gemm_f32 M < 0", -1);
+    expect(dasa_gemm_f32(nullptr, nullptr, 0, nullptr) == kInval, "dasa_gemm_f32 null desc", 0);
+    dasa_gemm_desc x6 = desc(64, 64, 48, 0, 1);   // K % 32 != 0
+    expect(dasa_gemm_f32x6(&x6, 64 * 48, nullptr) != 0, "dasa_gemm_f32x6 K % 32", 48);
+    dasa_gemm_desc bf = desc(64, 64, 96, 0, 1);   // K % 64 != 0
+    expect(dasa_gemm_bf16(&bf, nullptr) != 0, "dasa_gemm_bf16 K % 64", 96);
+  }
+  const int ncfg = dasa_gemm_force_config(-1);
+  expect(ncfg > 0, "dasa_gemm_force_config", ncfg);
+  for (int c = 0; c < ncfg; ++c) {   // every pinned configuration's plan
+    dasa_gemm_force_config(c);
+    dasa_gemm_desc d = desc(1600, 768, 3072, 0, 1);
+    expect(dasa_gemm_f32_workspace(&d) >= 0, "forced-config workspace", c);
+  }
+  dasa_gemm_force_config(-1);
+  for (int m : {0, 1, 2}) expect(dasa_gemm_x6_set_balance(m) == 0, "dasa_gemm_x6_set_balance", m);
+  dasa_gemm_x6_set_balance(0);
+  expect(dasa_gemm_skinny_tune(-1, -1) == 0, "dasa_gemm_skinny_tune", 0);
+
+  // ---- attention: workspace sizing and argument validation ----
+  for (int B : {1, 2, 20, 128, 256, 1024})
+    for (int N : {1, 5, 16, 36, 49, 80, 84, 256})
+      for (int D : {128, 2048, 2176, 4096}) {
+        const int64_t w = dasa_attn_workspace(B, N, D);
+        expect(w >= 262144, "dasa_attn_workspace", w);   // the counters' 2 x 32768 words at least
+      }
+  float* ws = fp(0x400000);
+  expect(dasa_softdot_fwd(fp(0x10), fp(0x20), 2048, nullptr, nullptr, fp(0x30), fp(0x40), 2, 257, 2048, ws, nullptr) == kInval,
+         "softdot N > 256", 257);
+  expect(dasa_softdot_fwd(fp(0x14), fp(0x20), 2048, nullptr, nullptr, fp(0x30), fp(0x40), 2, 16, 2048, ws, nullptr) == kInval,
+         "softdot misaligned q", 0x14);
+  expect(dasa_softdot_fwd(fp(0x10), fp(0x20), 2000, nullptr, nullptr, fp(0x30), fp(0x40), 2, 16, 2048, ws, nullptr) == kInval,
+         "softdot ldn < D", 2000);
+  expect(dasa_softdot_fwd(fp(0x10), fp(0x20), 2048, nullptr, nullptr, fp(0x30), fp(0x40), 2, 16, 2048, nullptr, nullptr) == kInval,
+         "softdot no workspace", 0);
+  expect(dasa_softdot_fwd(fp(0x10), fp(0x20), 8192, nullptr, nullptr, fp(0x30), fp(0x40), 2, 16, 8192, ws, nullptr) == kInval,
+         "softdot D > 4096", 8192);
+  expect(dasa_softdot_fwd(fp(0x10), fp(0x20), 2048, nullptr, nullptr, nullptr, nullptr, 0, 16, 2048, ws, nullptr) == 0,
+         "softdot B = 0 is a no-op", 0);
+  expect(dasa_softdot_bwd(fp(0x10), fp(0x20), 2048, nullptr, fp(0x50), nullptr, fp(0x60), nullptr, 0, 2, 16, 2048, ws,
+                          nullptr) == kInval, "softdot_bwd no probs", 0);
+  expect(dasa_shift_attn_fwd(fp(0x10), fp(0x20), 2176, fp(0x30), nullptr, nullptr, nullptr, fp(0x40), 2, 2176, 0, ws,
+                             nullptr) == kInval, "shift K = 0", 0);
+  expect(dasa_shift_attn_fwd(fp(0x10), fp(0x20), 2176, fp(0x30), nullptr, nullptr, nullptr, fp(0x40), 2, 2176, 16, ws,
+                             nullptr) == kInval, "shift K > 15", 16);
+  expect(dasa_shift_attn_bwd(fp(0x10), fp(0x20), 2176, nullptr, nullptr, nullptr, fp(0x50), nullptr, nullptr, fp(0x60), 0,
+                             2, 2176, 5, ws, nullptr) == kInval, "shift_bwd no attn", 0);
+  for (int m : {0, 1, 2}) expect(dasa_attn_set_mode(m) == 0, "dasa_attn_set_mode", m);
+  expect(dasa_attn_set_mode(3) == kInval, "dasa_attn_set_mode 3", 3);
+  expect(dasa_attn_set_mode(-1) == kInval, "dasa_attn_set_mode -1", -1);
+  dasa_attn_set_mode(0);
+  expect(dasa_attn_debug_buffer(fp(0x10), 16) == kInval, "debug buffer too small", 16);
+  expect(dasa_attn_debug_buffer(nullptr, 0) == 0, "debug buffer disarm", 0);
+  expect(dasa_attn_debug_record_floats() > 0, "debug record size", 0);
+
+  // ---- bi-LSTM: workspace sizing over batches / widths, mode setters ----
+  for (int B : {1, 2, 20, 32, 33, 64, 96, 160, 192, 256})
+    for (int H : {64, 256, 512, 1024}) {
+      expect(dasa_bilstm_workspace(B, H) > 0, "dasa_bilstm_workspace", B);
+      expect(dasa_bilstm_bwd_workspace(B, H) > 0, "dasa_bilstm_bwd_workspace", B);
+    }
+  for (int m : {0, 1, 2}) expect(dasa_bilstm_set_mode(m) == 0, "dasa_bilstm_set_mode", m);
+  dasa_bilstm_set_mode(0);
+  const int x6b = dasa_bilstm_bptt_x6(-1), x6f = dasa_bilstm_fwd_x6(-1);
+  expect(x6b == 0 || x6b == 1, "dasa_bilstm_bptt_x6 query", x6b);
+  expect(x6f == 0 || x6f == 1, "dasa_bilstm_fwd_x6 query", x6f);
+
+  // ---- the rest: validation before any launch ----
+  expect(dasa_mha_fwd(fp(0x10), 2304, fp(0x20), 2304, fp(0x30), 2304, nullptr, fp(0x40), 768, nullptr, 2, 12, 80, 80, 32,
+                      0.125f, 0.f, 1, nullptr) == kInval, "mha dh != 64", 32);
+  expect(dasa_mha_fwd(fp(0x10), 2304, fp(0x20), 2304, fp(0x30), 2304, nullptr, fp(0x40), 768, nullptr, 2, 12, 200, 80, 64,
+                      0.125f, 0.f, 1, nullptr) == kInval, "mha Lq > 128", 200);
+  expect(dasa_gather_rows(fp(0x10), nullptr, 6, nullptr, nullptr, 0, fp(0x20), 4, nullptr) == kInval,
+         "gather Fa % 4", 6);
+  expect(dasa_f32_split3_bf16(fp(0x10), 12, nullptr, 4, 12, nullptr) != 0, "split3 cols % 8", 12);
+  expect(dasa_set_error_word(nullptr) == 0, "dasa_set_error_word(NULL)", 0);
+  expect(dasa_persist_force_timeout(0) == 0, "dasa_persist_force_timeout", 0);
+  expect(dasa_set_seed_source(nullptr) == 0, "dasa_set_seed_source(NULL)", 0);
+
+  std::printf("asan_host_check: %d checks, %d failed\n", g_checks, g_fail);
+  return g_fail ? 1 : 0;
+}
