@@ -14,6 +14,8 @@ from dasa_amd.kbench import _time_graph  # noqa: E402
 SHAPES = [(12800, 3072, 768), (12800, 2304, 768), (12800, 768, 3072), (12800, 768, 768), (1600, 3072, 768),
           (1600, 768, 3072), (720, 3072, 768), (720, 768, 3072), (1600, 4096, 768), (720, 2048, 2048),
           (1600, 768, 768), (720, 768, 768), (720, 1536, 768), (720, 2304, 768)]
+# tail-free shapes (whole rounds of 256 workgroups for 256 x 128 AND 128 x 128 tiles): the per-CU rate of a form
+SHAPES_ROUND = [(8192, 1024, 3072), (8192, 1024, 768), (8192, 2048, 768), (16384, 1024, 3072)]
 
 
 def main():
@@ -22,7 +24,10 @@ def main():
     if "--forms" in sys.argv:
         forms = [int(f) for f in sys.argv[sys.argv.index("--forms") + 1].split(",")]
     lib = _lib.lib()
-    for M, N, K in SHAPES:
+    shapes = SHAPES_ROUND + SHAPES if "--round" in sys.argv else SHAPES
+    if "--lang" in sys.argv:
+        shapes = [s for s in shapes if s[0] >= 8192]
+    for M, N, K in shapes:
         x = torch.randn(M, K, device=dev)
         W = torch.randn(N, K, device=dev) * 0.05
         b = torch.randn(N, device=dev)
