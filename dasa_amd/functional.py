@@ -2,10 +2,11 @@
 
 These are the differentiable building blocks of the reference-API modules in dasa_amd.r2r. Only
 the tensors a backward actually needs are saved, and nothing is saved when no input requires grad.
-Parameters are held as ctx attributes (ctx.params), not saved tensors: a captured training step
-(graph.AutogradGraphs) keeps its autograd graph across optimizer steps, whose in-place parameter
-updates would otherwise fail the saved-tensor version check; the backward reads the parameters as
-they are at backward time, which in every training loop here is before the optimizer step.
+Parameters are held as ctx attributes (ctx.params, a _Kept tuple), not saved tensors: a captured
+training step (graph.AutogradGraphs) keeps its autograd graph across optimizer steps, whose in-place
+parameter updates would otherwise fail the saved-tensor version check; the backward reads the parameters
+as they are at backward time, which in every training loop here is before the optimizer step. Outside a
+capture the same version check runs on first access in the backward (_Kept).
 """
 import contextlib
 
@@ -36,6 +37,37 @@ class _SeedStream:
 
 
 _SEEDS = _SeedStream()
+
+
+class _Kept(tuple):
+    """The parameters a backward reads (ctx.params), with the in-place guard save_for_backward would
+    give them: their _version at forward time is recorded (not inside a hipGraph capture — a captured
+    training step's backward legitimately runs after optimizer updates of the same storage), and the
+    first access in the backward raises if a parameter was modified in place since."""
+
+    def __new__(cls, params):
+        t = super().__new__(cls, params)
+        t._ver = None if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing() else \
+            tuple(None if q is None else q._version for q in params)
+        return t
+
+    def _check(self):
+        ver = self._ver
+        if ver is not None:
+            self._ver = None           # once per backward
+            for q, v in zip(tuple.__iter__(self), ver):
+                if q is not None and q._version != v:
+                    raise RuntimeError("one of the parameters needed for gradient computation has been modified "
+                                       f"by an inplace operation: {tuple(q.shape)} is at version {q._version}; "
+                                       f"expected version {v} (dasa_amd.functional)")
+
+    def __getitem__(self, i):
+        self._check()
+        return tuple.__getitem__(self, i)
+
+    def __iter__(self):
+        self._check()
+        return tuple.__iter__(self)
 
 
 def new_seed():
@@ -145,7 +177,7 @@ class LinearFn(torch.autograd.Function):
     def forward(ctx, x, W, b, act):
         ctx.act = act
         ctx.has_b = b is not None
-        ctx.params = (W, b)
+        ctx.params = _Kept((W, b))
         need = any(ctx.needs_input_grad)
         if need and act == "gelu":
             z = ops.linear(x, W, b)
@@ -324,7 +356,7 @@ class ShiftAttnFn(torch.autograd.Function):
         wctx, attn, shifted, wsm = ops.shift_attn_fwd(q, feat, z)
         if any(ctx.needs_input_grad):
             ctx.save_for_backward(h, feat, q, attn, shifted, wsm)
-            ctx.params = (W_in, W_s, b_s)
+            ctx.params = _Kept((W_in, W_s, b_s))
         ctx.mark_non_differentiable(attn)
         return wctx, attn
 
@@ -361,7 +393,7 @@ class SoftDotTildeFn(torch.autograd.Function):
         y = ops.linear(cat, W_out, act="tanh")
         if any(ctx.needs_input_grad):
             ctx.save_for_backward(h, c, q, probs, cat, y)
-            ctx.params = (W_in, W_out)
+            ctx.params = _Kept((W_in, W_out))
         ctx.mark_non_differentiable(probs)
         return y, probs
 
@@ -399,7 +431,7 @@ class SoftDotFn(torch.autograd.Function):
             scores = scores.masked_fill(mask.bool(), -float("inf"))
         if any(ctx.needs_input_grad):
             ctx.save_for_backward(h, c, q, probs, mask.bool() if mask is not None else None)
-            ctx.params = (W_in,)
+            ctx.params = _Kept((W_in,))
         ctx.want_scores = want_scores
         if not want_scores:
             ctx.mark_non_differentiable(probs)
@@ -432,7 +464,7 @@ class CandLogitFn(torch.autograd.Function):
         scores, _, _ = ops.softdot_fwd(q, cand, None, want_probs=False, want_wctx=False)
         if any(ctx.needs_input_grad):
             ctx.save_for_backward(h, cand, q, scores)
-            ctx.params = (W_in,)
+            ctx.params = _Kept((W_in,))
         return scores
 
     @staticmethod
@@ -499,7 +531,7 @@ class LSTMCellFn(torch.autograd.Function):
         h1, c1, act = ops.lstm_cell_fwd(gates, c, save=need)
         if need:
             ctx.save_for_backward(xcat, h, c, c1, act)
-            ctx.params = (W_ih, W_hh, b_ih, b_hh)
+            ctx.params = _Kept((W_ih, W_hh, b_ih, b_hh))
         ctx.E = E
         return h1, c1
 
@@ -632,7 +664,7 @@ class BiLSTMFn(torch.autograd.Function):
         out, h_n, c_n, saved = ops.bilstm_fwd(xproj, W_hh_f, W_hh_b, lengths_i32, H, save=need)
         if need:
             ctx.save_for_backward(x, lengths_i32, out, saved[0], saved[1], W_ih_f, W_hh_f, W_ih_b, W_hh_b)
-            ctx.params = (W_ih_f, W_hh_f, b_ih_f, b_hh_f, W_ih_b, W_hh_b, b_ih_b, b_hh_b)
+            ctx.params = _Kept((W_ih_f, W_hh_f, b_ih_f, b_hh_f, W_ih_b, W_hh_b, b_ih_b, b_hh_b))
         ctx.H = H
         return out, h_n, c_n
 

@@ -218,9 +218,9 @@ class AutogradGraphs:
         self.replays = 0
 
     def _param_key(self):
-        if self._params is None:
-            self._params = [p for m in self.modules for p in m.parameters()]
-        return tuple((id(p), p.data_ptr()) for p in self._params)
+        # walked every call (a few dozen parameters): a Parameter object replaced on a module
+        # (module.weight = nn.Parameter(...)) changes the key as well as a storage swap (p.data = ...)
+        return tuple((id(p), p.data_ptr()) for m in self.modules for p in m.parameters())
 
     def new_iteration(self):
         """Every slot replayed since the last call has had its backward (or will never get one)."""

@@ -197,6 +197,20 @@ def load_pretrained_bert(path, model_type="DicAddActionPreTrain"):
     return bert
 
 
+MAX_CANDIDATES = 255   # navigable viewpoints per observation (+ the stop row = 256 = the HIP kernels' C limit)
+
+
+def _check_candidates(obs):
+    """The candidate attention and the policy head take C <= 256 rows per decision (include/dasa_hip.h:
+    dasa_softdot_fwd N <= 256, dasa_policy_head_fwd C <= 256; R2R viewpoints have at most a few dozen
+    navigable neighbours). The reference's masked_fill + CrossEntropy + Categorical take any count, so a
+    larger candidate list is refused here, where the observation is read, with the limit named."""
+    n = max((len(ob["candidate"]) for ob in obs), default=0)
+    if n > MAX_CANDIDATES:
+        raise NotImplementedError(f"an observation has {n} navigable candidates; the MI355X path takes at most "
+                                  f"{MAX_CANDIDATES} (+ stop) per decision step")
+
+
 class Seq2SeqAgent(BaseAgent):
     """agent_dg.py:102-1510 (encoder_type 'Dic' — the DASA configuration)."""
 
@@ -293,7 +307,7 @@ class Seq2SeqAgent(BaseAgent):
         return (sorted_tensor.long().to(self.device), mask.bool().to(self.device), list(seq_lengths),
                 list(perm_idx), progresses)
 
-    def _fused_head(self, logit):
+    def _fused_head(self, logit):  # noqa: D401
         """Every decision step's loss / action stage is the one-kernel policy head (dasa_policy_head_fwd,
         C <= 256 candidates); --submit's visited candidates and the back-prediction head (--pred_back) are
         fed to it as an extra mask / a second teacher-mode call."""
@@ -360,6 +374,7 @@ class Seq2SeqAgent(BaseAgent):
 
     def get_input_feat(self, obs):
         """agent_dg.py:313-323; device-side gather when the env provides one."""
+        _check_candidates(obs)
         if hasattr(self.env, "device_input_feat"):
             return self.env.device_input_feat(obs, self.device)
         input_a_t = np.zeros((len(obs), args.angle_feat_size), np.float32)
@@ -621,7 +636,9 @@ class Seq2SeqAgent(BaseAgent):
             return h_t, c_t, logit, h1, ce, ent, lpa, act, back
         inputs = (e["a"], e["df"], e["cand"], h0, prev_h1, c0, e["ctx"], ctx_mask, cand_lens, target, forced)
         if self._train_graphs is None:
-            self._train_graphs = graph.AutogradGraphs([self.decoder])
+            # every module any captured region reads (teacher-forcing decoder steps AND the AdaIN + decoder
+            # regions of _adain_decode), so a re-assigned parameter of either re-captures
+            self._train_graphs = graph.AutogradGraphs([self.decoder, self.adaIn])
         B, C, F = e["cand"].shape
         L, H2 = e["ctx"].shape[1:]
         Cp, Lp = self._slot_pads(C, L)

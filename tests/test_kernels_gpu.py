@@ -25,6 +25,27 @@ def test_linear(dev, M, N, K):
     assert (y - ref).abs().max().item() < 1e-4 * max(1.0, ref.abs().max().item())
 
 
+def test_inplace_weight_update_between_forward_and_backward_raises(dev):
+    """Parameters ride in ctx.params (not save_for_backward); their version is still checked:
+    an in-place update between forward and backward raises like torch's saved-tensor check, while an
+    untouched weight gives the plain gradient."""
+    from dasa_amd import functional as DF
+    g = torch.Generator().manual_seed(5)
+    x = _rand(64, 96, g=g).to(dev).requires_grad_()
+    W = torch.nn.Parameter(_rand(32, 96, g=g, scale=0.1).to(dev))
+    b = torch.nn.Parameter(_rand(32, g=g).to(dev))
+    y = DF.linear(x, W, b, "tanh")
+    y.sum().backward()
+    ref = ((1 - torch.tanh(x.detach().double() @ W.detach().double().t() + b.detach().double()) ** 2).t()
+           @ x.detach().double())
+    assert (W.grad.double() - ref).abs().max().item() < 1e-4 * ref.abs().max().item()
+    y = DF.linear(x, W, b, "tanh")
+    with torch.no_grad():
+        W.mul_(0.5)                                   # in place, after the forward
+    with pytest.raises(RuntimeError, match="modified by an inplace operation"):
+        y.sum().backward()
+
+
 @pytest.mark.parametrize("M,N,K,opB", [(160, 768, 768, 1), (72, 768, 3072, 0), (100, 3072, 768, 1), (33, 70, 1000, 0)])
 def test_gemm_short_m_split(dev, M, N, K, opB):
     """The short-GEMM plan (33..192 rows, split-K over 32x64 tiles + the fixed-order reduce) with the fused
