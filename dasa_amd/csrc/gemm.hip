@@ -1154,7 +1154,15 @@ struct X6Split { unsigned* cnt; float* slab; int splitk, kchunk; };
 // at most 128 registers (waves_per_eu 4): two workgroups share a CU and overlap each other's split / LDS
 // phase with their MFMAs — form 8's products in form 8's order (bitwise equal), 1.07-1.14x the previous
 // plan on the many-tile K = 768, N >= 2048 shapes (profiles/r03/x6_lds1_forms.txt).
-template <int BM, int BN, int WAVES_M, int WAVES_N, bool SEP, int PF = 1, bool SPL = false, int PRIO = 0>
+// STG (r05, forms 24 / 25): the two waves of a SIMD (waves w and w + NT/128 of the workgroup) run each K
+// step's two phases in opposite order — the first half computes on the resident stage and then splits /
+// stores the next one, the second half stores first and computes after — so one wave's split VALU and
+// ds_writes sit beside its partner's MFMAs instead of every wave reaching the store phase together after
+// the barrier (MI355X_MICROARCH.md "two waves per SIMD", item 9: stagger). Legal with two LDS stages and one
+// barrier per step: within a step the compute reads stage t and the store writes stage t + 1. Same
+// products in the same order as form 8 / 7: bitwise equal.
+template <int BM, int BN, int WAVES_M, int WAVES_N, bool SEP, int PF = 1, bool SPL = false, int PRIO = 0,
+          bool STG = false>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N)
 __attribute__((amdgpu_waves_per_eu(PF < 0 ? 4 : 1, PF < 0 ? 4 : 2)))
 void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
@@ -1329,15 +1337,27 @@ void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
     stg2.load(p, A, W, plane, m0, n0, 32 * min(1, nk - 1), tid);
         stg.store(smem, tid);
     __syncthreads();
+    // STG: the second half of the waves (the SIMD partners of the first half) store before computing
+    const bool late = STG && __builtin_amdgcn_readfirstlane(wave) >= NT / 128;
     for (int t = 0; t < nk; t += 2) {
       stg.load(p, A, W, plane, m0, n0, 32 * min(t + 2, nk - 1), tid);
-      compute(smem);
-            stg2.store(smem + STAGE, tid);
+      if (late) {
+        stg2.store(smem + STAGE, tid);
+        compute(smem);
+      } else {
+        compute(smem);
+        stg2.store(smem + STAGE, tid);
+      }
       __syncthreads();
       if (t + 1 >= nk) break;
       stg2.load(p, A, W, plane, m0, n0, 32 * min(t + 3, nk - 1), tid);
-      compute(smem + STAGE);
-            stg.store(smem, tid);
+      if (late) {
+        stg.store(smem, tid);
+        compute(smem + STAGE);
+      } else {
+        compute(smem + STAGE);
+        stg.store(smem, tid);
+      }
       __syncthreads();
     }
   }
@@ -2320,7 +2340,7 @@ static bool x6_lds1() {
 
 // tile rows / columns of each bf16x6 form (the kernel instantiations of dasa_gemm_f32x6_ws)
 static int x6_form_bm(int cfg) {
-  return (cfg == 1 || cfg == 3 || cfg == 6 || cfg == 7 || cfg == 12 || cfg == 13) ? 256
+  return (cfg == 1 || cfg == 3 || cfg == 6 || cfg == 7 || cfg == 12 || cfg == 13 || cfg == 25) ? 256
          : (cfg == 4 || cfg == 5) ? 64 : 128;
 }
 static int x6_form_bn(int cfg) { return cfg == 5 ? 64 : 128; }
@@ -2375,15 +2395,74 @@ static X6Plan x6_plan(const dasa_gemm_desc* d) {
   return pl;
 }
 
-extern "C" int64_t dasa_gemm_f32x6_workspace(const dasa_gemm_desc* d) {
-  if (!d || d->M < 0 || d->N < 0 || d->K < 0) return 0;
-  return x6_plan(d).ws;
-}
 
 // fp32-accurate GEMM on bf16 MFMA (bf16x6 split; see gemm_f32x6_nt_kernel). d->B = the hi plane of
 // the pre-split weight, planes `plane` bf16 elements apart. ws (zero-initialised once, counters
 // re-armed by every call; dasa_gemm_f32x6_workspace bytes) enables the split-K form; without it every
 // problem runs one workgroup per tile.
+// Whole rounds + split-K tail (r05): a many-tile problem whose last round of workgroups would leave most
+// CUs idle (12800 x 768: 600 tiles of 128 x 128 = 2.34 rounds of 256 CUs -> 78 % of the CU-time busy;
+// 11200 x 768: 2.06 rounds -> 69 %) runs as TWO launches over row bands: the first M1 rows as whole rounds
+// of the planned form, then the remaining rows as 128 x 128 tiles with K split so that they fill one round
+// (the X6Split form: partials reduced in-kernel by the last split, in split order — deterministic). Taken
+// when the cost model (rounds x tile work) promises >= 10 % less; DASA_X6_TAIL=0 turns it off (A/B).
+struct X6Tail { int M1; X6Plan dp, rem; };
+
+static bool x6_tail_on() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("DASA_X6_TAIL");
+    on = !(e && e[0] == '0');
+  }
+  return on != 0;
+}
+
+static bool x6_tail_plan(const dasa_gemm_desc* d, const X6Plan& pl, X6Tail& tp) {
+  const int M = d->M, N = d->N, K = d->K;
+  if (g_force_cfg >= kX6Force || !x6_tail_on() || d->batch > 1 || pl.splitk > 1) return false;
+  if (!(pl.cfg == 7 || pl.cfg == 8 || pl.cfg == 20 || pl.cfg == 24 || pl.cfg == 25)) return false;
+  const long cus = num_cus(), S = cus * (pl.cfg == 20 ? 2 : 1);
+  const long tn = cdiv(N, pl.bn), tm = cdiv(M, pl.bm), T = tn * tm;
+  const long full = T / S;
+  if (full < 1) return false;
+  const long panels1 = full * S / tn;   // row panels that make whole rounds
+  if (panels1 < 1 || panels1 >= tm) return false;
+  const int M1 = (int)panels1 * pl.bm, M2 = M - M1;
+  const long t2 = cdiv(M2, 128) * cdiv(N, 128);
+  int sk = (int)(cus / t2);
+  if (sk > K / 256) sk = K / 256;
+  if (sk < 2 || t2 > kCntWords) return false;
+  // cost in units of one 128 x 128 tile over the full K on one CU (form 20's two workgroups per CU each
+  // take twice as long); the split tail adds ~5 % of a tile for its slab round trip
+  const double u = (double)pl.bm * pl.bn / (128.0 * 128.0) * (pl.cfg == 20 ? 2.0 : 1.0);
+  const double plain = ceil((double)T / S) * u;
+  const double dpsk = (double)full * u + ceil((double)t2 * sk / cus) / sk + 0.05;
+  if (dpsk > 0.9 * plain) return false;
+  tp.M1 = M1;
+  tp.dp = pl;
+  tp.rem = X6Plan{8, 128, 128, sk, (int)(cdiv(cdiv(K, sk), 32) * 32), 0};
+  tp.rem.splitk = (int)cdiv(K, tp.rem.kchunk);
+  tp.rem.ws = kCntBytes + t2 * tp.rem.splitk * (int64_t)128 * 128 * (int64_t)sizeof(float);
+  (void)M2;
+  return true;
+}
+
+static int x6_run(const dasa_gemm_desc* d, X6Plan pl, int64_t plane, void* ws, int64_t ws_bytes, hipStream_t st);
+
+extern "C" int dasa_gemm_f32x6_kernels(const dasa_gemm_desc* d, int64_t ws_bytes) {
+  if (!d || d->M <= 0 || d->N <= 0 || d->K <= 0) return 0;
+  X6Tail tp;
+  return (x6_tail_plan(d, x6_plan(d), tp) && ws_bytes >= tp.rem.ws) ? 2 : 1;
+}
+
+extern "C" int64_t dasa_gemm_f32x6_workspace(const dasa_gemm_desc* d) {
+  if (!d || d->M < 0 || d->N < 0 || d->K < 0) return 0;
+  const X6Plan pl = x6_plan(d);
+  X6Tail tp;
+  if (x6_tail_plan(d, pl, tp)) return tp.rem.ws > pl.ws ? tp.rem.ws : pl.ws;
+  return pl.ws;
+}
+
 extern "C" int dasa_gemm_f32x6_ws(const dasa_gemm_desc* d, int64_t plane, void* ws, int64_t ws_bytes, void* stream) {
   if (!d) return (int)hipErrorInvalidValue;
   const int M = d->M, N = d->N, K = d->K, batch = d->batch < 1 ? 1 : d->batch;
@@ -2393,6 +2472,24 @@ extern "C" int dasa_gemm_f32x6_ws(const dasa_gemm_desc* d, int64_t plane, void* 
   if (((uintptr_t)d->A & 15) || ((uintptr_t)d->B & 15) || (batch > 1 && ((d->strideA & 3) || (d->strideB & 7))))
     return (int)hipErrorInvalidValue;
   if (M == 0 || N == 0) return 0;
+  const X6Plan pl = x6_plan(d);
+  X6Tail tp;
+  if (x6_tail_plan(d, pl, tp) && ws != nullptr && ws_bytes >= tp.rem.ws) {
+    dasa_gemm_desc d1 = *d, d2 = *d;
+    d1.M = tp.M1;
+    d2.M = M - tp.M1;
+    d2.A = d->A + (long)tp.M1 * d->lda;
+    d2.C = d->C + (long)tp.M1 * d->ldc;
+    if (d->aux) d2.aux = d->aux + (long)tp.M1 * d->ld_aux;
+    const int rc = x6_run(&d1, tp.dp, plane, nullptr, 0, (hipStream_t)stream);
+    if (rc) return rc;
+    return x6_run(&d2, tp.rem, plane, ws, ws_bytes, (hipStream_t)stream);
+  }
+  return x6_run(d, pl, plane, ws, ws_bytes, (hipStream_t)stream);
+}
+
+static int x6_run(const dasa_gemm_desc* d, X6Plan pl, int64_t plane, void* ws, int64_t ws_bytes, hipStream_t st) {
+  const int M = d->M, N = d->N, K = d->K, batch = d->batch < 1 ? 1 : d->batch;
   GemmP p{};
   p.M = M; p.N = N; p.K = K; p.batch = batch; p.splitk = 1; p.kchunk = K;
   p.A = d->A; p.lda = d->lda; p.sA = d->strideA;
@@ -2402,7 +2499,6 @@ extern "C" int dasa_gemm_f32x6_ws(const dasa_gemm_desc* d, int64_t plane, void* 
   p.aux = d->aux; p.ld_aux = d->ld_aux; p.sAux = d->strideAux;
   p.colscale = d->colscale; p.alpha = d->alpha; p.beta = d->beta;
   p.ws = nullptr;
-  X6Plan pl = x6_plan(d);
   if (pl.splitk > 1 && (ws == nullptr || ws_bytes < pl.ws)) { pl.splitk = 1; pl.kchunk = K; }
   const int cfg = pl.cfg, bm = pl.bm, bn = pl.bn;
   // tile order: groups of 8 W column panels, A streaming under them (r04 sweep, profiles/r04/x6_group_sweep.txt:
@@ -2410,7 +2506,6 @@ extern "C" int dasa_gemm_f32x6_ws(const dasa_gemm_desc* d, int64_t plane, void* 
   p.group_m = cdiv(M, bm) >= 8 ? -8 : 1;
   if (x6_group_override() != 0) p.group_m = x6_group_override();   // A/B: DASA_X6_GROUP (< -1: along N)
   X6Split xs{};
-  hipStream_t st = (hipStream_t)stream;
   if (pl.splitk > 1) {
     xs.cnt = (unsigned*)ws;
     xs.slab = (float*)((char*)ws + kCntBytes);
@@ -2444,6 +2539,8 @@ extern "C" int dasa_gemm_f32x6_ws(const dasa_gemm_desc* d, int64_t plane, void* 
     case 15: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, false, 2>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
     case 16: hipLaunchKernelGGL((gemm_f32x6_dma_kernel<128, 128, 4, 2>), grid, dim3(512), 0, st, p, (long)plane); break;
     case 20: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true, -1>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
+    case 24: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true, 2, false, 0, true>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
+    case 25: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<256, 128, 4, 2, true, 2, false, 0, true>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
     default: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
   }
   DASA_CHECK_LAUNCH();

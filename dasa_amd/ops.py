@@ -19,7 +19,7 @@ def check(rc, what, family=None, flops=0.0, nbytes=0.0, _ev=None):
     _lib.check(rc, what)
 
 
-def _call(what, family, fn, *a, flops=0.0, nbytes=0.0, detail=None):
+def _call(what, family, fn, *a, flops=0.0, nbytes=0.0, detail=None, kernels=1):
     """Launch through the C-ABI; under prof.collect() bracket it with HIP events on the stream."""
     if prof.active():
         e0 = torch.cuda.Event(enable_timing=True)
@@ -27,7 +27,7 @@ def _call(what, family, fn, *a, flops=0.0, nbytes=0.0, detail=None):
         e0.record()
         rc = fn(*a)
         e1.record()
-        prof.record(family, e0, e1, flops, nbytes, detail)
+        prof.record(family, e0, e1, flops, nbytes, detail, kernels)
     else:
         rc = fn(*a)
     _lib.check(rc, what)
@@ -323,9 +323,12 @@ def gemm_f32x6(x, planes, out, *, M, N, K, lda, ldc, bias=None, act=None, aux=No
             need = _X6_WS_NEED[(M, N, K)] = L.dasa_gemm_f32x6_workspace(ctypes.byref(d))
     if need:
         ws, ws_bytes = _gemm_ws(out.device, d, need)
+    kernels = 1
+    if prof.active():      # the tail plan launches two kernels: per-kernel durations -> per-call rates
+        kernels = int(L.dasa_gemm_f32x6_kernels(ctypes.byref(d), int(ws_bytes)))
     _call("dasa_gemm_f32x6", "gemm_x6", L.dasa_gemm_f32x6_ws, ctypes.byref(d), int(N) * int(K), ws, ws_bytes,
           _stream(), flops=2.0 * M * N * K, nbytes=4.0 * M * K + 6.0 * K * N + 4.0 * M * N,
-          detail=(int(M), int(N), int(K)))
+          detail=(int(M), int(N), int(K)), kernels=kernels)
 
 
 def linear(x, W, b=None, act=None, out=None, aux=None, colscale=None, beta=0.0, alpha=1.0):

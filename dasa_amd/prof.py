@@ -49,9 +49,9 @@ class _Recorder:
         """Per-family table + the dominant kernel's roofline. PMC values (HBM bytes, MFMA busy) are
         attached only from the committed rocprofv3 --pmc summary of THIS workload (PMC_FILES)."""
         torch.cuda.synchronize()
-        fam = defaultdict(lambda: {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0})
+        fam = defaultdict(lambda: {"launches": 0, "kernels": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0})
         shapes = defaultdict(lambda: [0, 0.0, 0.0])
-        for name, e0, e1, flops, nbytes, detail in self.items:
+        for name, e0, e1, flops, nbytes, detail, nk in self.items:
             f = fam[name]
             if detail is not None:
                 sh = shapes[(name,) + tuple(detail)]
@@ -59,6 +59,7 @@ class _Recorder:
                 sh[1] += e0.elapsed_time(e1)
                 sh[2] += flops
             f["launches"] += 1
+            f["kernels"] += nk
             f["ms"] += e0.elapsed_time(e1)
             f["flops"] += flops
             f["bytes"] += nbytes
@@ -83,7 +84,8 @@ class _Recorder:
         roof = {"kernel": dom_name, "bound": d["bound"], "achieved": d["achieved"], "peak": d["peak"],
                 "unit": d["unit"], "frac": d["frac"], "traffic": None,
                 "per_launch": {"avg_us": d["avg_launch_us"], "alg_flops": fam[dom_name]["flops"] / nl,
-                               "alg_bytes": fam[dom_name]["bytes"] / nl}}
+                               "alg_bytes": fam[dom_name]["bytes"] / nl,
+                               "kernels_per_call": round(fam[dom_name]["kernels"] / nl, 4)}}
         if dom_name == "gemm_x6":
             # fp32 work on bf16 matrix cores: `peak` is the bf16 dense peak / 6 (six bf16 MFMA products per
             # fp32 product), i.e. frac = the bf16 MFMA utilisation; against the fp32 MFMA peak the same
@@ -105,12 +107,14 @@ class _Recorder:
             # committed rocprofv3 --kernel-trace --stats summary of this workload. The line's achieved /
             # frac follow that summary (the judge's cross-check); the HIP-event figures of the bracketed
             # launches above — which run with less overlap, so faster per launch — stay beside them
-            ach_tp = roof["per_launch"]["alg_flops"] / (tp["avg_us"] * 1e-6) / 1e12
+            # rocprof averages per KERNEL; a call of the bf16x6 tail plan is two kernels
+            kpc = roof["per_launch"]["kernels_per_call"]
+            ach_tp = roof["per_launch"]["alg_flops"] / (tp["avg_us"] * kpc * 1e-6) / 1e12
             roof["hip_event"] = {"achieved": d["achieved"], "frac": d["frac"], "avg_us": d["avg_launch_us"],
                                  "note": "HIP events around each launch of one extra profiled iteration"}
             roof["achieved"] = round(ach_tp, 2)
             roof["frac"] = round(ach_tp / d["peak"], 4)
-            roof["per_launch"]["avg_us"] = tp["avg_us"]
+            roof["per_launch"]["avg_us"] = round(tp["avg_us"] * kpc, 2)
             roof["timed_path_rocprof"] = dict(tp, frac=roof["frac"])
             roof["source"] = ("achieved = algorithmic FLOPs per launch (HIP-event profile iteration) / the average "
                               "launch duration in the committed rocprofv3 --kernel-trace --stats summary of the timed "
@@ -185,8 +189,8 @@ def active():
     return _REC is not None
 
 
-def record(name, e0, e1, flops, nbytes, detail=None):
-    _REC.items.append((name, e0, e1, float(flops), float(nbytes), detail))
+def record(name, e0, e1, flops, nbytes, detail=None, kernels=1):
+    _REC.items.append((name, e0, e1, float(flops), float(nbytes), detail, int(kernels)))
 
 
 @contextlib.contextmanager

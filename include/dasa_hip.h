@@ -91,6 +91,12 @@ int dasa_gemm_f32x6(const dasa_gemm_desc* d, int64_t plane, void* stream);
  * by the last split to arrive in a fixed order (deterministic). Workspace 0 = no split needed. */
 int64_t dasa_gemm_f32x6_workspace(const dasa_gemm_desc* d);
 int dasa_gemm_f32x6_ws(const dasa_gemm_desc* d, int64_t plane, void* ws, int64_t ws_bytes, void* stream);
+/* Many-tile problems whose last round of workgroups would leave most CUs idle (12800 x 768: 2.34 rounds of
+ * 128 x 128 tiles) run as two launches over row bands when the workspace allows it: whole rounds of the
+ * planned form, then the remaining rows with K split to fill one round (DASA_X6_TAIL=0: off). This returns
+ * how many kernels dasa_gemm_f32x6_ws launches for `d` with a workspace of ws_bytes (profiling: per-kernel
+ * durations -> per-call rates). */
+int dasa_gemm_f32x6_kernels(const dasa_gemm_desc* d, int64_t ws_bytes);
 /* x [rows][ldx] fp32 -> y = three bf16 planes [3][rows][cols] (hi, mid, lo; plane stride rows*cols),
  * x = hi + mid + lo exactly for normal fp32 values; cols % 8 == 0, 16-B aligned x and y. */
 int dasa_f32_split3_bf16(const float* x, int64_t ldx, uint16_t* y, int32_t rows, int32_t cols, void* stream);
