@@ -114,7 +114,17 @@ __device__ __forceinline__ void lds_wave_sync() {
 constexpr int kDbgHdr = 4, kDbgMaxT = 1024;
 constexpr int kDbgRec = kDbgHdr + kDbgMaxT * 16 + kDbgMaxT + kMaxW * 16 + 16;
 
-template <int RB, bool DBG = false>
+//
+// Loads (r05): every row of the block is read by ONE buffer_load_dwordx4 with the same per-thread byte
+// offset VGPR (column t) and the row's offset in an SGPR (soffset), so no load's address lives in
+// registers that a younger load's data return overwrites. The r04 form (LEG = true: a 64-bit VGPR
+// address per row; the compiler reused the address registers of in-flight loads as the destinations of
+// younger ones, one even overlapping its own address) returned wrong data on lanes 48-63 of one row's
+// load in 10-60 % of calls while a bf16x6 form-20 GEMM started on another stream
+// (tools/rowsplit_diag.py, profiles/r05/rowsplit_diag_a.log: every bad workgroup's per-thread partials
+// already differ — the loads, not the reduction); the whole-row kernel, whose loads all share one offset
+// VGPR, never did. LEG stays for the diagnosis (dasa_attn_set_mode(3)).
+template <int RB, bool DBG = false, bool LEG = false>
 __device__ __forceinline__ float block_row_dots(const float* rows, long ldn, int nr, const float* vec, int D4,
                                                 float4 (&x)[RB], float (*red)[16], float* dbg = nullptr) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, W = blockDim.x >> 6;
@@ -124,8 +134,18 @@ __device__ __forceinline__ float block_row_dots(const float* rows, long ldn, int
   float qsum = 0.f;
   if (t < D4) {   // D4 <= blockDim: one float4 column per thread
     const float4 qv = reinterpret_cast<const float4*>(vec)[t];
+    if (LEG) {
 #pragma unroll
-    for (int i = 0; i < RB; ++i) x[i] = reinterpret_cast<const float4*>(rows + (long)min(i, nr - 1) * ldn)[t];
+      for (int i = 0; i < RB; ++i) x[i] = reinterpret_cast<const float4*>(rows + (long)min(i, nr - 1) * ldn)[t];
+    } else {
+      const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(rows), 0, 0x7fffffff,
+                                                                          0x00020000);
+      const int voff = t * 16;
+#pragma unroll
+      for (int i = 0; i < RB; ++i)
+        x[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                              rr, voff, __builtin_amdgcn_readfirstlane(min(i, nr - 1) * (int)ldn * 4), 0));
+    }
 #pragma unroll
     for (int i = 0; i < RB; ++i) v[i] = dot4(x[i], qv);
     if (DBG) qsum = (qv.x + qv.y) + (qv.z + qv.w);
@@ -186,7 +206,7 @@ struct FwdArgs {
   float* dbg;                                          // row-split diagnosis dump (DBG instantiation only)
 };
 
-template <int RB, bool DBG = false>
+template <int RB, bool DBG = false, bool LEG = false>
 __global__ __launch_bounds__(1024) void attn_fwd_kernel(FwdArgs a) {
   __shared__ float red[kMaxW][16];
   __shared__ float se[16], sep[16], sw[kMaxK + 1], ssc[kMaxBlk];
@@ -197,8 +217,8 @@ __global__ __launch_bounds__(1024) void attn_fwd_kernel(FwdArgs a) {
   const bool shift = a.shift_logits != nullptr;
   const float* rows = a.ctx + ((long)b * N + r0) * a.ldn;
   float4 x[RB];
-  const float s = block_row_dots<RB, DBG>(rows, a.ldn, nr, a.q + (long)b * a.D, D4, x, red,
-                                          DBG ? a.dbg + (long)(b * nblk + j) * kDbgRec : nullptr);
+  const float s = block_row_dots<RB, DBG, LEG>(rows, a.ldn, nr, a.q + (long)b * a.D, D4, x, red,
+                                               DBG ? a.dbg + (long)(b * nblk + j) * kDbgRec : nullptr);
   const bool combine = a.wctx || a.probs || a.shifted;
   const __amdgpu_buffer_rsrc_t wr = ws_rsrc(a.ws);
   if (t < 64) {
@@ -957,6 +977,8 @@ inline WsLayout ws_layout(void* ws, int B, int N, int D) {
   return L;
 }
 
+int g_attn_mode = -1;   // dasa_attn_set_mode: 0 automatic, 1 row-split only, 2 = 0 + the two-launch
+                        // D-split forward for SoftDot too (tests); -1 = not read from the env yet
 float* g_attn_dbg = nullptr;   // dasa_attn_debug_buffer: the next row-split forward dumps here
 int64_t g_attn_dbg_bytes = 0;
 
@@ -965,12 +987,16 @@ int launch_fwd(FwdArgs a, int B, void* ws, hipStream_t st) {
   a.nblk = (a.N + RB - 1) / RB;
   WsLayout L = ws_layout(ws, B, a.N, a.D);
   a.cnt = L.cnt1; a.ws = (float*)ws; a.o_part = L.o_part; a.o_ml = L.o_ml; a.o_ee = L.o_ee;
+  const dim3 grid(a.nblk, B), block(block_threads(a.D));
+  const bool leg = g_attn_mode == 3;   // diagnosis: the r04 per-row-address loads
   if (g_attn_dbg && (int64_t)a.nblk * B * kDbgRec * 4 <= g_attn_dbg_bytes) {
     a.dbg = g_attn_dbg;
     g_attn_dbg = nullptr;   // one launch per armed buffer
-    hipLaunchKernelGGL((attn_fwd_kernel<RB, true>), dim3(a.nblk, B), dim3(block_threads(a.D)), 0, st, a);
+    if (leg) hipLaunchKernelGGL((attn_fwd_kernel<RB, true, true>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((attn_fwd_kernel<RB, true>), grid, block, 0, st, a);
   } else {
-    hipLaunchKernelGGL(attn_fwd_kernel<RB>, dim3(a.nblk, B), dim3(block_threads(a.D)), 0, st, a);
+    if (leg) hipLaunchKernelGGL((attn_fwd_kernel<RB, false, true>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL(attn_fwd_kernel<RB>, grid, block, 0, st, a);
   }
   DASA_CHECK_LAUNCH();
   return 0;
@@ -994,15 +1020,13 @@ int launch_bwd(BwdArgs a, int B, void* ws, hipStream_t st) {
 
 // D-split eligibility (0 = use the row-split kernels): rows per thread for N <= 80, D a multiple of 128,
 // and B x G within kSplitMaxWG when the call needs the group barrier. DASA_ATTN_SPLIT=0 disables it.
-int g_attn_mode = -1;   // dasa_attn_set_mode: 0 automatic, 1 row-split only, 2 = 0 + the two-launch
-                        // D-split forward for SoftDot too (tests); -1 = not read from the env yet
 
 int split_rpt(int B, int N, int D, bool spin) {
   if (g_attn_mode < 0) {
     const char* e = getenv("DASA_ATTN_SPLIT");
     g_attn_mode = (e && e[0] == '0') ? 1 : 0;
   }
-  if (g_attn_mode == 1 || N < 1 || N > kSplitMaxN || D % (4 * kCW) != 0) return 0;
+  if (g_attn_mode == 1 || g_attn_mode == 3 || N < 1 || N > kSplitMaxN || D % (4 * kCW) != 0) return 0;
   if (spin && (long)B * (D / (4 * kCW)) > kSplitMaxWG) return 0;
   return N <= 16 ? 2 : (N <= 40 ? 5 : 10);
 }
@@ -1020,7 +1044,7 @@ constexpr int kRowsMinB = 128;
 bool rows_ok(int B, int N, int D, bool shift = true) {
   if (g_attn_mode < 0) split_rpt(1, 1, 128, false);   // reads DASA_ATTN_SPLIT once
   // the shift attention's rings need N <= 36; SoftDot takes up to seven 12-row slices (N <= 84)
-  return g_attn_mode != 1 && B >= kRowsMinB && N >= 1 && N <= (shift ? 36 : 84) && D <= 4 * 576;
+  return g_attn_mode != 1 && g_attn_mode != 3 && B >= kRowsMinB && N >= 1 && N <= (shift ? 36 : 84) && D <= 4 * 576;
 }
 
 int launch_rows(const FwdArgs& a, int B, hipStream_t st) {
@@ -1057,7 +1081,8 @@ int launch_split_bwd(SplitArgs a, int rpt, int B, void* ws, hipStream_t st) {
 // batches), N <= 80, D a multiple of 128 (G <= 32 chunks).
 bool split2_ok(int B, int N, int D) {
   if (g_attn_mode < 0) split_rpt(1, 1, 128, false);
-  return g_attn_mode != 1 && B < kRowsMinB && N >= 1 && N <= kSplitMaxN && D % (4 * kCW) == 0 && D <= 4 * kCW * 32;
+  return g_attn_mode != 1 && g_attn_mode != 3 && B < kRowsMinB && N >= 1 && N <= kSplitMaxN && D % (4 * kCW) == 0 &&
+         D <= 4 * kCW * 32;
 }
 
 template <int RPT>
@@ -1090,7 +1115,7 @@ bool bad_common(const float* q, const float* ctx, int64_t ldn, int B, int N, int
 }  // namespace
 
 extern "C" int dasa_attn_set_mode(int32_t mode) {
-  if (mode < 0 || mode > 2) return (int)hipErrorInvalidValue;
+  if (mode < 0 || mode > 3) return (int)hipErrorInvalidValue;
   g_attn_mode = mode;
   return 0;
 }
@@ -1117,7 +1142,7 @@ extern "C" int dasa_softdot_fwd(const float* q, const float* ctx, int64_t ldn, c
   FwdArgs a{q, ctx, (long)ldn, mask, nullptr, 0, scores, probs, nullptr, nullptr, wctx, N, D};
   if (g_attn_mode < 0) split_rpt(1, 1, 128, false);   // reads DASA_ATTN_SPLIT once
   if ((probs || wctx) && rows_ok(B, N, D, false)) return launch_rows(a, B, (hipStream_t)stream);
-  if (!probs && !wctx && scores && g_attn_mode != 1 && D <= 4 * 1024) {   // scores only (every B: see below)
+  if (!probs && !wctx && scores && g_attn_mode != 1 && g_attn_mode != 3 && D <= 4 * 1024) {   // scores only (every B: see below)
     hipLaunchKernelGGL(attn_dot_rows_kernel, dim3(N, B), dim3(256), 0, (hipStream_t)stream, q, ctx, (long)ldn,
                        scores, N, D);
     DASA_CHECK_LAUNCH();
@@ -1129,7 +1154,7 @@ extern "C" int dasa_softdot_fwd(const float* q, const float* ctx, int64_t ldn, c
   // profiles/r04/attn_rowsplit_concurrency.txt); every other kernel of the step, the D-split and
   // whole-row forms included, stayed bitwise reproducible under the same load. It is left for mode 1
   // (tests) and for shapes no other form takes (N > 80 or D % 128 != 0).
-  if (g_attn_mode != 1 && N <= kSplitMaxN && D % (4 * kCW) == 0 && D <= 4 * kCW * 32)
+  if (g_attn_mode != 1 && g_attn_mode != 3 && N <= kSplitMaxN && D % (4 * kCW) == 0 && D <= 4 * kCW * 32)
     return launch_split2_fwd(a, B, ws, (hipStream_t)stream);
   return launch_fwd<16>(a, B, ws, (hipStream_t)stream);
 }

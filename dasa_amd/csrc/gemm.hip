@@ -1154,15 +1154,7 @@ struct X6Split { unsigned* cnt; float* slab; int splitk, kchunk; };
 // at most 128 registers (waves_per_eu 4): two workgroups share a CU and overlap each other's split / LDS
 // phase with their MFMAs — form 8's products in form 8's order (bitwise equal), 1.07-1.14x the previous
 // plan on the many-tile K = 768, N >= 2048 shapes (profiles/r03/x6_lds1_forms.txt).
-// STG (r05, forms 24 / 25): the two waves of a SIMD (waves w and w + NT/128 of the workgroup) run each K
-// step's two phases in opposite order — the first half computes on the resident stage and then splits /
-// stores the next one, the second half stores first and computes after — so one wave's split VALU and
-// ds_writes sit beside its partner's MFMAs instead of every wave reaching the store phase together after
-// the barrier (MI355X_MICROARCH.md "two waves per SIMD", item 9: stagger). Legal with two LDS stages and one
-// barrier per step: within a step the compute reads stage t and the store writes stage t + 1. Same
-// products in the same order as form 8 / 7: bitwise equal.
-template <int BM, int BN, int WAVES_M, int WAVES_N, bool SEP, int PF = 1, bool SPL = false, int PRIO = 0,
-          bool STG = false>
+template <int BM, int BN, int WAVES_M, int WAVES_N, bool SEP, int PF = 1, bool SPL = false, int PRIO = 0>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N)
 __attribute__((amdgpu_waves_per_eu(PF < 0 ? 4 : 1, PF < 0 ? 4 : 2)))
 void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
@@ -1337,27 +1329,15 @@ void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
     stg2.load(p, A, W, plane, m0, n0, 32 * min(1, nk - 1), tid);
         stg.store(smem, tid);
     __syncthreads();
-    // STG: the second half of the waves (the SIMD partners of the first half) store before computing
-    const bool late = STG && __builtin_amdgcn_readfirstlane(wave) >= NT / 128;
     for (int t = 0; t < nk; t += 2) {
       stg.load(p, A, W, plane, m0, n0, 32 * min(t + 2, nk - 1), tid);
-      if (late) {
-        stg2.store(smem + STAGE, tid);
-        compute(smem);
-      } else {
-        compute(smem);
-        stg2.store(smem + STAGE, tid);
-      }
+      compute(smem);
+            stg2.store(smem + STAGE, tid);
       __syncthreads();
       if (t + 1 >= nk) break;
       stg2.load(p, A, W, plane, m0, n0, 32 * min(t + 3, nk - 1), tid);
-      if (late) {
-        stg.store(smem, tid);
-        compute(smem + STAGE);
-      } else {
-        compute(smem + STAGE);
-        stg.store(smem, tid);
-      }
+      compute(smem + STAGE);
+            stg.store(smem, tid);
       __syncthreads();
     }
   }
@@ -2340,7 +2320,7 @@ static bool x6_lds1() {
 
 // tile rows / columns of each bf16x6 form (the kernel instantiations of dasa_gemm_f32x6_ws)
 static int x6_form_bm(int cfg) {
-  return (cfg == 1 || cfg == 3 || cfg == 6 || cfg == 7 || cfg == 12 || cfg == 13 || cfg == 25) ? 256
+  return (cfg == 1 || cfg == 3 || cfg == 6 || cfg == 7 || cfg == 12 || cfg == 13) ? 256
          : (cfg == 4 || cfg == 5) ? 64 : 128;
 }
 static int x6_form_bn(int cfg) { return cfg == 5 ? 64 : 128; }
@@ -2420,7 +2400,7 @@ static bool x6_tail_on() {
 static bool x6_tail_plan(const dasa_gemm_desc* d, const X6Plan& pl, X6Tail& tp) {
   const int M = d->M, N = d->N, K = d->K;
   if (g_force_cfg >= kX6Force || !x6_tail_on() || d->batch > 1 || pl.splitk > 1) return false;
-  if (!(pl.cfg == 7 || pl.cfg == 8 || pl.cfg == 20 || pl.cfg == 24 || pl.cfg == 25)) return false;
+  if (!(pl.cfg == 7 || pl.cfg == 8 || pl.cfg == 20)) return false;
   const long cus = num_cus(), S = cus * (pl.cfg == 20 ? 2 : 1);
   const long tn = cdiv(N, pl.bn), tm = cdiv(M, pl.bm), T = tn * tm;
   const long full = T / S;
@@ -2539,8 +2519,6 @@ static int x6_run(const dasa_gemm_desc* d, X6Plan pl, int64_t plane, void* ws, i
     case 15: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, false, 2>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
     case 16: hipLaunchKernelGGL((gemm_f32x6_dma_kernel<128, 128, 4, 2>), grid, dim3(512), 0, st, p, (long)plane); break;
     case 20: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true, -1>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
-    case 24: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true, 2, false, 0, true>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
-    case 25: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<256, 128, 4, 2, true, 2, false, 0, true>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
     default: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
   }
   DASA_CHECK_LAUNCH();

@@ -156,7 +156,8 @@ int dasa_mha_bwd(const float* Q, int64_t ldq, const float* K, int64_t ldk, const
  * the whole-row form does not take (r04: the row-split kernel is not reproducible beside bf16x6
  * form-20 GEMMs on another stream; it remains for mode 1 and for shapes no other form takes).
  * dasa_attn_set_mode: 0 = automatic (the default; DASA_ATTN_SPLIT=0 in the environment starts in
- * mode 1), 1 = row-split only, 2 = the same as 0 (kept for callers of r03). Host-only setting.      */
+ * mode 1), 1 = row-split only, 2 = the same as 0 (kept for callers of r03), 3 = row-split only with
+ * the r04 per-row-address loads (diagnosis, tools/rowsplit_diag.py). Host-only setting.            */
 int64_t dasa_attn_workspace(int32_t B, int32_t N, int32_t D);
 int dasa_attn_set_mode(int32_t mode);
 /* Diagnosis hook (r05, tools/rowsplit_diag.py): arm a device buffer of `bytes` (16-B aligned) that the

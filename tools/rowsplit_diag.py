@@ -11,7 +11,8 @@ with the quiet call on the same input:
   shuffle  every v equal, a wave partial differs: the ds_bpermute reduce-scatter;
   lds      every wave partial equal, the row dot differs: the LDS write / barrier / read;
   merge    the row dot equal, an output differs: the cross-workgroup merge.
-    python tools/rowsplit_diag.py [iters] [period] [side: x6|nobg]"""
+    python tools/rowsplit_diag.py [iters] [period] [side: x6|nobg] [mode: 1 = row-split (r05 loads) | 3 = the
+    r04 per-row-address loads]"""
 import collections
 import os
 import sys
@@ -34,6 +35,7 @@ def main():
     iters = int(sys.argv[1]) if len(sys.argv) > 1 else 200
     period = int(sys.argv[2]) if len(sys.argv) > 2 else 4
     side = sys.argv[3] if len(sys.argv) > 3 else "x6"
+    mode = int(sys.argv[4]) if len(sys.argv) > 4 else 1
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
     B, N, D = 20, 80, 2048
@@ -44,7 +46,7 @@ def main():
     Abg, Wbg = torch.randn(12800, 768, device=dev), torch.randn(3072, 768, device=dev) * 0.02
     ybg = torch.empty(12800, 3072, device=dev)
     bg = torch.cuda.Stream()
-    ops.attn_set_mode(1)                       # row-split kernel only
+    ops.attn_set_mode(mode)                    # row-split kernel only (3: with the r04 loads)
     rec = ops.attn_debug_buffer(None)
     nblk = (N + 15) // 16
     T = D // 4
@@ -75,6 +77,7 @@ def main():
     ops.attn_set_mode(0)
 
     stages = collections.Counter()
+    lanes, rowsc, match = collections.Counter(), collections.Counter(), collections.Counter()
     bad_calls = 0
     bad_hw, all_hw = collections.Counter(), collections.Counter()
     shown = 0
@@ -105,6 +108,23 @@ def main():
             redr = rv[HDR + MAXT * 17:HDR + MAXT * 17 + MAXW * 16].view(MAXW, 16)[:T // 64]
             tot, totr = dv[-16:], rv[-16:]
             vbad = torch.nonzero(~torch.eq(v, vr)).tolist()
+            for t, r in vbad:
+                lanes[t % 64] += 1
+                rowsc[r] += 1
+                # whose data did the load return? the quiet partial of another row of this thread, or of
+                # the same row of another thread (+-16 / 32 / 48 lanes), or nothing seen in the quiet call
+                got = v[t, r].item()
+                who = "none"
+                for r2 in range(16):
+                    if r2 != r and vr[t, r2].item() == got:
+                        who = f"row{r2 - r:+d}"
+                        break
+                else:
+                    for dt in (-48, -32, -16, 16, 32, 48, -64, 64):
+                        if 0 <= t + dt < T and vr[t + dt, r].item() == got:
+                            who = f"lane{dt:+d}"
+                            break
+                match[who] += 1
             qbad = torch.nonzero(~torch.eq(qsum, qref)).flatten().tolist()
             rbad = torch.nonzero(~torch.eq(red, redr)).tolist()
             tbad = torch.nonzero(~torch.eq(tot, totr)).flatten().tolist()
@@ -135,8 +155,11 @@ def main():
                 for r in tbad[:4]:
                     print(f"    tot[{r}] got {tot[r].item():.7g} quiet {totr[r].item():.7g} "
                           f"sum(dumped red) {red[:, r].double().sum().item():.7g}", flush=True)
-    print(f"side={side} period={period}: bad calls {bad_calls}/{iters}; bad workgroups by stage {dict(stages)}")
+    print(f"mode={mode} side={side} period={period}: bad calls {bad_calls}/{iters}; bad workgroups by stage {dict(stages)}")
     print(f"bad workgroups by (xcc, se, cu): {dict(bad_hw.most_common(12))}")
+    print(f"bad partials by lane within the wave: {dict(sorted(lanes.items()))}")
+    print(f"bad partials by row of the block: {dict(sorted(rowsc.items()))}")
+    print(f"a bad partial equals the quiet partial of: {dict(match.most_common(10))}")
     print(f"distinct (xcc, se, cu) over all workgroups: {len(all_hw)}")
 
 
