@@ -11,6 +11,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # DASA_DEBUG=1: the debug library (device input checks compiled in; dasa_amd/build.py --debug)
 LIB_PATH = os.path.join(_HERE, "libdasa_hip_debug.so" if os.environ.get("DASA_DEBUG", "0") not in ("", "0")
                         else "libdasa_hip.so")
+# DASA_LIB=<path>: an alternate build of the same sources (A/B diagnosis builds, e.g. tools/build_variant.sh)
+LIB_PATH = os.environ.get("DASA_LIB") or LIB_PATH
 
 f32p = C.c_void_p  # device pointers travel as integers
 i64 = C.c_int64
