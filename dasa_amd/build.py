@@ -15,7 +15,16 @@ OUT = os.path.join(HERE, "libdasa_hip.so")
 BUILD_DIR = os.path.join(HERE, "build")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
+# -fno-slp-vectorize -fno-vectorize and the packed-fp32-ops target feature off (device; the host compile ignores
+# it with a warning): no packed-FP32 VALU (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32) anywhere. r05 traced the
+# r04 row-split attention failure to them: with an MFMA-dense bf16x6 GEMM workgroup starting on the same CU,
+# the LOW half of a packed result came back wrong on lanes 48-63 (profiles/r05/rowsplit_diag_b_m*.log: every
+# bad partial is an even row of a compiler-packed row pair, lanes 48-63); built without them the same stress
+# has 0 bad calls in 200 for either load form and every hand-off kernel stays bitwise reproducible
+# (rowsplit_diag_c_noslp_m*.log, stress_c_noslp_all_mode1.log), at equal iteration time (bench_c_*.log).
+# tests/test_host_cpu.py::test_no_packed_fp32 scans the built library's device code for them.
 FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-pass-failed", "-Wno-inline-asm",
+         "-fno-slp-vectorize", "-fno-vectorize", "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops",
          "-I" + os.path.join(os.path.dirname(HERE), "include")]
 
 
@@ -36,7 +45,8 @@ SAN = ["-Xarch_host", "-fsanitize=address,undefined", "-Xarch_host", "-fno-omit-
        "-Xarch_host", "-fno-sanitize-recover=undefined"]
 _INC = ["-I" + os.path.join(os.path.dirname(HERE), "include")]
 DEBUG_FLAGS = ["-O3", "-Xarch_host", "-O1", "-g", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}",
-               "-Wno-pass-failed", "-Wno-inline-asm", "-DDASA_DEBUG=1"] + _INC
+               "-Wno-pass-failed", "-Wno-inline-asm", "-fno-slp-vectorize", "-fno-vectorize", "-Xclang", "-target-feature", "-Xclang",
+               "-packed-fp32-ops", "-DDASA_DEBUG=1"] + _INC
 HOSTSAN_FLAGS = ["-O1", "-g", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "--cuda-host-only",
                  "-Wno-pass-failed", "-Wno-inline-asm", "-DDASA_DEBUG=1"] + _INC + SAN
 HOSTSAN_OUT = os.path.join(BUILD_DIR, "hostsan", "libdasa_hip_hostsan.so")

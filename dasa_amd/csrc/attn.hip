@@ -824,8 +824,8 @@ __global__ __launch_bounds__(256) void attn_split_bwd_kernel(SplitArgs a) {
 //             also writes scores / probs / shifted / the tap weights.
 // Measured (profiles/r03/attn_forms_b.txt, B = 20): shift attention 8.55 us vs 8.89 for the row-split
 // kernel's in-launch merge, so the shift forward takes it; the instruction SoftDot (N = 80) ran 12.1 vs
-// 10.8 us on it, and r04 moved it here as well (dasa_softdot_fwd: the row-split kernel is not reproducible
-// beside bf16x6 form-20 GEMMs on another stream).
+// 10.8 us on it and stays there (r04 moved it here while the row-split kernel was not reproducible beside
+// bf16x6 form-20 GEMMs; r05 found and removed the cause: dasa_softdot_fwd).
 template <int RPT>
 __global__ __launch_bounds__(256) void attn_split_dots_kernel(SplitArgs a) {
   const int g = blockIdx.x, b = blockIdx.y, t = threadIdx.x, col = t & 31, rl = t >> 5;
@@ -1148,13 +1148,14 @@ extern "C" int dasa_softdot_fwd(const float* q, const float* ctx, int64_t ldn, c
     DASA_CHECK_LAUNCH();
     return 0;
   }
-  // Every B the whole-row form does not take: the two-launch D-split form. The row-split kernel
-  // (attn_fwd_kernel, 1.2 us faster per call at B = 20) returned wrong row dots in 10-50 % of calls, at
-  // B = 20 and at B = 256, while bf16x6 form-20 GEMMs ran on another stream (tools/determinism_stress.py,
-  // profiles/r04/attn_rowsplit_concurrency.txt); every other kernel of the step, the D-split and
-  // whole-row forms included, stayed bitwise reproducible under the same load. It is left for mode 1
-  // (tests) and for shapes no other form takes (N > 80 or D % 128 != 0).
-  if (g_attn_mode != 1 && g_attn_mode != 3 && N <= kSplitMaxN && D % (4 * kCW) == 0 && D <= 4 * kCW * 32)
+  // Every B the whole-row form does not take: the row-split kernel (1.2-1.3 us faster per call than the
+  // two-launch D-split form at B = 20, profiles/r03/attn_forms_b.txt); mode 2 takes the D-split form. r04
+  // routed SoftDot away from the row-split kernel because it returned wrong row dots beside starting bf16x6
+  // form-20 GEMMs; r05 found the cause — packed-FP32 VALU results (the compiler's v_pk_fma_f32 row pairs)
+  // corrupted on lanes 48-63 beside a starting MFMA-dense workgroup — and builds every kernel without packed
+  // FP32 (dasa_amd/build.py), after which the kernel is bitwise reproducible under the same stress
+  // (profiles/r05/rowsplit_diag_c_noslp_m1.log, stress_c_noslp_all_mode1.log).
+  if (g_attn_mode == 2 && N <= kSplitMaxN && D % (4 * kCW) == 0 && D <= 4 * kCW * 32)
     return launch_split2_fwd(a, B, ws, (hipStream_t)stream);
   return launch_fwd<16>(a, B, ws, (hipStream_t)stream);
 }

@@ -152,11 +152,12 @@ int dasa_mha_bwd(const float* Q, int64_t ldq, const float* K, int64_t ldk, const
  * meet at a bounded group barrier; a timeout NaN-poisons the outputs and ORs 4 into the error word,
  * dasa_set_error_word); shift-attention forward with B < 128: two-launch D-split (row-dot partials,
  * then softmax + context per column chunk); candidate scores (no probs / wctx): one workgroup per
- * row at every B; SoftDot with probs / wctx (N <= 80, D % 128 == 0) on the two-launch form at every B
- * the whole-row form does not take (r04: the row-split kernel is not reproducible beside bf16x6
- * form-20 GEMMs on another stream; it remains for mode 1 and for shapes no other form takes).
+ * row at every B; SoftDot with probs / wctx at every B the whole-row form does not take: row-split
+ * (mode 2: the two-launch D-split form for N <= 80, D % 128 == 0). Every kernel is built without
+ * packed-FP32 VALU (r05: their results were corrupted beside starting MFMA-dense workgroups of another
+ * kernel, the r04 row-split failure), and every form is bitwise reproducible under that load.
  * dasa_attn_set_mode: 0 = automatic (the default; DASA_ATTN_SPLIT=0 in the environment starts in
- * mode 1), 1 = row-split only, 2 = the same as 0 (kept for callers of r03), 3 = row-split only with
+ * mode 1), 1 = row-split only, 2 = 0 with the D-split SoftDot forward, 3 = row-split only with
  * the r04 per-row-address loads (diagnosis, tools/rowsplit_diag.py). Host-only setting.            */
 int64_t dasa_attn_workspace(int32_t B, int32_t N, int32_t D);
 int dasa_attn_set_mode(int32_t mode);

@@ -28,6 +28,31 @@ def test_library_exports_every_declared_symbol():
     assert L.dasa_version() >= 1 and b"gfx950" in L.dasa_build_info()
 
 
+def test_no_packed_fp32(tmp_path):
+    """No device kernel of the built library uses packed-FP32 VALU (v_pk_fma/mul/add_f32): r05 traced the
+    r04 row-split attention corruption to their results beside a starting MFMA-dense GEMM workgroup
+    (dasa_amd/build.py FLAGS, -fno-slp-vectorize). Disassembles every gfx950 code object of the .so."""
+    import shutil
+    import subprocess
+    objdump = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    if not os.path.exists(objdump):
+        pytest.skip("llvm-objdump not available")
+    from dasa_amd import _lib
+    lib = os.path.join(tmp_path, "lib.so")
+    shutil.copy(_lib.LIB_PATH, lib)
+    subprocess.run([objdump, "--offloading", lib], cwd=tmp_path, capture_output=True, check=True)
+    objs = sorted(f for f in os.listdir(tmp_path) if f.endswith("gfx950"))
+    assert len(objs) >= 7, objs          # one code object per source
+    found = {}
+    for f in objs:
+        r = subprocess.run([objdump, "-d", "--mcpu=gfx950", os.path.join(tmp_path, f)], capture_output=True, text=True,
+                           check=True)
+        n = len(re.findall(r"\bv_pk_(?:fma|mul|add)_f32\b", r.stdout))
+        if n:
+            found[f] = n
+    assert not found, found
+
+
 def test_gemm_workspace_query_is_host_only():
     """dasa_gemm_f32_workspace plans split-K without touching the device."""
     import ctypes

@@ -8,7 +8,7 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 B=$ROOT/dasa_amd/build
 OUT=$ROOT/dasa_amd/variant_$NAME
 mkdir -p $OUT
-FLAGS="-O3 -fPIC -std=c++17 --offload-arch=gfx950 -Wno-pass-failed -Wno-inline-asm -I$ROOT/include"
+FLAGS="-O3 -fPIC -std=c++17 --offload-arch=gfx950 -Wno-pass-failed -Wno-inline-asm -fno-slp-vectorize -fno-vectorize -Xclang -target-feature -Xclang -packed-fp32-ops -I$ROOT/include"
 /opt/rocm/bin/hipcc $FLAGS "$@" -c $ROOT/dasa_amd/csrc/$SRC -o $OUT/$SRC.o
 OBJS=""
 for o in $B/*.hip.o; do
