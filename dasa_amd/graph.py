@@ -18,7 +18,9 @@ the static output buffers (the bi-LSTM that consumes them keeps its input for th
 and the next replay overwrites the static buffers). A captured region is re-captured when any
 parameter of the modules it reads changes (data pointer or in-place version), e.g. after load_state_dict.
 """
+import contextlib
 import ctypes
+import gc
 import os
 
 import torch
@@ -30,6 +32,21 @@ from . import debug as _debug
 # DASA_CHECK_FINITE (dasa_amd/debug.py) synchronises after every op: no capture / replay then
 ENABLED = os.environ.get("DASA_GRAPH", "1") != "0" and not _debug.active()
 _NESTED = [0]    # > 0 while an enclosing region is being warmed up / captured: inner regions run inline
+
+
+@contextlib.contextmanager
+def _no_gc():
+    """No Python garbage collection while a stream is being captured: a collection there runs finalizers of
+    unrelated garbage (an earlier rollout's events or graphs in a reference cycle) whose HIP calls are not
+    permitted during a global-mode capture — the process aborted that way once in r05 (an MHA launch of the
+    VL-stack capture, `tests_r05d.log`). torch.cuda.graph collects once before the capture begins."""
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
 
 
 def capturing():
@@ -85,7 +102,7 @@ class StepGraphs:
             ctr = ctypes.c_void_p(self.counter.data_ptr())
             L.dasa_set_seed_source(ctr)
             try:
-                with torch.cuda.graph(g, stream=self.stream), torch.no_grad():
+                with _no_gc(), torch.cuda.graph(g, stream=self.stream), torch.no_grad():
                     _lib.check(L.dasa_seed_bump(ctr, ctypes.c_void_p(self.stream.cuda_stream)),
                                "dasa_seed_bump")
                     out = fn(*static_in)
@@ -262,7 +279,7 @@ class AutogradGraphs:
             ctr = ctypes.c_void_p(slot.counter.data_ptr())
             L.dasa_set_seed_source(ctr)
             try:
-                with torch.cuda.graph(g, pool=self.pool, stream=self.stream), torch.enable_grad():
+                with _no_gc(), torch.cuda.graph(g, pool=self.pool, stream=self.stream), torch.enable_grad():
                     _lib.check(L.dasa_seed_bump(ctr, ctypes.c_void_p(self.stream.cuda_stream)), "dasa_seed_bump")
                     out = fn(*static_in)
             finally:

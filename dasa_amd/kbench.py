@@ -28,7 +28,8 @@ def _time_graph(fn, reps=REPS):
     torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    from .graph import _no_gc
+    with _no_gc(), torch.cuda.graph(g):
         for _ in range(reps):
             fn()
     g.replay()
