@@ -9,6 +9,7 @@ as they are at backward time, which in every training loop here is before the op
 capture the same version check runs on first access in the backward (_Kept).
 """
 import contextlib
+import weakref
 
 import numpy as np
 import torch
@@ -123,9 +124,27 @@ def defer_weight_grads():
         _WG.active = prev
 
 
+# capture-time parameter aliases (graph.AutogradGraphs): id(alias) -> (weakref(alias), weakref(parameter)),
+# the parameter whose .grad the alias's gradients feed (weak both ways: a dead alias's id may be reused)
+_GRAD_OF = {}
+
+
+def set_grad_target(alias, p):
+    _GRAD_OF[id(alias)] = (weakref.ref(alias), weakref.ref(p))
+
+
+def grad_target(p):
+    e = _GRAD_OF.get(id(p))
+    if e is None or e[0]() is not p:
+        return p
+    q = e[1]()
+    return p if q is None else q
+
+
 def _wgrad(W, dz, x):
     """dW = dz^T x (both [rows, .]), or queued while weight gradients are deferred (returns None)."""
     if _WG.active:
+        W = grad_target(W)
         e = _WG.w.get(id(W))
         if e is None:
             e = _WG.w[id(W)] = [W, [], []]
@@ -138,6 +157,7 @@ def _wgrad(W, dz, x):
 def _bgrad(b, dz):
     """db = column sums of dz, or queued while weight gradients are deferred (returns None)."""
     if _WG.active:
+        b = grad_target(b)
         e = _WG.b.get(id(b))
         if e is None:
             e = _WG.b[id(b)] = [b, []]
@@ -574,10 +594,18 @@ class _BpttDeferral:
     BiLSTMFn.backward only queues its saved tensors and the incoming gradients; flush() then runs ONE
     recurrence over all queued sequences (B = steps x batch: an MFMA GEMM per timestep instead of 70
     latency-bound recurrences) and adds dW_ih / dW_hh / db into the parameters' .grad. Same sums as
-    the per-call backward, in a different order."""
+    the per-call backward, in a different order.
+
+    input_grads=True (r05; the finetune config, --d_update_add_layer True, where the LXRT output feeding the
+    bi-LSTM trains): the calls whose input needs a gradient are queued too — their backward returns no input
+    gradient, which stops the first backward pass at the bi-LSTM input — and flush() computes every call's
+    dx from the same batched recurrence (dx = dgates_f W_ih_f + dgates_b W_ih_b over all queued rows) and
+    continues the backward from the queued inputs (torch.autograd.backward(inputs, dx)) through the LXRT /
+    VisionEncoder stacks. The first pass must retain its graph (the stopped branches run later)."""
 
     def __init__(self):
         self.active = False
+        self.dx = False
         self.items = []
 
 
@@ -585,16 +613,18 @@ _BPTT = _BpttDeferral()
 
 
 @contextlib.contextmanager
-def defer_bilstm_backward():
-    prev = _BPTT.active
+def defer_bilstm_backward(input_grads=False):
+    prev = (_BPTT.active, _BPTT.dx)
     _BPTT.active = True
+    _BPTT.dx = bool(input_grads)
     try:
         yield
     finally:
-        _BPTT.active = prev
+        _BPTT.active, _BPTT.dx = prev
 
 
 def _acc_grad(p, g):
+    p = grad_target(p)
     if p.grad is None:
         p.grad = g
     else:
@@ -602,14 +632,21 @@ def _acc_grad(p, g):
 
 
 def flush_bilstm_backward():
-    """Run the queued bi-LSTM backward passes (grouped by weights and shapes) into .grad."""
+    """Run the queued bi-LSTM backward passes (grouped by weights and shapes) into .grad; for calls queued
+    with their input gradient (input_grads mode) continue the backward from their inputs."""
     items, _BPTT.items = _BPTT.items, []
     groups = {}
     for it in items:
         key = (tuple(id(p) for p in it["params"]), tuple(it["x"].shape[1:]))
         groups.setdefault(key, []).append(it)
-    for grp in groups.values():
-        _batched_bptt(grp)
+    xs, dxs = [], []
+    with torch.no_grad():
+        for grp in groups.values():
+            for x, dx in _batched_bptt(grp):
+                xs.append(x)
+                dxs.append(dx)
+    if xs:
+        torch.autograd.backward(xs, dxs)
 
 
 def _batched_bptt(grp):
@@ -631,10 +668,18 @@ def _batched_bptt(grp):
     dgates = ops.bilstm_bwd(W_hh_f, W_hh_b, lens, (sa, sc), dout, carry("dh_n"), carry("dc_n"), H)
     del sa, sc, dout
     hprev = ops.bilstm_hprev(torch.cat([it["out"] for it in grp], 0), H)    # [2][NB][L][H]
-    x2 = torch.cat([it["x"] for it in grp], 0).reshape(NB * L, E)
+    x2 = torch.cat([it["x"].detach() for it in grp], 0).reshape(NB * L, E)
+    want_dx = any(it["needs"][0] for it in grp)
+    dx = None
     for d, (iw, ihh, ibi, ibh) in enumerate(((2, 3, 4, 5), (6, 7, 8, 9))):
         dg = dgates[:, :, d, :]                                # [NB, L, 4H] rows of stride 8H
         P = grp[0]["params"]
+        if want_dx:                                            # dx = sum_d dgates_d . W_ih_d (all rows at once)
+            Wih = P[iw - 2]
+            if dx is None:
+                dx = ops.matmul_nn(dg, Wih)
+            else:
+                ops.matmul_nn(dg, Wih, out=dx, beta=1.0)
         if n[iw]:
             _acc_grad(P[iw - 2], ops.matmul_tn(dg, x2))
         if n[ihh]:
@@ -645,6 +690,16 @@ def _batched_bptt(grp):
                 _acc_grad(P[ibi - 2], db)
             if n[ibh]:
                 _acc_grad(P[ibh - 2], db.clone() if n[ibi] else db)
+    out = []
+    if dx is not None:
+        dx = dx.view(NB, L, E)
+        r = 0
+        for it in grp:
+            b = it["x"].shape[0]
+            if it["needs"][0]:
+                out.append((it["x"], dx[r:r + b]))
+            r += b
+    return out
 
 
 class BiLSTMFn(torch.autograd.Function):
@@ -674,7 +729,7 @@ class BiLSTMFn(torch.autograd.Function):
         H = ctx.H
         B, L, E = x.shape
         n = ctx.needs_input_grad
-        if _BPTT.active and not n[0]:
+        if _BPTT.active and (not n[0] or _BPTT.dx):
             _BPTT.items.append(dict(x=x, lens=lens, out=out, sa=sa, sc=sc, params=ctx.params, needs=n,
                                     dout=dout.contiguous() if dout is not None else None,
                                     dh_n=dh_n.contiguous() if dh_n is not None else None,

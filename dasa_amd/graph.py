@@ -146,7 +146,7 @@ class StepGraphs:
 
 # ------------------------------------------------------------------ training-mode (autograd) regions
 class _Slot:
-    __slots__ = ("graph", "static_in", "static_out", "counter", "pkey", "fills", "shapes")
+    __slots__ = ("graph", "static_in", "static_out", "counter", "pkey", "fills", "shapes", "leaves")
 
 
 def _lead(t, shape):
@@ -194,21 +194,51 @@ class _BridgeFn(torch.autograd.Function):
             if o is not None and o.requires_grad and g is not None:
                 outs.append(o)
                 grads.append(g)
-        if outs:
+        got = {}
+        if outs and slot.leaves:
             L = _lib.lib()
             L.dasa_set_seed_source(ctypes.c_void_p(slot.counter.data_ptr()))
             try:
-                torch.autograd.backward(outs, grads, retain_graph=True)
+                # autograd.grad over the recorded graph's leaves (static inputs + the capture's parameter
+                # aliases, AutogradGraphs._aliased): their gradients come back synced to the caller's
+                # stream and the parameters' are accumulated into the real parameters' .grad there
+                gl = torch.autograd.grad(outs, slot.leaves, grads, retain_graph=True, allow_unused=True)
             finally:
                 L.dasa_set_seed_source(None)
+            got = {id(v): g for v, g in zip(slot.leaves, gl) if g is not None}
+            statics = {id(s) for s in slot.static_in if s is not None}
+            from . import functional as DF
+            with torch.no_grad():
+                for v in slot.leaves:
+                    g = got.get(id(v))
+                    if g is None or id(v) in statics:
+                        continue
+                    v = DF.grad_target(v)
+                    if v.grad is None:
+                        v.grad = g
+                    else:
+                        v.grad.add_(g)
         res = []
         for s, shape in zip(slot.static_in, ctx.shapes):
-            g = None
-            if s is not None and s.requires_grad and s.grad is not None:
-                g = _lead(s.grad, shape)
-                s.grad = None
-            res.append(g)
+            g = got.get(id(s)) if s is not None and s.requires_grad else None
+            res.append(_lead(g, shape) if g is not None else None)
         return (None,) + tuple(res)
+
+
+def _graph_leaves(outs):
+    """Every leaf tensor (AccumulateGrad node) of the autograd graph behind `outs`."""
+    seen, leaves = set(), []
+    stack = [o.grad_fn for o in outs if o is not None and o.grad_fn is not None]
+    while stack:
+        n = stack.pop()
+        if n is None or n in seen:
+            continue
+        seen.add(n)
+        v = getattr(n, "variable", None)
+        if v is not None:
+            leaves.append(v)
+        stack.extend(f for f, _ in n.next_functions)
+    return leaves
 
 
 class AutogradGraphs:
@@ -231,6 +261,7 @@ class AutogradGraphs:
         self.uses = {}
         self.stream = None
         self.pool = None
+        self._alias = {}
         self.captures = 0
         self.replays = 0
 
@@ -238,6 +269,37 @@ class AutogradGraphs:
         # walked every call (a few dozen parameters): a Parameter object replaced on a module
         # (module.weight = nn.Parameter(...)) changes the key as well as a storage swap (p.data = ...)
         return tuple((id(p), p.data_ptr()) for m in self.modules for p in m.parameters())
+
+    @contextlib.contextmanager
+    def _aliased(self):
+        """The modules' trainable parameters replaced, while a region is warmed up and captured, by alias
+        leaves sharing their storage (replays read optimizer updates in place). The retained capture graph
+        then holds the aliases' gradient accumulators — created on the capture stream, where the recorded
+        backward produces their gradients — and not the parameters' own, which stay per-iteration nodes on
+        the stream of the parameters' eager uses. One accumulator node serving both streams is what torch
+        warns about (AccumulateGrad stream mismatch) and syncs the streams for. Gradients
+        of an alias reach its parameter's .grad (functional.grad_target)."""
+        from . import functional as DF
+        swapped = []
+        for m in self.modules:
+            for mod in m.modules():
+                for name, p in list(mod._parameters.items()):
+                    if p is None or not p.requires_grad:
+                        continue
+                    a = self._alias.get(id(p))
+                    if a is None or a.data_ptr() != p.data_ptr() or a.shape != p.shape:
+                        if a is not None:
+                            DF._GRAD_OF.pop(id(a), None)
+                        a = torch.nn.Parameter(p.data)
+                        self._alias[id(p)] = a
+                        DF.set_grad_target(a, p)
+                    mod._parameters[name] = a
+                    swapped.append((mod, name, p))
+        try:
+            yield
+        finally:
+            for mod, name, p in swapped:
+                mod._parameters[name] = p
 
     def new_iteration(self):
         """Every slot replayed since the last call has had its backward (or will never get one)."""
@@ -270,7 +332,7 @@ class AutogradGraphs:
         try:
             # warm-up on the capture stream (lazily built workspaces / caches outside the capture); its
             # autograd graph is dropped
-            with torch.cuda.stream(self.stream), torch.enable_grad():
+            with self._aliased(), torch.cuda.stream(self.stream), torch.enable_grad():
                 fn(*static_in)
             torch.cuda.current_stream().wait_stream(self.stream)
             torch.cuda.synchronize(dev)
@@ -279,7 +341,8 @@ class AutogradGraphs:
             ctr = ctypes.c_void_p(slot.counter.data_ptr())
             L.dasa_set_seed_source(ctr)
             try:
-                with _no_gc(), torch.cuda.graph(g, pool=self.pool, stream=self.stream), torch.enable_grad():
+                with self._aliased(), _no_gc(), torch.cuda.graph(g, pool=self.pool, stream=self.stream), \
+                        torch.enable_grad():
                     _lib.check(L.dasa_seed_bump(ctr, ctypes.c_void_p(self.stream.cuda_stream)), "dasa_seed_bump")
                     out = fn(*static_in)
             finally:
@@ -288,6 +351,7 @@ class AutogradGraphs:
             _NESTED[0] -= 1
             ops._FRESH_PLANES[0] -= 1
         slot.graph, slot.static_in, slot.static_out = g, static_in, tuple(out)
+        slot.leaves = _graph_leaves(slot.static_out)
         slot.pkey = self._param_key()
         self.captures += 1
         return slot
@@ -312,5 +376,9 @@ class AutogradGraphs:
         return _BridgeFn.apply(slot, *inputs)
 
     def clear(self):
+        from . import functional as DF
         self.slots.clear()
         self.uses.clear()
+        for a in self._alias.values():
+            DF._GRAD_OF.pop(id(a), None)
+        self._alias.clear()

@@ -96,7 +96,9 @@ class _Recorder:
         pmc = _pmc_traffic(pmc_workload)
         if pmc is not None and dom_name in pmc["families"]:
             pf = pmc["families"][dom_name]
-            roof["traffic"] = pf.get("hbm_bytes", pf.get("hbm_bytes_per_launch"))
+            # PMC bytes are per kernel dispatch; the roofline is per call (a bf16x6 tail-plan call is two)
+            tb = pf.get("hbm_bytes", pf.get("hbm_bytes_per_launch"))
+            roof["traffic"] = None if tb is None else tb * roof["per_launch"]["kernels_per_call"]
             if pf.get("mfma_busy") is not None:
                 roof["mfma_busy"] = round(pf["mfma_busy"], 4)
             roof["traffic_source"] = (pmc["file"] + ": " + pmc["source"] + " (a separate rocprofv3 --pmc run of the "

@@ -1055,10 +1055,16 @@ class Seq2SeqAgent(BaseAgent):
     def optim_step(self, **kwargs):
         """agent_dg.py:1389-1405 (+ data-parallel gradient all-reduce before clipping)."""
         # the encoder's per-step bi-LSTM BPTTs and the per-step decoder / critic weight gradients run
-        # batched after the backward pass (dasa_amd/functional.py)
-        with DF.defer_bilstm_backward(), DF.defer_weight_grads():
-            self.loss.backward()
-        DF.flush_bilstm_backward()
+        # batched after the backward pass (dasa_amd/functional.py). When the bi-LSTM's input trains (the
+        # language stack updates: --d_update_add_layer / --d_transformer_update, cfg4's finetune) its input
+        # gradients come from the batched recurrence too and the backward continues from there, so the
+        # first pass keeps its graph for that second one
+        bert = self.encoder.bert
+        dx = bool(getattr(bert, "update_add_layer", False) or getattr(bert, "update_lang_bert", False))
+        dx = dx and os.environ.get("DASA_BPTT_DX", "1") != "0"       # 0: the per-call BPTT there (A/B)
+        with DF.defer_bilstm_backward(input_grads=dx), DF.defer_weight_grads():
+            self.loss.backward(retain_graph=dx)
+            DF.flush_bilstm_backward()
         DF.flush_weight_grads()
         if self._train_graphs is not None:
             self._train_graphs.new_iteration()     # every replayed step has had its backward

@@ -459,6 +459,47 @@ def test_bilstm_bptt_x6_vs_native(dev, B, L):
     assert (dg6 - dgn).abs().max().item() < 2e-5 * scale
 
 
+@pytest.mark.parametrize("input_grads", [False, True])
+def test_bilstm_deferred_input_grads(dev, input_grads):
+    """defer_bilstm_backward(input_grads=True) (optim_step's path when the language stack trains, cfg4): three
+    bi-LSTM calls sharing weights, whose inputs come from one trainable tensor through different ops, run
+    their BPTT as one batched recurrence and continue the backward from the queued inputs; the input
+    tensor's and the weights' gradients equal the per-call backward's to fp32 re-association."""
+    from dasa_amd import functional as DF
+    torch.manual_seed(11)
+    H, E, L = 1024, 768, 12
+    lstm = torch.nn.LSTM(E, H, 1, batch_first=True, bidirectional=True).to(dev)
+    with torch.no_grad():
+        for p_ in lstm.parameters():
+            p_.uniform_(-0.05, 0.05)
+    params = [lstm.weight_ih_l0, lstm.weight_hh_l0, lstm.bias_ih_l0, lstm.bias_hh_l0, lstm.weight_ih_l0_reverse,
+              lstm.weight_hh_l0_reverse, lstm.bias_ih_l0_reverse, lstm.bias_hh_l0_reverse]
+    a = torch.randn(6, L, E, device=dev).requires_grad_()
+    gs = [torch.randn(6, L, 2 * H, device=dev) for _ in range(3)]
+    lens = torch.tensor([12, 12, 9, 7, 3, 1], dtype=torch.int32, device=dev)
+
+    def run(deferred):
+        for p_ in params + [a]:
+            p_.grad = None
+        xs = [a * 0.5, torch.tanh(a), a[:, :, torch.arange(E - 1, -1, -1, device=dev)] * 2.0]
+        loss = sum((DF.BiLSTMFn.apply(x.contiguous(), lens, *params)[0] * g).sum() for x, g in zip(xs, gs))
+        if deferred:
+            with DF.defer_bilstm_backward(input_grads=input_grads), DF.defer_weight_grads():
+                loss.backward(retain_graph=input_grads)
+                DF.flush_bilstm_backward()
+            DF.flush_weight_grads()
+        else:
+            loss.backward()
+        torch.cuda.synchronize()
+        return [p_.grad.clone() for p_ in params + [a]]
+
+    ref = run(False)
+    got = run(True)
+    for r, g in zip(ref, got):
+        assert torch.isfinite(g).all()
+        assert (g - r).abs().max().item() <= 2e-5 * max(1.0, r.abs().max().item())
+
+
 def _check_bilstm(dev, B, L):
     from dasa_amd import ops
     torch.manual_seed(B + L)

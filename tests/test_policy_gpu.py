@@ -335,10 +335,12 @@ def test_hoist_language_train(R, dev):
         param.args.hoist_language = False
 
 
-@pytest.mark.parametrize("deferred", [False, True])
+@pytest.mark.parametrize("deferred", [0, 1, 2])
 def test_finetune_train_iteration_grads(R, dev, monkeypatch, deferred):
     """cfg4 finetune path (--d_update_add_layer True): the LXRT stack and VisionEncoder are trained.
-    accumulate_gradient('sample') + backward with dropout 0 and argmax 'sampling' vs the reference."""
+    accumulate_gradient('sample') + backward with dropout 0 and argmax 'sampling' vs the reference.
+    deferred 1: batched weight gradients, per-call bi-LSTM BPTT (its input trains); 2: optim_step's path,
+    the bi-LSTM BPTTs batched with their input gradients and the backward continued from there."""
     from dasa_amd import functional as DF
     param = R[0]
     G = golden("cfg4_finetune")
@@ -363,9 +365,9 @@ def test_finetune_train_iteration_grads(R, dev, monkeypatch, deferred):
     assert abs(ag.logs["ml_loss"][1] - float(G["ft/ml_loss_sample"])) < 1e-3
     assert abs(ag.logs["normalized_rl_loss"][-1] - float(G["ft/rl_loss"])) < TOL
     if deferred:
-        with DF.defer_bilstm_backward(), DF.defer_weight_grads():
-            ag.loss.backward()
-        DF.flush_bilstm_backward()
+        with DF.defer_bilstm_backward(input_grads=deferred == 2), DF.defer_weight_grads():
+            ag.loss.backward(retain_graph=deferred == 2)
+            DF.flush_bilstm_backward()
         DF.flush_weight_grads()
     else:
         ag.loss.backward()

@@ -104,7 +104,10 @@ def _iteration(ag, it):
     return loss, list(ag.logs["entropy"][-4:]), grads
 
 
+@pytest.mark.filterwarnings("error:The AccumulateGrad node's stream does not match")
 def test_train_graph_matches_eager(dev, monkeypatch):
+    """... and without torch's AccumulateGrad stream-mismatch warning (the captured
+    backward feeding accumulators of another stream), here an error."""
     from dasa_amd.r2r import param
     param.readme_train(["--d_vl_layers", "3", "--batchSize", "20", "--maxAction", "4"])
     try:

@@ -50,6 +50,33 @@ def main(path, t_last_ms=None):
         print(f"  gaps {k:>7}: {hist[k][0]:6d}  total {hist[k][1] / 1e6:8.2f} ms")
     big = sorted(gaps, reverse=True)[:15]
     print("  largest gaps (ms):", " ".join(f"{g / 1e6:.2f}" for g in big))
+    # per stream: kernels, union of its kernel intervals; and how much of the window 0 / 1 / 2+ streams
+    # were running a kernel at once (the overlap the language pipe gets beside the rollout)
+    by_stream = defaultdict(list)
+    for r in rows:
+        by_stream[r[3]].append(r)
+    for sid, rs in sorted(by_stream.items(), key=lambda kv: -len(kv[1])):
+        b, _ = union_busy(sorted(rs))
+        tops = defaultdict(int)
+        for s_, e_, n_, _ in rs:
+            tops[n_.split("(")[0].split("<")[0][-40:]] += e_ - s_
+        top = ", ".join(f"{k} {v / 1e6:.1f}" for k, v in sorted(tops.items(), key=lambda kv: -kv[1])[:3])
+        print(f"  stream {sid:>4}: {len(rs):6d} kernels  busy {b / 1e6:8.2f} ms  ({top})")
+    ev = []
+    for s_, e_, _, sid in rows:
+        ev.append((s_, 1, sid))
+        ev.append((e_, -1, sid))
+    ev.sort()
+    active = defaultdict(int)
+    level = defaultdict(float)
+    prev = ev[0][0]
+    for t, d, sid in ev:
+        n_act = sum(1 for v in active.values() if v > 0)
+        level[min(n_act, 2)] += t - prev
+        prev = t
+        active[sid] += d
+    print("  streams running at once: " + "  ".join(f"{k if k < 2 else '2+'}: {v / 1e6:.1f} ms"
+                                                     for k, v in sorted(level.items())))
     per = defaultdict(lambda: [0, 0])
     for s, e, n, _ in rows:
         k = n.split("(")[0][:70]
