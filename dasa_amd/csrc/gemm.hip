@@ -166,7 +166,9 @@ __device__ __forceinline__ float f4get(const float4& v, int e) {
 // row = (r&3) + 8*(r>>2) + 4*(lane>>5) for 32x32, row = 4*(lane>>4) + r for 16x16.
 // Every optional operand is fetched with unconditional clamped loads inside ONE uniform branch per
 // operand (a per-element branch around a load makes hipcc wait vmcnt(0) per element).
-template <int MF, int TM, int TN, int BM, int BN, typename AccT>
+// CBF: C is bf16 ([M][ldc] bf16 elements, round to nearest even; beta must be 0), the bf16-activation
+// form of dasa_gemm_bf16_ex.
+template <int MF, int TM, int TN, int BM, int BN, typename AccT, bool CBF = false>
 __device__ __forceinline__ void store_tile_mf(const GemmP& p, AccT (&acc)[TM][TN], int b, int split, int m0,
                                               int n0, int wm, int wn, int lane) {
   constexpr int NR = MF == 32 ? 16 : 4;
@@ -226,6 +228,16 @@ __device__ __forceinline__ void store_tile_mf(const GemmP& p, AccT (&acc)[TM][TN
       }
 #pragma unroll
       for (int r = 0; r < NR; ++r) v[r] *= cs;
+      if constexpr (CBF) {
+        unsigned short* cb = reinterpret_cast<unsigned short*>(p.C) + (long)b * p.sC;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          const int row = rowof(rbase, r);
+          if (full_tile || (row < p.M && col < p.N))
+            cb[(long)row * p.ldc + col] = __builtin_bit_cast(unsigned short, (__bf16)v[r]);
+        }
+        continue;
+      }
       float* cb = p.C + (long)b * p.sC;
       if (p.beta != 0.f) {
         float cv[NR];
@@ -985,7 +997,10 @@ __device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
 
 __device__ __forceinline__ int bswz(int row) { return (row >> 1) & 7; }
 
-template <int BM, int BN, int WAVES_M, int WAVES_N, int PF = 1>
+// ABF: A arrives as bf16 ([M][lda] bf16 elements: an activation a producer already rounded, e.g. the
+// bf16 GELU output of the FFN-up GEMM) and is copied into LDS as is; CBF: C is written as bf16 (above).
+// Rounding A in its producer's epilogue instead of on this kernel's load gives the same bf16 values.
+template <int BM, int BN, int WAVES_M, int WAVES_N, int PF = 1, bool ABF = false, bool CBF = false>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_nt_kernel(GemmP p) {
   constexpr int NT = 64 * WAVES_M * WAVES_N;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N, TM = WM / 16, TN = WN / 16;
@@ -1008,7 +1023,8 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_nt_kernel(Ge
     m0 = (wgid / gridDim.x) * BM;
   }
   const int b = blockIdx.z;
-  const float* A = p.A + (long)b * p.sA;
+  const float* A = ABF ? p.A : p.A + (long)b * p.sA;
+  const unsigned short* Ab = reinterpret_cast<const unsigned short*>(p.A) + (long)b * p.sA;
   const unsigned short* W = reinterpret_cast<const unsigned short*>(p.B) + (long)b * p.sB;
 
   floatx4 acc[TM][TN];
@@ -1020,16 +1036,21 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_nt_kernel(Ge
   // staging registers of the next K tile (a struct with member functions like TileLoader: hipcc keeps
   // it in VGPRs, where lambda-captured local arrays were promoted to LDS)
   struct Stage {
-    floatx4 a[NA][2];
+    floatx4 a[ABF ? 1 : NA][2];
+    u32x4 ab[ABF ? NA : 1];
     u32x4 b[NB];
-    __device__ __forceinline__ void load(const GemmP& p, const float* A, const unsigned short* W, int m0, int n0,
-                                         int k0, int tid) {
+    __device__ __forceinline__ void load(const GemmP& p, const float* A, const unsigned short* Ab,
+                                         const unsigned short* W, int m0, int n0, int k0, int tid) {
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
         const int q = tid + NT * i, row = q >> 3, kq = q & 7;
-        const float* src = A + (long)min(m0 + row, p.M - 1) * p.lda + k0 + 8 * kq;
-        a[i][0] = *reinterpret_cast<const floatx4*>(src);
-        a[i][1] = *reinterpret_cast<const floatx4*>(src + 4);
+        if constexpr (ABF) {
+          ab[i] = *reinterpret_cast<const u32x4*>(Ab + (long)min(m0 + row, p.M - 1) * p.lda + k0 + 8 * kq);
+        } else {
+          const float* src = A + (long)min(m0 + row, p.M - 1) * p.lda + k0 + 8 * kq;
+          a[i][0] = *reinterpret_cast<const floatx4*>(src);
+          a[i][1] = *reinterpret_cast<const floatx4*>(src + 4);
+        }
       }
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
@@ -1042,9 +1063,13 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_nt_kernel(Ge
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
         const int q = tid + NT * i, row = q >> 3, kq = q & 7;
-        const floatx4 x = a[i][0], y = a[i][1];
-        S[row * 8 + (kq ^ bswz(row))] = uint4{pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]),
-                                              pack_bf16x2(y[0], y[1]), pack_bf16x2(y[2], y[3])};
+        if constexpr (ABF) {
+          S[row * 8 + (kq ^ bswz(row))] = __builtin_bit_cast(uint4, ab[i]);
+        } else {
+          const floatx4 x = a[i][0], y = a[i][1];
+          S[row * 8 + (kq ^ bswz(row))] = uint4{pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3]),
+                                                pack_bf16x2(y[0], y[1]), pack_bf16x2(y[2], y[3])};
+        }
       }
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
@@ -1081,34 +1106,34 @@ __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) void gemm_bf16_nt_kernel(Ge
   };
 
   const int nk = p.K / 64;
-  stg.load(p, A, W, m0, n0, 0, tid);
+  stg.load(p, A, Ab, W, m0, n0, 0, tid);
   if (PF == 1) {
     stg.store(smem, tid);
     __syncthreads();
     for (int t = 0; t < nk; ++t) {
-      stg.load(p, A, W, m0, n0, 64 * min(t + 1, nk - 1), tid);   // unconditional (see gemm_nt_k64_kernel)
+      stg.load(p, A, Ab, W, m0, n0, 64 * min(t + 1, nk - 1), tid);   // unconditional (see gemm_nt_k64_kernel)
       compute(smem + (t & 1) * STAGE);
       stg.store(smem + ((t + 1) & 1) * STAGE, tid);
       __syncthreads();
     }
   } else {
     // two register stages (as gemm_f32x6_nt_kernel): tile t + 2's loads are issued before tile t's MFMAs
-    stg2.load(p, A, W, m0, n0, 64 * min(1, nk - 1), tid);
+    stg2.load(p, A, Ab, W, m0, n0, 64 * min(1, nk - 1), tid);
         stg.store(smem, tid);
     __syncthreads();
     for (int t = 0; t < nk; t += 2) {
-      stg.load(p, A, W, m0, n0, 64 * min(t + 2, nk - 1), tid);
+      stg.load(p, A, Ab, W, m0, n0, 64 * min(t + 2, nk - 1), tid);
       compute(smem);
             stg2.store(smem + STAGE, tid);
       __syncthreads();
       if (t + 1 >= nk) break;
-      stg2.load(p, A, W, m0, n0, 64 * min(t + 3, nk - 1), tid);
+      stg2.load(p, A, Ab, W, m0, n0, 64 * min(t + 3, nk - 1), tid);
       compute(smem + STAGE);
             stg.store(smem, tid);
       __syncthreads();
     }
   }
-  store_tile_mf<16, TM, TN, BM, BN>(p, acc, b, 0, m0, n0, wm, wn, lane);
+  store_tile_mf<16, TM, TN, BM, BN, floatx4, CBF>(p, acc, b, 0, m0, n0, wm, wn, lane);
 }
 
 // ---- fp32 GEMM emulated on bf16 matrix cores ("bf16x6") ------------------------------------------
@@ -2246,12 +2271,18 @@ extern "C" int dasa_gemm_f32(const dasa_gemm_desc* d, void* ws, int64_t ws_bytes
 constexpr int kBf16Force = 1 << 20;
 constexpr int kX6Force = 1 << 21;   // dasa_gemm_force_config(kX6Force + cfg): bf16x6 tile forms 0..5
 
-extern "C" int dasa_gemm_bf16(const dasa_gemm_desc* d, void* stream) {
+extern "C" int dasa_gemm_bf16(const dasa_gemm_desc* d, void* stream) { return dasa_gemm_bf16_ex(d, 0, stream); }
+
+extern "C" int dasa_gemm_bf16_ex(const dasa_gemm_desc* d, int32_t flags, void* stream) {
   if (!d) return (int)hipErrorInvalidValue;
   const int M = d->M, N = d->N, K = d->K, batch = d->batch < 1 ? 1 : d->batch;
+  const bool abf = flags & DASA_BF16_A, cbf = flags & DASA_BF16_C;
   if (M < 0 || N < 0 || K < 0 || d->opA != 0 || d->opB != 1) return (int)hipErrorInvalidValue;
-  if (K % 64 != 0 || (d->lda & 3) || (d->ldb & 7) || d->lda < K || d->ldb < K || d->ldc < N)
+  if (flags & ~(DASA_BF16_A | DASA_BF16_C)) return (int)hipErrorInvalidValue;
+  if (K % 64 != 0 || (d->lda & (abf ? 7 : 3)) || (d->ldb & 7) || d->lda < K || d->ldb < K || d->ldc < N)
     return (int)hipErrorInvalidValue;
+  if (cbf && (d->beta != 0.f || ((uintptr_t)d->C & 1))) return (int)hipErrorInvalidValue;
+  if (abf && batch > 1 && (d->strideA & 7)) return (int)hipErrorInvalidValue;
   if (((uintptr_t)d->A & 15) || ((uintptr_t)d->B & 15) || (batch > 1 && ((d->strideA & 3) || (d->strideB & 7))))
     return (int)hipErrorInvalidValue;
   if (M == 0 || N == 0) return 0;
@@ -2277,6 +2308,20 @@ extern "C" int dasa_gemm_bf16(const dasa_gemm_desc* d, void* stream) {
   p.group_m = cdiv(M, bm) >= 8 ? 4 : 1;
   dim3 grid((unsigned)cdiv(N, bn), (unsigned)cdiv(M, bm), batch);
   hipStream_t st = (hipStream_t)stream;
+  if (abf || cbf) {   // the bf16-activation forms: the two tile shapes of the default plan
+    const dim3 g9((unsigned)cdiv(N, 256), (unsigned)cdiv(M, 256), batch), g2((unsigned)cdiv(N, 128), (unsigned)cdiv(M, 128), batch);
+    const bool big = cfg == 9;
+    p.group_m = cdiv(M, big ? 256 : 128) >= 8 ? 4 : 1;
+#define DASA_BF16_FORM(AB, CB)                                                                              \
+    if (big) hipLaunchKernelGGL((gemm_bf16_nt_kernel<256, 256, 4, 4, 1, AB, CB>), g9, dim3(1024), 0, st, p); \
+    else hipLaunchKernelGGL((gemm_bf16_nt_kernel<128, 128, 4, 2, 1, AB, CB>), g2, dim3(512), 0, st, p);
+    if (abf && cbf) { DASA_BF16_FORM(true, true) }
+    else if (abf) { DASA_BF16_FORM(true, false) }
+    else { DASA_BF16_FORM(false, true) }
+#undef DASA_BF16_FORM
+    DASA_CHECK_LAUNCH();
+    return 0;
+  }
   switch (cfg) {
     case 1: hipLaunchKernelGGL((gemm_bf16_nt_kernel<256, 128, 4, 2>), grid, dim3(512), 0, st, p); break;
     case 2: hipLaunchKernelGGL((gemm_bf16_nt_kernel<128, 128, 4, 2>), grid, dim3(512), 0, st, p); break;

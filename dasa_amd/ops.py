@@ -138,7 +138,7 @@ def gemm(A, B, C, *, M, N, K, opA=0, opB=1, lda, ldb, ldc, bias=None, act=None, 
 # Forward-only: nn.Linear forwards whose K % 64 == 0 run dasa_gemm_bf16 on a bf16 copy of the weight
 # (converted once per weight version); LayerNorm, softmax, attention cores, the LSTM recurrences and
 # every elementwise op stay fp32.
-_BF16 = {"on": False}
+_BF16 = {"on": False, "acts": os.environ.get("DASA_BF16_ACTS", "1") != "0"}
 _bf16_w = {}
 
 
@@ -204,6 +204,7 @@ def _bf16_weight(W):
 
 def gemm_bf16(x, Wb, out, *, M, N, K, lda, ldc, bias=None, act=None, aux=None, ld_aux=0, colscale=None,
               alpha=1.0, beta=0.0):
+    """dasa_gemm_bf16_ex; x and out each fp32 or bf16 (a bf16 activation / bf16 output)."""
     d = GemmDesc()
     d.M, d.N, d.K, d.batch = int(M), int(N), int(K), 1
     d.opA, d.opB = 0, 1
@@ -215,8 +216,10 @@ def gemm_bf16(x, Wb, out, *, M, N, K, lda, ldc, bias=None, act=None, aux=None, l
     d.aux, d.ld_aux, d.strideAux = _p(aux), int(ld_aux), 0
     d.colscale = _p(colscale)
     d.alpha, d.beta = float(alpha), float(beta)
-    _call("dasa_gemm_bf16", "gemm_bf16", _lib.lib().dasa_gemm_bf16, ctypes.byref(d), _stream(),
-          flops=2.0 * M * N * K, nbytes=4.0 * M * K + 2.0 * K * N + 4.0 * M * N, detail=(int(M), int(N), int(K)))
+    flags = (1 if x.dtype == torch.bfloat16 else 0) | (2 if out.dtype == torch.bfloat16 else 0)
+    _call("dasa_gemm_bf16_ex", "gemm_bf16", _lib.lib().dasa_gemm_bf16_ex, ctypes.byref(d), flags, _stream(),
+          flops=2.0 * M * N * K, nbytes=x.element_size() * M * K + 2.0 * K * N + out.element_size() * M * N,
+          detail=(int(M), int(N), int(K)))
 
 
 # fp32 GEMM emulated on bf16 matrix cores (include/dasa_hip.h dasa_gemm_f32x6): the nn.Linear weight
@@ -331,21 +334,38 @@ def gemm_f32x6(x, planes, out, *, M, N, K, lda, ldc, bias=None, act=None, aux=No
           detail=(int(M), int(N), int(K)), kernels=kernels)
 
 
-def linear(x, W, b=None, act=None, out=None, aux=None, colscale=None, beta=0.0, alpha=1.0):
-    """y = act(x @ W^T + b) [* aux] [* colscale] (+ beta*out). x [..., K] (row-strided ok), W [N, K]."""
-    _f32(x, "linear.x")
+def bf16_acts_ok(x, N):
+    """Under bf16_matmul: may this linear's output be handed on as a bf16 activation (the consumer is a
+    bf16 GEMM)? DASA_BF16_ACTS=0 keeps every activation fp32 (A/B)."""
+    K = x.shape[-1]
+    return (_BF16["on"] and _BF16["acts"] and x.dtype in (torch.float32, torch.bfloat16) and K % 64 == 0
+            and N % 64 == 0 and _rows(x)[1] % 8 == 0 and x.data_ptr() % 16 == 0)
+
+
+def linear(x, W, b=None, act=None, out=None, aux=None, colscale=None, beta=0.0, alpha=1.0, out_dtype=None):
+    """y = act(x @ W^T + b) [* aux] [* colscale] (+ beta*out). x [..., K] (row-strided ok), W [N, K].
+    Under bf16_matmul, x may be a bf16 activation and out_dtype=torch.bfloat16 stores y as bf16."""
+    bf_io = x.dtype == torch.bfloat16 or out_dtype == torch.bfloat16 or (out is not None and out.dtype == torch.bfloat16)
+    if not bf_io:
+        _f32(x, "linear.x")
     K = x.shape[-1]
     N = W.shape[0]
     assert W.shape[1] == K and W.stride(1) == 1, "W must be [N, K] with contiguous rows"
     M, lda = _rows(x)
     if out is None:
-        out = torch.empty(*x.shape[:-1], N, dtype=torch.float32, device=x.device)
+        out = torch.empty(*x.shape[:-1], N, dtype=out_dtype or torch.float32, device=x.device)
     Mo, ldc = _rows(out)
     assert Mo == M and out.shape[-1] == N
     ld_aux = 0
     if aux is not None:
         Ma, ld_aux = _rows(aux)
         assert Ma == M
+    if bf_io:
+        if not (_BF16["on"] and K % 64 == 0 and lda % 8 == 0 and x.data_ptr() % 16 == 0 and beta == 0.0):
+            raise _lib.DasaError("bf16 activations: bf16_matmul mode, K % 64 == 0, 16-B rows and beta 0 only")
+        gemm_bf16(x, _bf16_weight(W), out, M=M, N=N, K=K, lda=lda, ldc=ldc, bias=b, act=act, aux=aux,
+                  ld_aux=ld_aux, colscale=colscale, alpha=alpha, beta=beta)
+        return out
     if _BF16["on"] and K % 64 == 0 and lda % 4 == 0 and x.data_ptr() % 16 == 0:
         gemm_bf16(x, _bf16_weight(W), out, M=M, N=N, K=K, lda=lda, ldc=ldc, bias=b, act=act, aux=aux,
                   ld_aux=ld_aux, colscale=colscale, alpha=alpha, beta=beta)

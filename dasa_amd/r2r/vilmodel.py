@@ -174,6 +174,10 @@ class BertIntermediate(nn.Module):
             raise NotImplementedError("only the gelu BERT configuration is on the DASA path")
 
     def forward(self, hidden_states):
+        if not _needs_grad(hidden_states, self.dense.weight) and ops.bf16_acts_ok(hidden_states, self.dense.out_features):
+            # bf16 matmul mode (configs[4]): the GELU output's one consumer is BertOutput's bf16 GEMM, which
+            # rounds its A operand to bf16 anyway — store it rounded (half the bytes written and re-read)
+            return ops.linear(hidden_states, self.dense.weight, self.dense.bias, act="gelu", out_dtype=torch.bfloat16)
         return _lin(hidden_states, self.dense, "gelu")
 
 

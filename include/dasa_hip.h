@@ -74,6 +74,13 @@ int dasa_gemm_f32(const dasa_gemm_desc* d, void* ws, int64_t ws_bytes, void* str
  * Only opA = 0, opB = 1; K % 64 == 0, lda % 4 == 0, ldb % 8 == 0, 16-B aligned A and B.
  * Replaces the nn.Linear forwards of model.py / vilmodel.py / agent_dg.py:1519 in that config. */
 int dasa_gemm_bf16(const dasa_gemm_desc* d, void* stream);
+/* dasa_gemm_bf16 with bf16 activations (configs[4]'s FFN: the GELU output is stored as bf16 by the
+   FFN-up GEMM and read as bf16 by the FFN-down GEMM; the values equal the fp32-A path's, which rounds A
+   on load the same way). flags: DASA_BF16_A = A is bf16 (lda, strideA in bf16 elements, lda % 8 == 0),
+   DASA_BF16_C = C is written as bf16, round to nearest even (ldc, strideC in bf16 elements; beta 0). */
+#define DASA_BF16_A 1
+#define DASA_BF16_C 2
+int dasa_gemm_bf16_ex(const dasa_gemm_desc* d, int32_t flags, void* stream);
 /* y[i] = bf16(x[i]) (round to nearest even), n even; weight copies for dasa_gemm_bf16. */
 int dasa_f32_to_bf16(const float* x, uint16_t* y, int64_t n, void* stream);
 /* fp32 nn.Linear forward at fp32 accuracy on the bf16 matrix cores ("bf16x6"): every fp32 operand is

@@ -824,6 +824,34 @@ def test_gemm_bf16_epilogue_and_strides(dev):
     assert (out.cpu().double() - ref).abs().max().item() < 2e-5
 
 
+@pytest.mark.parametrize("M", [300, 5120])
+def test_gemm_bf16_activations(dev, M):
+    """dasa_gemm_bf16_ex (configs[4]'s FFN with bf16 activations): the bf16-stored GELU output equals the
+    fp32 output rounded to bf16 (RNE, torch's rounding) bit for bit, and the FFN-down GEMM reading it as
+    bf16 equals the one reading the fp32 tensor (rounded on load) bit for bit — both tile forms (M = 300:
+    128 x 128; M = 5120: 256 x 256)."""
+    from dasa_amd import ops, _lib
+    g = torch.Generator().manual_seed(M)
+    N, K = 3072, 768
+    x = _rand(M, K, g=g).to(dev)
+    W1, b1 = _rand(N, K, g=g, scale=0.05).to(dev), _rand(N, g=g).to(dev)
+    W2, b2 = _rand(K, N, g=g, scale=0.05).to(dev), _rand(K, g=g).to(dev)
+    with torch.no_grad(), ops.bf16_matmul():
+        assert ops.bf16_acts_ok(x, N)
+        h32 = ops.linear(x, W1, b1, act="gelu")
+        hbf = ops.linear(x, W1, b1, act="gelu", out_dtype=torch.bfloat16)
+        assert hbf.dtype == torch.bfloat16
+        assert torch.equal(hbf.view(torch.int16), h32.to(torch.bfloat16).view(torch.int16))
+        z32 = ops.linear(h32, W2, b2)
+        zbf = ops.linear(hbf, W2, b2)
+        zbb = ops.linear(hbf, W2, b2, out_dtype=torch.bfloat16)
+    torch.cuda.synchronize()
+    assert torch.equal(z32, zbf)
+    assert torch.equal(zbb.view(torch.int16), z32.to(torch.bfloat16).view(torch.int16))
+    with torch.no_grad(), pytest.raises(_lib.DasaError):     # bf16 activations only in bf16 matmul mode
+        ops.linear(hbf, W2, b2)
+
+
 def test_bf16_mode_is_forward_only(dev):
     from dasa_amd import ops, _lib
     with pytest.raises(_lib.DasaError):
