@@ -146,7 +146,18 @@ class StepGraphs:
 
 # ------------------------------------------------------------------ training-mode (autograd) regions
 class _Slot:
-    __slots__ = ("graph", "static_in", "static_out", "counter", "pkey", "fills", "shapes", "leaves")
+    __slots__ = ("graph", "static_in", "static_out", "counter", "pkey", "fills", "shapes", "leaves", "bwd", "owner")
+
+
+class _Bwd:
+    """A captured backward of one slot for one pattern of incoming gradients: static grad-output buffers,
+    the graph, its static leaf gradients, and the deferred weight-gradient products the capture queued
+    (functional.defer_weight_grads: re-queued on every replay, their dz buffers rewritten by it)."""
+    __slots__ = ("graph", "gin", "grads", "wq", "bq")
+
+
+# DASA_TRAIN_GRAPH_BWD=0: a captured training region's backward runs its recorded autograd graph eagerly
+BWD_GRAPH = os.environ.get("DASA_TRAIN_GRAPH_BWD", "1") != "0"
 
 
 def _lead(t, shape):
@@ -195,7 +206,19 @@ class _BridgeFn(torch.autograd.Function):
                 outs.append(o)
                 grads.append(g)
         got = {}
-        if outs and slot.leaves:
+        mask = tuple(o is not None and o.requires_grad and g is not None for o, g in zip(slot.static_out, gouts))
+        if outs and slot.leaves and BWD_GRAPH and not prof.active():
+            bw = slot.bwd.get(mask)
+            if bw is None:
+                bw = slot.bwd[mask] = slot.owner._capture_bwd(slot, outs, grads)
+            else:
+                for s_, g in zip(bw.gin, grads):
+                    s_.copy_(g)
+                bw.graph.replay()
+                _requeue(bw)
+            got = {id(v): g for v, g in zip(slot.leaves, bw.grads) if g is not None}
+            _accumulate_params(slot, got)
+        elif outs and slot.leaves:
             L = _lib.lib()
             L.dasa_set_seed_source(ctypes.c_void_p(slot.counter.data_ptr()))
             try:
@@ -206,23 +229,45 @@ class _BridgeFn(torch.autograd.Function):
             finally:
                 L.dasa_set_seed_source(None)
             got = {id(v): g for v, g in zip(slot.leaves, gl) if g is not None}
-            statics = {id(s) for s in slot.static_in if s is not None}
-            from . import functional as DF
-            with torch.no_grad():
-                for v in slot.leaves:
-                    g = got.get(id(v))
-                    if g is None or id(v) in statics:
-                        continue
-                    v = DF.grad_target(v)
-                    if v.grad is None:
-                        v.grad = g
-                    else:
-                        v.grad.add_(g)
+            _accumulate_params(slot, got)
         res = []
         for s, shape in zip(slot.static_in, ctx.shapes):
             g = got.get(id(s)) if s is not None and s.requires_grad else None
             res.append(_lead(g, shape) if g is not None else None)
         return (None,) + tuple(res)
+
+
+def _accumulate_params(slot, got):
+    """Add the leaf gradients that belong to parameters (through their capture aliases) into .grad."""
+    from . import functional as DF
+    statics = {id(s) for s in slot.static_in if s is not None}
+    with torch.no_grad():
+        for v in slot.leaves:
+            g = got.get(id(v))
+            if g is None or id(v) in statics:
+                continue
+            v = DF.grad_target(v)
+            if v.grad is None:
+                v.grad = g.clone()
+            else:
+                v.grad.add_(g)
+
+
+def _requeue(bw):
+    """Queue the captured backward's deferred weight / bias gradient products again (the replay rewrote
+    their dz buffers in place)."""
+    from . import functional as DF
+    for W, dz, x in bw.wq:
+        e = DF._WG.w.get(id(W))
+        if e is None:
+            e = DF._WG.w[id(W)] = [W, [], []]
+        e[1].append(dz)
+        e[2].append(x)
+    for b, dz in bw.bq:
+        e = DF._WG.b.get(id(b))
+        if e is None:
+            e = DF._WG.b[id(b)] = [b, []]
+        e[1].append(dz)
 
 
 def _graph_leaves(outs):
@@ -263,6 +308,7 @@ class AutogradGraphs:
         self.pool = None
         self._alias = {}
         self.captures = 0
+        self.captures_bwd = 0
         self.replays = 0
 
     def _param_key(self):
@@ -352,9 +398,43 @@ class AutogradGraphs:
             ops._FRESH_PLANES[0] -= 1
         slot.graph, slot.static_in, slot.static_out = g, static_in, tuple(out)
         slot.leaves = _graph_leaves(slot.static_out)
+        slot.bwd, slot.owner = {}, self
         slot.pkey = self._param_key()
         self.captures += 1
         return slot
+
+    def _capture_bwd(self, slot, outs, grads):
+        """Capture the slot's recorded backward (autograd.grad over its leaves) for this pattern of incoming
+        gradients as a graph on the capture stream, then replay it once for the current step. Its kernels
+        are a fixed sequence for a slot: replaying it costs one launch instead of the ~40 host-issued
+        launches of the per-step backward (the launch-bound phase of the iteration, r05 trace). The
+        dropout kernels of the backward read the slot's seed counter at run time, as the eager backward."""
+        from . import functional as DF
+        from . import ops
+        bw = _Bwd()
+        bw.gin = [g.detach().clone() for g in grads]
+        wq0 = {k: len(v[1]) for k, v in DF._WG.w.items()}
+        bq0 = {k: len(v[1]) for k, v in DF._WG.b.items()}
+        self.stream.wait_stream(torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        L = _lib.lib()
+        _NESTED[0] += 1
+        ops._FRESH_PLANES[0] += 1
+        L.dasa_set_seed_source(ctypes.c_void_p(slot.counter.data_ptr()))
+        try:
+            with _no_gc(), torch.cuda.graph(g, pool=self.pool, stream=self.stream):
+                gl = torch.autograd.grad(outs, slot.leaves, bw.gin, retain_graph=True, allow_unused=True)
+        finally:
+            L.dasa_set_seed_source(None)
+            _NESTED[0] -= 1
+            ops._FRESH_PLANES[0] -= 1
+        bw.graph, bw.grads = g, tuple(gl)
+        bw.wq = [(e[0], dz, x) for k, e in DF._WG.w.items() for dz, x in zip(e[1][wq0.get(k, 0):], e[2][wq0.get(k, 0):])]
+        bw.bq = [(e[0], dz) for k, e in DF._WG.b.items() for dz in e[1][bq0.get(k, 0):]]
+        g.replay()          # the capture launched nothing: compute this step's gradients now
+        self.captures_bwd += 1
+        return bw
 
     def run(self, key, fn, inputs, pads=None):
         """fn(*inputs) -> tuple of tensors / None, recorded with autograd; returns the outputs linked to

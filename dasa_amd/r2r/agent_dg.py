@@ -1061,7 +1061,7 @@ class Seq2SeqAgent(BaseAgent):
         # first pass keeps its graph for that second one
         bert = self.encoder.bert
         dx = bool(getattr(bert, "update_add_layer", False) or getattr(bert, "update_lang_bert", False))
-        dx = dx and os.environ.get("DASA_BPTT_DX", "1") != "0"       # 0: the per-call BPTT there (A/B)
+        dx = dx and os.environ.get("DASA_BPTT_DX", "0") == "1"       # off by default: measured slower (DESIGN r05)
         with DF.defer_bilstm_backward(input_grads=dx), DF.defer_weight_grads():
             self.loss.backward(retain_graph=dx)
             DF.flush_bilstm_backward()

@@ -121,6 +121,9 @@ def test_train_graph_matches_eager(dev, monkeypatch):
                 tg = ag._train_graphs
                 assert tg is not None and tg.captures == 8 and len(tg.slots) == 8, (tg and tg.captures)
                 assert tg.replays == 16
+                from dasa_amd import graph as G
+                # every slot's backward captured once (iteration 0) and replayed after
+                assert tg.captures_bwd == (8 if G.BWD_GRAPH else 0), tg.captures_bwd
             else:
                 assert ag._train_graphs is None
             del ag

@@ -14,6 +14,11 @@ def load(path):
     return rows
 
 
+def short(name):
+    n = name.replace("void ", "").replace("(anonymous namespace)::", "").replace("at::native::", "")
+    return n.split("(")[0][:60]
+
+
 def union_busy(rows):
     busy, cur_s, cur_e, gaps = 0, None, None, []
     for s, e, _, _ in rows:
@@ -59,7 +64,7 @@ def main(path, t_last_ms=None):
         b, _ = union_busy(sorted(rs))
         tops = defaultdict(int)
         for s_, e_, n_, _ in rs:
-            tops[n_.split("(")[0].split("<")[0][-40:]] += e_ - s_
+            tops[short(n_).split("<")[0][-40:]] += e_ - s_
         top = ", ".join(f"{k} {v / 1e6:.1f}" for k, v in sorted(tops.items(), key=lambda kv: -kv[1])[:3])
         print(f"  stream {sid:>4}: {len(rs):6d} kernels  busy {b / 1e6:8.2f} ms  ({top})")
     ev = []
@@ -77,9 +82,34 @@ def main(path, t_last_ms=None):
         active[sid] += d
     print("  streams running at once: " + "  ".join(f"{k if k < 2 else '2+'}: {v / 1e6:.1f} ms"
                                                      for k, v in sorted(level.items())))
+    # where the idle time sits: gaps >= 5 us by the kernel that ENDS the gap (the host was late to launch
+    # it), and the window in 20 slices (busy fraction per slice: rollout / backward / optimizer phases)
+    after = defaultdict(lambda: [0, 0])
+    cur_e = None
+    prev_name = None
+    for s_, e_, n_, _ in rows:
+        if cur_e is not None and s_ - cur_e >= 5e3:
+            k = f"{short(prev_name)[:28]} -> {short(n_)[:28]}"
+            after[k][0] += 1
+            after[k][1] += s_ - cur_e
+        if cur_e is None or e_ > cur_e:
+            cur_e, prev_name = e_, n_
+    print("  idle gaps >= 5 us by (last kernel -> next kernel):")
+    for k, (c, t) in sorted(after.items(), key=lambda kv: -kv[1][1])[:20]:
+        print(f"    {k:<60} {c:6d} {t / 1e6:8.2f} ms")
+    w0, w1 = rows[0][0], max(r[1] for r in rows)
+    nsl = 20
+    sl = (w1 - w0) / nsl
+    line = []
+    for i in range(nsl):
+        a, b = w0 + i * sl, w0 + (i + 1) * sl
+        clip = sorted((max(s_, a), min(e_, b), n_, sid) for s_, e_, n_, sid in rows if e_ > a and s_ < b)
+        bb, _ = union_busy(clip) if clip else (0, [])
+        line.append(f"{100 * bb / sl:3.0f}")
+    print(f"  busy % per {sl / 1e6:.1f} ms slice: " + " ".join(line))
     per = defaultdict(lambda: [0, 0])
     for s, e, n, _ in rows:
-        k = n.split("(")[0][:70]
+        k = short(n)
         per[k][0] += 1
         per[k][1] += e - s
     for k, (c, t) in sorted(per.items(), key=lambda kv: -kv[1][1])[:25]:
