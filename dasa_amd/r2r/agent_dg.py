@@ -598,7 +598,7 @@ class Seq2SeqAgent(BaseAgent):
         needs the eager calls, the profiler brackets every launch, or it is switched off
         (DASA_TRAIN_GRAPH=0)."""
         dec = self.decoder
-        return (graph.ENABLED and os.environ.get("DASA_TRAIN_GRAPH", "0") != "0" and torch.is_grad_enabled()
+        return (graph.ENABLED and os.environ.get("DASA_TRAIN_GRAPH", "1") != "0" and torch.is_grad_enabled()
                 and dec.training and not prof.active() and not graph.capturing()
                 and not args.decoder_consistent_drop and not args.pred_back and not args.submit
                 and isinstance(dec.drop_env, nn.Dropout)
