@@ -39,6 +39,14 @@ class GemmDesc(C.Structure):
     ]
 
 
+class CopySeg(C.Structure):
+    _fields_ = [("src", vp), ("dst", vp), ("n0", i64), ("n1", i64), ("row_bytes", i64),
+                ("src_s0", i64), ("src_s1", i64), ("dst_s0", i64), ("dst_s1", i64)]
+
+
+COPY_MAX_SEGS = 16
+
+
 # name -> (restype, argtypes)
 SIGNATURES = {
     "dasa_version": (i32, []),
@@ -47,6 +55,7 @@ SIGNATURES = {
     "dasa_gemm_f32_workspace": (i64, [C.POINTER(GemmDesc)]),
     "dasa_gemm_f32": (i32, [C.POINTER(GemmDesc), vp, i64, vp]),
     "dasa_gemm_bf16": (i32, [C.POINTER(GemmDesc), vp]),
+    "dasa_copy_segments": (i32, [C.POINTER(CopySeg), i32, vp]),
     "dasa_gemm_bf16_ex": (i32, [C.POINTER(GemmDesc), i32, vp]),
     "dasa_f32_to_bf16": (i32, [vp, vp, i64, vp]),
     "dasa_gemm_f32x6": (i32, [C.POINTER(GemmDesc), i64, vp]),

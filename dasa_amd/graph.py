@@ -134,11 +134,11 @@ class StepGraphs:
         if e is None:
             e = self._capture(fn, inputs)
             self.entries[key] = e
-        for s, x in zip(e.static_in, inputs):
-            s.copy_(x)
+        from . import ops
+        ops.copy_many(list(zip(inputs, e.static_in)))      # one launch for all inputs (ops.copy_many)
         e.graph.replay()
         self.replays += 1
-        return tuple(o.clone() if o is not None else None for o in e.static_out)
+        return _copies(e.static_out)
 
     def clear(self):
         self.entries.clear()
@@ -160,6 +160,15 @@ class _Bwd:
 BWD_GRAPH = os.environ.get("DASA_TRAIN_GRAPH_BWD", "1") != "0"
 
 
+def _copies(ts):
+    """Fresh copies of a replayed graph's static outputs (the next replay overwrites them), in one launch."""
+    from . import ops
+    with torch.no_grad():
+        outs = tuple(torch.empty_like(o) if o is not None else None for o in ts)
+        ops.copy_many([(o.detach(), c) for o, c in zip(ts, outs) if o is not None])
+    return outs
+
+
 def _lead(t, shape):
     """The leading sub-block of `t` with `shape` (a padded static input holds its input there)."""
     if tuple(t.shape) == tuple(shape):
@@ -178,7 +187,9 @@ class _BridgeFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, slot, *inputs):
+        from . import ops
         with torch.no_grad():
+            pairs = []
             for i, (s, x) in enumerate(zip(slot.static_in, inputs)):
                 if s is None:
                     continue
@@ -187,11 +198,12 @@ class _BridgeFn(torch.autograd.Function):
                     # past the new extent go back to the padding value (e.g. True in a padded mask)
                     s.data.fill_(slot.fills[i])
                     slot.shapes[i] = tuple(x.shape)
-                _lead(s.data, x.shape).copy_(x)
+                pairs.append((x.detach(), _lead(s.data, x.shape)))
+            ops.copy_many(pairs)       # one launch for the step's inputs instead of one blit each
         slot.graph.replay()
         ctx.slot = slot
         ctx.shapes = [x.shape if x is not None else None for x in inputs]
-        outs = tuple(o.detach().clone() if o is not None else None for o in slot.static_out)
+        outs = _copies(slot.static_out)
         nd = [o for o in outs if o is not None and not o.is_floating_point()]
         if nd:
             ctx.mark_non_differentiable(*nd)
@@ -212,8 +224,8 @@ class _BridgeFn(torch.autograd.Function):
             if bw is None:
                 bw = slot.bwd[mask] = slot.owner._capture_bwd(slot, outs, grads)
             else:
-                for s_, g in zip(bw.gin, grads):
-                    s_.copy_(g)
+                from . import ops
+                ops.copy_many([(g.detach(), s_) for s_, g in zip(bw.gin, grads)])
                 bw.graph.replay()
                 _requeue(bw)
             got = {id(v): g for v, g in zip(slot.leaves, bw.grads) if g is not None}

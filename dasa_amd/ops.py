@@ -457,6 +457,65 @@ def dropout(x, p, seed, out=None):
     return out
 
 
+_BATCHED_COPY = os.environ.get("DASA_BATCHED_COPY", "1") != "0"     # 0: torch copies (A/B)
+
+
+def _copy_layout(src, dst):
+    """Joint (n0, n1, inner elements, src s0, src s1, dst s0, dst s1) in elements for a pair whose innermost
+    dim is contiguous in both and whose other dims collapse (contiguous in BOTH) to at most two, else None."""
+    if src.dim() == 0:
+        return 1, 1, 1, 0, 0, 0, 0
+    dims = []                       # (extent, src stride, dst stride), innermost first
+    for n, a, b in zip(reversed(src.shape), reversed(src.stride()), reversed(dst.stride())):
+        if n == 1:
+            continue
+        if dims and a == dims[-1][0] * dims[-1][1] and b == dims[-1][0] * dims[-1][2]:
+            dims[-1] = (dims[-1][0] * n, dims[-1][1], dims[-1][2])
+        else:
+            dims.append((n, a, b))
+    if not dims:
+        return 1, 1, 1, 0, 0, 0, 0
+    if dims[0][1] != 1 or dims[0][2] != 1:
+        dims.insert(0, (1, 1, 1))
+    if len(dims) > 3:
+        return None
+    while len(dims) < 3:
+        dims.append((1, 0, 0))
+    (inner, _, _), (n1, a1, b1), (n0, a0, b0) = dims
+    return n0, n1, inner, a0, a1, b0, b1
+
+
+def copy_many(pairs):
+    """dst.copy_(src) for every (src, dst) pair (same shape and dtype, same device) in batched launches of
+    dasa_copy_segments; a pair whose layouts do not fit a segment is copied by torch."""
+    segs = []
+    nbytes = 0.0
+    for src, dst in pairs:
+        if src is None or dst is None or src.numel() == 0:
+            continue
+        if not _BATCHED_COPY:
+            dst.copy_(src)
+            continue
+        assert src.shape == dst.shape and src.dtype == dst.dtype, (src.shape, dst.shape, src.dtype, dst.dtype)
+        lay = _copy_layout(src, dst) if src.device == dst.device and src.is_cuda else None
+        if lay is None:
+            dst.copy_(src)
+            continue
+        es = src.element_size()
+        seg = _lib.CopySeg()
+        seg.src, seg.dst = src.data_ptr(), dst.data_ptr()
+        seg.n0, seg.n1, seg.row_bytes = lay[0], lay[1], lay[2] * es
+        seg.src_s0, seg.src_s1, seg.dst_s0, seg.dst_s1 = lay[3] * es, lay[4] * es, lay[5] * es, lay[6] * es
+        segs.append(seg)
+        nbytes += 2.0 * src.numel() * es
+    L = _lib.lib()
+    for i in range(0, len(segs), _lib.COPY_MAX_SEGS):
+        chunk = segs[i:i + _lib.COPY_MAX_SEGS]
+        arr = (_lib.CopySeg * len(chunk))(*chunk)
+        _call("dasa_copy_segments", "elementwise", L.dasa_copy_segments, arr, len(chunk), _stream(), nbytes=nbytes)
+        nbytes = 0.0
+
+
 def copy2d(x, out):
     rows, ldx = _rows(x)
     _, ldo = _rows(out)

@@ -49,6 +49,14 @@ typedef struct dasa_gemm_desc {
   const float* colscale;   /* [N] or NULL (shared env-drop noise, agent_dg.py:780-785) */
   float alpha, beta;
 } dasa_gemm_desc;
+/* One block of a batched strided copy (dasa_copy_segments): n0 x n1 rows of row_bytes contiguous bytes,
+   row (i0, i1) at src + i0*src_s0 + i1*src_s1 (bytes), written to dst + i0*dst_s0 + i1*dst_s1. */
+typedef struct dasa_copy_seg {
+  const void* src; void* dst;
+  int64_t n0, n1, row_bytes;
+  int64_t src_s0, src_s1, dst_s0, dst_s1;
+} dasa_copy_seg;
+#define DASA_COPY_MAX_SEGS 16
 /* Workspace bytes for this descriptor: 64 KiB of stream-K arrival counters, then split-K partials
  * (the skinny M <= 32 decoder GEMMs' split-K partials) or stream-K partial-tile slabs (mid-size GEMMs that do not fill the CUs).
  * The buffer must be ZERO-FILLED when first allocated; every call leaves the counters zero again,
@@ -283,6 +291,10 @@ int dasa_colscale(const float* x, int64_t ldx, const float* scale, float* out, i
 /* ---- observation pipeline (agent_dg.py:286-323, env.py:317-360 on a device-resident store) -----
  * out[r] = [ta[ia[r]] (Fa floats; zeros if ia[r] < 0) | tb[ib[r]] (Fb floats; zeros if ib == NULL or
  * ib[r] < 0)]: panorama blocks [B][36][2048+128] and candidate blocks [B][C][2176] in one gather.  */
+/* Up to DASA_COPY_MAX_SEGS strided block copies in ONE launch (no reference counterpart: the static-buffer
+   traffic around replayed hipGraphs, dasa_amd/graph.py). Segments must not overlap each other's
+   destinations or alias their own source; n == 0 is a no-op. */
+int dasa_copy_segments(const dasa_copy_seg* segs, int32_t n, void* stream);
 int dasa_gather_rows(const float* ta, const int32_t* ia, int32_t Fa, const float* tb, const int32_t* ib,
                      int32_t Fb, float* out, int32_t R, void* stream);
 

@@ -294,3 +294,18 @@ def test_synth_back_teacher_is_a_candidate_or_here():
         for ob in env._get_obs():
             assert ob["back_teacher"] == ob["viewpoint"] or any(
                 c["viewpointId"] == ob["back_teacher"] for c in ob["candidate"]), ob["viewpoint"]
+
+
+def test_copy_layout_collapse():
+    """ops._copy_layout: the joint (n0, n1, inner, strides) of a copy pair — contiguous dims merged only
+    where both sides are contiguous, at most three levels (a strided inner dim becomes 1-element rows), else None."""
+    import torch
+    from dasa_amd.ops import _copy_layout
+    s = torch.zeros(20, 96, 2048)
+    assert _copy_layout(torch.zeros(20, 80, 2048), s[:, :80]) == (1, 20, 163840, 0, 163840, 0, 196608)
+    assert _copy_layout(torch.zeros(20), torch.zeros(20)) == (1, 1, 20, 0, 0, 0, 0)
+    assert _copy_layout(torch.zeros(()), torch.zeros(())) == (1, 1, 1, 0, 0, 0, 0)
+    assert _copy_layout(torch.zeros(20, 5).t(), torch.zeros(5, 20)) == (5, 20, 1, 1, 5, 20, 1)
+    assert _copy_layout(torch.zeros(3, 5, 7, 9)[:, 1:4, :, :8], torch.zeros(3, 3, 7, 8)) == (3, 21, 8, 315, 9, 168, 8)
+    assert _copy_layout(torch.zeros(2, 3, 4, 5)[:, :, :, ::2], torch.zeros(2, 3, 4, 3)) == (24, 3, 1, 5, 2, 3, 1)
+    assert _copy_layout(torch.zeros(3, 4, 5, 6)[:, ::2, ::2, ::2], torch.zeros(3, 2, 3, 3)) is None

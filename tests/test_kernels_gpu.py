@@ -1104,3 +1104,35 @@ def test_gemm_skinny_nn_kernel(dev, M, N, K):
             assert (out.cpu().double() - (z + c0.double())).abs().max().item() < tol + 1e-6, (waves, ks)
     finally:
         lib.dasa_gemm_skinny_tune(-1, -1)
+
+
+def test_copy_many(dev):
+    """ops.copy_many (dasa_copy_segments, the batched static-buffer copies around graph replays): padded
+    3-D destinations, strided and expanded sources, bool / int64 / bf16 / 0-dim tensors and more pairs than
+    one launch takes (16), each equal to torch's copy_ bit for bit."""
+    from dasa_amd import ops
+    g = torch.Generator(device=dev).manual_seed(3)
+    pairs, refs = [], []
+
+    def add(src, dst):
+        ref = dst.clone()
+        ref.copy_(src)
+        pairs.append((src, dst))
+        refs.append(ref)
+    big = torch.zeros(20, 96, 2048, device=dev)
+    add(torch.rand(20, 80, 2048, device=dev, generator=g), big[:, :80])
+    add(torch.rand(20, 16, 2176, device=dev, generator=g)[:, :5], torch.zeros(20, 32, 2176, device=dev)[:, :5])
+    add(torch.rand(20, 1024, device=dev, generator=g).t(), torch.zeros(1024, 20, device=dev))
+    add(torch.ones(1, device=dev).expand(20, 1024), torch.zeros(20, 1024, device=dev))
+    add(torch.rand(20, 80, device=dev, generator=g) < 0.5, torch.ones(20, 96, dtype=torch.bool, device=dev)[:, :80])
+    add(torch.randint(0, 9, (20,), device=dev, generator=g), torch.zeros(20, dtype=torch.int64, device=dev))
+    add(torch.rand(7, 33, device=dev, generator=g).to(torch.bfloat16), torch.zeros(7, 33, dtype=torch.bfloat16, device=dev))
+    add(torch.tensor(3.5, device=dev), torch.zeros((), device=dev))
+    add(torch.rand(3, 5, 7, 9, device=dev, generator=g)[:, 1:4, :, :8], torch.zeros(3, 3, 7, 8, device=dev))
+    for i in range(14):
+        add(torch.rand(i + 1, 13, device=dev, generator=g), torch.zeros(i + 1, 13, device=dev))
+    ops.copy_many(pairs)
+    torch.cuda.synchronize()
+    for (src, dst), ref in zip(pairs, refs):
+        assert torch.equal(dst, ref), (src.shape, src.stride(), dst.stride())
+    assert torch.equal(big[:, 80:], torch.zeros_like(big[:, 80:]))     # the padding stayed untouched
