@@ -330,16 +330,50 @@ def aug_leg(a, steps=2):
         agent.optim_step()
         args.ml_weight = args.ml_weight_org
         return n * a.batch
-    iteration()
+    extra = _warm(agent, 1, step=iteration)
     words.clear()
+    cap0 = _captures(agent)
     u, dt = timed(iteration, steps, 0, 1)
     res = {"workload": "full auglistener iteration (train.py:226-243): GT half + aug half (speaker "
                        "back-translation + env-drop noise, teacher + sampled rollout) + optim_step",
            "value": round(u / dt, 2), "unit": "agent-decisions/s", "ms_per_step": round(1000 * dt / steps, 2),
-           "decisions_per_iteration": u / steps, "speaker_words_per_decode": words}
+           "decisions_per_iteration": u / steps, "speaker_words_per_decode": words,
+           "capture_warmup_iterations": extra, "train_graph_captures_in_timed": _captures(agent) - cap0}
     del agent, spk
     torch.cuda.empty_cache()
     return res
+
+
+def _captures(agent):
+    """Captured training regions + their backward graphs so far (graph.AutogradGraphs): a capture inside the
+    timed region (a slot first seen there) is reported beside the number it slowed."""
+    tg = getattr(agent, "_train_graphs", None)
+    return 0 if tg is None else tg.captures + tg.captures_bwd
+
+
+def _warm(agent, n, world=1, step=None):
+    """n untimed iterations; then, while the last one still captured training regions (graph.AutogradGraphs
+    records a slot the first time a step index / padded shape occurs), up to two more, so that the timed
+    iterations replay. Every rank runs the same count (the decision is all-reduced: the ranks' episodes
+    differ, and optim_step's gradient all-reduce needs them in step). Returns the extra count."""
+    step = step or (lambda: train_step(agent))
+    last = 0
+    for _ in range(n):
+        c = _captures(agent)
+        step()
+        last = _captures(agent) - c
+    extra = 0
+    while n > 0 and extra < 2:
+        flag = torch.tensor([float(last > 0)], device=torch.device("cuda", torch.cuda.current_device()))
+        if world > 1:
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        if flag.item() == 0:
+            break
+        c = _captures(agent)
+        step()
+        last = _captures(agent) - c
+        extra += 1
+    return extra
 
 
 def cfg4_leg(a, steps=3):
@@ -354,11 +388,14 @@ def cfg4_leg(a, steps=3):
     c.batch, c.vl = 2, 3
     agent, _ = build_agent(c, 0, 1, finetune=True)
     assert agent.encoder.bert.update_add_layer
-    train_step(agent)
+    extra = _warm(agent, max(1, a.warmup))
+    cap0 = _captures(agent)
     u, dt = timed(lambda: train_step(agent), steps, 0, 1)
     res = {"workload": "configs[3] per rank: README finetune iteration (d_update_add_layer, vl=3, B=2, "
                        f"maxAction {c.max_action}, teacher + sample rollout, backward, RMSprop)",
-           "value": round(u / dt, 2), "unit": "agent-decisions/s", "ms_per_step": round(1000 * dt / steps, 2)}
+           "value": round(u / dt, 2), "unit": "agent-decisions/s", "ms_per_step": round(1000 * dt / steps, 2),
+           "warmup": max(1, a.warmup), "capture_warmup_iterations": extra,
+           "train_graph_captures_in_timed": _captures(agent) - cap0}
     with prof.collect(a.shapes) as rec:
         train_step(agent)
     summ = rec.summary(pmc_workload="cfg4")
@@ -434,13 +471,14 @@ def main():
         print(json.dumps({"aug": aug_leg(a)}), flush=True)
         return
     agent, env = build_agent(a, rank, world)
-    for _ in range(a.warmup):
-        train_step(agent)
+    extra = _warm(agent, a.warmup, world)
     if a.profile_only:
         summ, punits = kernel_profile(agent, lambda: train_step(agent), a.shapes)
         print(json.dumps({"profile_only": True, "decisions": punits, **summ}), flush=True)
         return
+    cap0 = _captures(agent)
     units, dt = timed(lambda: train_step(agent), a.steps, rank, world)
+    cap_timed = _captures(agent) - cap0
     value = units / dt
     out = {
         "metric": "agent decision-steps/sec at B=20, 36x2048 feats, maxAction=35; 1/2/4/8 MI355X",
@@ -455,6 +493,7 @@ def main():
                    "global_batch": a.batch * world, "per_rank_batch": a.batch, "max_action": a.max_action,
                    "instr_len": 80, "vl_layers": a.vl, "la_layers": 9, "parallelism": f"dp{world}",
                    "world_size": world, "backend": (dist.get_backend() if world > 1 else None)},
+        "train_graph_captures_in_timed": cap_timed, "capture_warmup_iterations": extra,
     }
     if not a.no_fwd:
         fwd_rollout(agent)

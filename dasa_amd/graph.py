@@ -49,6 +49,22 @@ def _no_gc():
             gc.enable()
 
 
+@contextlib.contextmanager
+def _graph(g, pool=None, stream=None):
+    """torch.cuda.graph without its torch.cuda.empty_cache(): that call returns every cached block to the
+    driver, so the allocations after each capture go back to hipMalloc — with a capture per new slot of a
+    small-batch finetune rollout (cfg4: candidate blocks / steps first seen in later iterations) the
+    release-and-reallocate cycle cost up to 155 ms in one iteration (r05 trace). The device is synchronised
+    and the capture runs in torch's global error mode on `stream`, as torch.cuda.graph does."""
+    torch.cuda.synchronize()
+    with torch.cuda.stream(stream):
+        g.capture_begin(*(() if pool is None else (pool,)), capture_error_mode="global")
+        try:
+            yield
+        finally:
+            g.capture_end()
+
+
 def capturing():
     """True while a StepGraphs region is being captured (or warmed up for capture)."""
     return _NESTED[0] > 0
@@ -102,7 +118,7 @@ class StepGraphs:
             ctr = ctypes.c_void_p(self.counter.data_ptr())
             L.dasa_set_seed_source(ctr)
             try:
-                with _no_gc(), torch.cuda.graph(g, stream=self.stream), torch.no_grad():
+                with _no_gc(), _graph(g, stream=self.stream), torch.no_grad():
                     _lib.check(L.dasa_seed_bump(ctr, ctypes.c_void_p(self.stream.cuda_stream)),
                                "dasa_seed_bump")
                     out = fn(*static_in)
@@ -399,7 +415,7 @@ class AutogradGraphs:
             ctr = ctypes.c_void_p(slot.counter.data_ptr())
             L.dasa_set_seed_source(ctr)
             try:
-                with self._aliased(), _no_gc(), torch.cuda.graph(g, pool=self.pool, stream=self.stream), \
+                with self._aliased(), _no_gc(), _graph(g, pool=self.pool, stream=self.stream), \
                         torch.enable_grad():
                     _lib.check(L.dasa_seed_bump(ctr, ctypes.c_void_p(self.stream.cuda_stream)), "dasa_seed_bump")
                     out = fn(*static_in)
@@ -435,7 +451,7 @@ class AutogradGraphs:
         ops._FRESH_PLANES[0] += 1
         L.dasa_set_seed_source(ctypes.c_void_p(slot.counter.data_ptr()))
         try:
-            with _no_gc(), torch.cuda.graph(g, pool=self.pool, stream=self.stream):
+            with _no_gc(), _graph(g, pool=self.pool, stream=self.stream):
                 gl = torch.autograd.grad(outs, slot.leaves, bw.gin, retain_graph=True, allow_unused=True)
         finally:
             L.dasa_set_seed_source(None)
