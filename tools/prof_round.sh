@@ -43,7 +43,7 @@ REGEX='gemm|mha|bilstm|attn_|ln_fwd|policy_head|ew4|gather|adain'
 # cfg4 = the README finetune iteration
 for W in ${PMC_WORKLOADS:-cfg2 cfg5 cfg4}; do
   case $W in
-    cfg2) WARGS="--steps 1 --warmup 0 --no-profile $BENCH_ARGS" ;;
+    cfg2) WARGS="--steps 1 --warmup 1 --no-profile $BENCH_ARGS" ;;
     *) WARGS="--only $W" ;;
   esac
   n=0
