@@ -547,7 +547,7 @@ extern "C" int dasa_bilstm_bwd(const float* whh_fwd, const float* whh_bwd, const
   }
   const int mode = lstm_mode();
   if (mode != 1 && bilstm_persist_ok(B, H)) {
-    hipLaunchKernelGGL(fill_kernel, dim3(1), dim3(64), 0, st, ws, 16L, 0.f);   // barrier words
+    hipLaunchKernelGGL(fill_kernel, dim3(2), dim3(256), 0, st, ws, 512L, 0.f);   // barrier words (sharded)
     DASA_CHECK_LAUNCH();
     const int rc = bilstm_persist_bwd(whh_fwd, whh_bwd, lengths, save_act, save_c, dout, dh_n, dc_n, dgates, B, L,
                                       H, reinterpret_cast<unsigned*>(ws), st);

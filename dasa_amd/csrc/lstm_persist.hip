@@ -43,29 +43,41 @@ __device__ __forceinline__ void st_sc1(float* p, float v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // global_store_dword ... sc1
 }
 
-// Arrive + wait on the direction's monotonic counter. Returns false (after setting *tmo) if the
-// other workgroups did not arrive within kSpinTicks; every thread of the workgroup gets the answer.
-// `force` (test hook dasa_persist_force_timeout) takes the timeout path without waiting.
-__device__ bool dir_barrier(unsigned* cnt, unsigned target, unsigned* tmo, float* flag_lds, int force) {
+// Arrive + wait on the direction's monotonic counter, kept as 8 shards (the arriving workgroup adds to shard
+// blockIdx % 8, i.e. its XCD under round-robin placement; the waiter sums all 8): 128 arrivals on ONE word
+// serialise at ≈12 ns each (MI355X_MICROARCH.md "fanin": shard the counter per XCD above a few dozen
+// arrivers), 16 per shard do not. Shard k of direction d at sync[32 + 16 (8 d + k)] (64 B apart); the
+// caller zeroes sync[0 .. 512). Returns false (after setting *tmo) if the other workgroups did not arrive
+// within kSpinTicks; every thread of the workgroup gets the answer. `force` (test hook
+// dasa_persist_force_timeout) takes the timeout path without waiting.
+__device__ bool dir_barrier(unsigned* sync, int dir, unsigned target, unsigned* tmo, float* flag_lds, int force) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave drains its sc1 stores
   __syncthreads();
-  if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x < 64) {                              // wave 0 arrives and polls (uniform loop)
+    const int lane = threadIdx.x;
+    unsigned* shards = sync + 32 + dir * 8 * 16;
+    if (lane == 0) __hip_atomic_fetch_add(shards + (blockIdx.x & 7) * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const long long t0 = wall_clock64();
-    float ok = 1.f;
+    bool ok = true;
     if (force) {
-      __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      ok = 0.f;
+      if (lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ok = false;
     }
-    while (ok != 0.f && __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    // the 8 shards through a buffer resource (lanes >= 8 read past num_records: 0) with sc1, one offset VGPR
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)shards, (short)0, 8 * 16 * 4, 0x00020000);
+    while (ok) {
+      unsigned v = __builtin_amdgcn_raw_buffer_load_b32(rs, lane * 64, 0, 16 /* sc1 */);
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      if (__shfl(v, 0, 64) >= target) break;
       __builtin_amdgcn_s_sleep(1);
       if (wall_clock64() - t0 > kSpinTicks) {
-        __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = 0.f;
-        break;
+        if (lane == 0) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = false;
       }
     }
-    *flag_lds = ok;
+    if (lane == 0) *flag_lds = ok ? 1.f : 0.f;
   }
   __syncthreads();
   return *flag_lds != 0.f;
@@ -321,7 +333,7 @@ __global__ __launch_bounds__(1024) void bilstm_persist_fwd_kernel(PFwd a) {
       if (bt + 1 < NBT && (bt + 1) * 32 < B) __syncthreads();
     }
     stamp(a.stamps, 8 * s + 3);
-    if (s + 1 < L && !dir_barrier(&a.sync[dir], (unsigned)(s + 1) * G, &a.sync[2], &smem[PW * 1024], a.force_tmo))
+    if (s + 1 < L && !dir_barrier(a.sync, dir, (unsigned)(s + 1) * G, &a.sync[2], &smem[PW * 1024], a.force_tmo))
       break;
     stamp(a.stamps, 8 * s + 4);
   }
@@ -464,7 +476,7 @@ __global__ __launch_bounds__(1024) void bilstm_persist_bwd_kernel(PBwd a) {
         dh = rec + dh;
       }
     }
-    if (s + 1 < L && !dir_barrier(&a.sync[dir], (unsigned)(s + 1) * G, &a.sync[2], &smem[PW * 512], a.force_tmo))
+    if (s + 1 < L && !dir_barrier(a.sync, dir, (unsigned)(s + 1) * G, &a.sync[2], &smem[PW * 512], a.force_tmo))
       break;
   }
   if (launch_failed(&a.sync[2], a.err, 2u, &smem[PW * 512]) && owner) {

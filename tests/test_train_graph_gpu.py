@@ -137,3 +137,48 @@ def test_train_graph_matches_eager(dev, monkeypatch):
                 assert err <= 1e-5 * max(1e-30, g0[k].abs().max().item()), (it, k, err)
     finally:
         param.readme_train(["--d_vl_layers", "1", "--batchSize", "2", "--maxAction", "5"])
+
+
+@pytest.mark.parametrize("bwd_graph", [True, False])
+def test_captured_backward_regenerates_replay_masks(dev, monkeypatch, bwd_graph):
+    """a captured region WITH dropout (p = 0.3 on the input, 0.2 on the output of a linear): the
+    gradient its backward returns (captured backward graph, or the recorded autograd graph run eagerly) is
+    the gradient of the forward the replay computed, masks included. The region is linear in x for fixed
+    masks, so <dx, d> must equal <gy, y(x + d) - y(x)> with y(x + d) replayed on the SAME masks (the slot's
+    seed counter stepped back by the one bump a replay adds). A backward that regenerated other masks than
+    the replay drew fails by O(1)."""
+    from dasa_amd import functional as DF
+    from dasa_amd import graph
+    monkeypatch.setattr(graph, "BWD_GRAPH", bwd_graph)
+    torch.manual_seed(5)
+    lin = torch.nn.Linear(256, 128).to(dev)
+    g = graph.AutogradGraphs([lin])
+    x = torch.randn(64, 256, device=dev, requires_grad=True)
+
+    def fn(x):
+        h = DF.dropout(x, 0.3, True)
+        y = DF.linear(h, lin.weight, lin.bias)
+        return (DF.dropout(y, 0.2, True),)
+    seen = []
+    for it in range(3):            # capture (+ backward capture), then replays of both
+        g.new_iteration()
+        (y,) = g.run("r", fn, (x,))
+        gy = torch.randn_like(y)
+        x.grad = None
+        y.backward(gy)
+        gx = x.grad.detach().clone()
+        d = torch.randn_like(x)
+        slot = next(iter(g.slots.values()))
+        slot.counter.sub_(1)       # the next replay draws this replay's masks again
+        g.new_iteration()
+        with torch.no_grad():
+            (y2,) = g.run("r", fn, (x.detach() + d,))
+        lhs = (gx.double() * d.double()).sum().item()
+        rhs = (gy.double() * (y2.double() - y.detach().double())).sum().item()
+        assert abs(lhs - rhs) <= 1e-4 * max(1.0, abs(rhs)), (it, lhs, rhs)
+        seen.append(y.detach().clone())
+        assert lin.weight.grad is not None          # parameter gradients reach the real parameters
+        lin.weight.grad = None
+        lin.bias.grad = None
+    assert g.captures == 1 and g.captures_bwd == (1 if bwd_graph else 0)
+    assert not torch.equal(seen[0], seen[1])        # fresh masks per replay
