@@ -216,9 +216,34 @@ __global__ __launch_bounds__(1024) void bilstm_persist_fwd_kernel(PFwd a) {
     }
   }
   const int b = lane & 31;
+  // One batch tile (B <= 32: the sampled rollout's per-step launches): the owners' input-projection gates of
+  // the NEXT timestep are fetched into LDS by buffer_load ... lds before this step's barrier (they do not
+  // depend on the recurrence; no registers held), the lengths once — the cell update then waits on no
+  // global load (phase clocks: cell+store 2860 -> 1930 cycles per step at B = 20, r05). The owners are
+  // waves 0-3: wave w's 64 lanes fill 64 consecutive words of each gate row. (Multi-tile launches keep the
+  // direct loads: their unrolled tile loop spills with the prefetch.)
+  constexpr int XQ = NBT == 1 ? 1 : 0;
+  __shared__ float xq_s[XQ ? 4 * 256 : 1];
+  __shared__ int len_s[XQ ? 256 : 1];
+  const __amdgpu_buffer_rsrc_t xrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.xproj, (short)0, (int)((long)B * L * 8 * H * 4), 0x00020000);
+  const int xvoff = (min(oi, B - 1) * L * 8 * H + uj) * 4;
+  auto load_xq = [&](int s_) {
+    if (!own) return;   // wave-uniform
+    const int t_ = dir == 0 ? s_ : L - 1 - s_;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (__attribute__((address_space(3))) void*)(xq_s + q * 256 + 64 * w), 4,
+                                               xvoff, (t_ * 8 * H + dir * 4 * H + q * H) * 4, 0, 0);
+  };
+  if constexpr (XQ) {
+    if (own) len_s[threadIdx.x] = a.len[min(oi, B - 1)];
+    load_xq(0);
+  }
   for (int s = 0; s < L; ++s) {
     stamp(a.stamps, 8 * s);
     const int t = dir == 0 ? s : L - 1 - s;
+    if constexpr (XQ) __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this wave's gate fetch has landed
     const float* hin = a.hbuf + (long)((s & 1) * 2 + dir) * B * H;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)hin, (short)0, B * H * 4, 0x00020000);
 #pragma unroll(X6 ? 1 : NBT)   // X6 unrolled over tiles spills (the compiler hoists the next tile's loads)
@@ -304,12 +329,13 @@ __global__ __launch_bounds__(1024) void bilstm_persist_fwd_kernel(PFwd a) {
         const float* xp = a.xproj + (((long)ob * L + t) * 2 + dir) * 4 * H;
         float gq[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) gq[q] = xp[q * H + uj] + smem[X6 ? oi * 32 + q * PU + ou : rr * 64 + lh + q * PU + ou];
+        for (int q = 0; q < 4; ++q)
+          gq[q] = (XQ ? xq_s[q * 256 + threadIdx.x] : xp[q * H + uj]) + smem[X6 ? oi * 32 + q * PU + ou : rr * 64 + lh + q * PU + ou];
         float* outp = a.out + ((long)ob * L + t) * 2 * H + dir * H + uj;
         float* sa = a.save_act ? a.save_act + (((long)t * 2 + dir) * B + ob) * 4 * H : nullptr;
         float c = NBT > 1 ? cst[bt * 256 + threadIdx.x] : c1;
         float hp = NBT > 1 ? hst[bt * 256 + threadIdx.x] : h1;
-        if (t < a.len[ob]) {
+        if (t < (XQ ? len_s[threadIdx.x] : a.len[ob])) {
           const float i = sigmoidf_(gq[0]), f = sigmoidf_(gq[1]), gg = tanhf(gq[2]), o = sigmoidf_(gq[3]);
           c = f * c + i * gg;
           hp = o * tanhf(c);
@@ -333,6 +359,7 @@ __global__ __launch_bounds__(1024) void bilstm_persist_fwd_kernel(PFwd a) {
       if (bt + 1 < NBT && (bt + 1) * 32 < B) __syncthreads();
     }
     stamp(a.stamps, 8 * s + 3);
+    if (XQ && s + 1 < L) load_xq(s + 1);   // in flight across the barrier
     if (s + 1 < L && !dir_barrier(a.sync, dir, (unsigned)(s + 1) * G, &a.sync[2], &smem[PW * 1024], a.force_tmo))
       break;
     stamp(a.stamps, 8 * s + 4);
@@ -411,6 +438,24 @@ __global__ __launch_bounds__(1024) void bilstm_persist_bwd_kernel(PBwd a) {
   const bool v0 = r16 < B, v1 = 16 + r16 < B;
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.dgates, (short)0, B * L * 2 * G4 * 4, 0x00020000);
+  // the owner's saved activations / cell states / output gradient of the NEXT step are loaded before this
+  // step's barrier (they do not depend on the recurrence): the cell phase then waits on no global load
+  float pf_do = 0.f, pf_i = 0.f, pf_f = 0.f, pf_g = 0.f, pf_o = 0.f, pf_c = 0.f, pf_cp = 0.f;
+  auto prefetch = [&](int s_) {
+    if (!owner) return;
+    const int t_ = dir == 0 ? (L - 1 - s_) : s_;
+    if (t_ >= lenb) return;
+    pf_do = a.dout[((long)ob * L + t_) * 2 * H + dir * H + j];
+    const float* sa = a.save_act + (((long)t_ * 2 + dir) * B + ob) * G4;
+    pf_i = sa[j];
+    pf_f = sa[H + j];
+    pf_g = sa[2 * H + j];
+    pf_o = sa[3 * H + j];
+    pf_c = a.save_c[(((long)t_ * 2 + dir) * B + ob) * H + j];
+    const int tq = dir == 0 ? t_ - 1 : t_ + 1;   // previous step in forward order
+    pf_cp = (tq >= 0 && tq < L) ? a.save_c[(((long)tq * 2 + dir) * B + ob) * H + j] : 0.f;
+  };
+  prefetch(0);
   for (int s = 0; s < L; ++s) {
     const int t = dir == 0 ? (L - 1 - s) : s;
     floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
@@ -454,12 +499,9 @@ __global__ __launch_bounds__(1024) void bilstm_persist_bwd_kernel(PBwd a) {
       const float rec = smem[PW * 512 - 512 + tile * 256 + (br & 3) * 64 + (br >> 2) * 16 + oj];
       float* dg = a.dgates + (((long)ob * L + t) * 2 + dir) * G4;
       if (t < lenb) {
-        const float G = rec + a.dout[((long)ob * L + t) * 2 * H + dir * H + j] + dh;
-        const float* sa = a.save_act + (((long)t * 2 + dir) * B + ob) * G4;
-        const float i_ = sa[j], f_ = sa[H + j], g_ = sa[2 * H + j], o_ = sa[3 * H + j];
-        const float ct = a.save_c[(((long)t * 2 + dir) * B + ob) * H + j];
-        const int tq = dir == 0 ? t - 1 : t + 1;   // previous step in forward order
-        const float cp = (tq >= 0 && tq < L) ? a.save_c[(((long)tq * 2 + dir) * B + ob) * H + j] : 0.f;
+        const float G = rec + pf_do + dh;
+        const float i_ = pf_i, f_ = pf_f, g_ = pf_g, o_ = pf_o;
+        const float ct = pf_c, cp = pf_cp;
         const float tc = tanhf(ct);
         const float dcv = dc + G * o_ * (1.f - tc * tc);
         st_sc1(dg + j, dcv * g_ * i_ * (1.f - i_));
@@ -476,6 +518,7 @@ __global__ __launch_bounds__(1024) void bilstm_persist_bwd_kernel(PBwd a) {
         dh = rec + dh;
       }
     }
+    if (s + 1 < L) prefetch(s + 1);   // in flight across the barrier
     if (s + 1 < L && !dir_barrier(a.sync, dir, (unsigned)(s + 1) * G, &a.sync[2], &smem[PW * 512], a.force_tmo))
       break;
   }
@@ -587,6 +630,8 @@ int bilstm_persist_fwd(const float* xproj, const float* whh_fwd, const float* wh
   PFwd a{xproj, whh_fwd, whh_bwd, lengths, out, save_act, save_c, h_n, c_n, hbuf, sync, g_err_word, g_force_tmo,
          B, L, H, g_stamps};
   const int grid = 2 * H / PU;
+  // the single-tile gate prefetch addresses xproj with 32-bit buffer offsets (the caller takes the step kernels)
+  if ((long)B * L * 8 * H * 4 >= (1L << 31)) return (int)hipErrorInvalidValue;
   // X6 at one or two 32-row tiles only (profiles/r03/lstm_x6_probe.txt, L = 80: B = 20 0.69-0.74 vs 0.76
   // ms, B = 40 1.03-1.05 vs 1.16-1.20; B = 96 / 160 3-5 % slower, the tile loop then spills): the step
   // is bound by the h-state hand-off latency and the direction barrier more than by the MFMA cycles
