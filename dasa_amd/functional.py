@@ -378,10 +378,13 @@ class ShiftAttnFn(torch.autograd.Function):
             ctx.save_for_backward(h, feat, q, attn, shifted, wsm)
             ctx.params = _Kept((W_in, W_s, b_s))
         ctx.mark_non_differentiable(attn)
+        ctx.set_materialize_grads(False)     # no zero-filled gradient for the attention output
         return wctx, attn
 
     @staticmethod
     def backward(ctx, dwctx, _dattn):
+        if dwctx is None:
+            return None, None, None, None, None
         h, feat, q, attn, shifted, wsm = ctx.saved_tensors
         W_in, W_s = ctx.params[0], ctx.params[1]
         dq, dfeat, dz = ops.shift_attn_bwd(q, feat.contiguous(), attn, shifted, wsm, dwctx.contiguous(),
@@ -415,10 +418,13 @@ class SoftDotTildeFn(torch.autograd.Function):
             ctx.save_for_backward(h, c, q, probs, cat, y)
             ctx.params = _Kept((W_in, W_out))
         ctx.mark_non_differentiable(probs)
+        ctx.set_materialize_grads(False)     # no zero-filled gradient for the attention weights
         return y, probs
 
     @staticmethod
     def backward(ctx, dy, _dalpha):
+        if dy is None:
+            return None, None, None, None, None
         h, c, q, probs, cat, y = ctx.saved_tensors
         W_in, W_out = ctx.params
         dz = ops.act_bwd(y, dy.contiguous(), "tanh")
@@ -455,6 +461,7 @@ class SoftDotFn(torch.autograd.Function):
         ctx.want_scores = want_scores
         if not want_scores:
             ctx.mark_non_differentiable(probs)
+        ctx.set_materialize_grads(False)     # backward takes None for an output without gradient
         return wctx, (scores if want_scores else probs)
 
     @staticmethod
@@ -515,10 +522,15 @@ class PolicyHeadFn(torch.autograd.Function):
         if action is None:   # teacher mode: no action drawn
             action = torch.empty(0, dtype=torch.int64, device=logit.device)
         ctx.mark_non_differentiable(action)
+        # the kernel takes a null pointer for a loss term without gradient (a teacher rollout's entropy and
+        # log-probability): no zero-filled [B] tensors per step
+        ctx.set_materialize_grads(False)
         return ce, ent, lpa, action
 
     @staticmethod
     def backward(ctx, d_ce, d_ent, d_lpa, _d_action):
+        if d_ce is None and d_ent is None and d_lpa is None:
+            return None, None, None, None, None, None, None
         logp, lens, target, action, ent = ctx.saved_tensors
         if action is not None and action.numel() == 0:
             action = None
@@ -553,10 +565,13 @@ class LSTMCellFn(torch.autograd.Function):
             ctx.save_for_backward(xcat, h, c, c1, act)
             ctx.params = _Kept((W_ih, W_hh, b_ih, b_hh))
         ctx.E = E
+        ctx.set_materialize_grads(False)     # the cell kernel takes null dh / dc (the last step's c1)
         return h1, c1
 
     @staticmethod
     def backward(ctx, dh1, dc1):
+        if dh1 is None and dc1 is None:
+            return (None,) * 8
         xcat, h, c, c1, act = ctx.saved_tensors
         W_ih, W_hh = ctx.params[0], ctx.params[1]
         dgates, dc_prev = ops.lstm_cell_bwd(act, c, c1, dh1, dc1)
@@ -721,6 +736,7 @@ class BiLSTMFn(torch.autograd.Function):
             ctx.save_for_backward(x, lengths_i32, out, saved[0], saved[1], W_ih_f, W_hh_f, W_ih_b, W_hh_b)
             ctx.params = _Kept((W_ih_f, W_hh_f, b_ih_f, b_hh_f, W_ih_b, W_hh_b, b_ih_b, b_hh_b))
         ctx.H = H
+        ctx.set_materialize_grads(False)     # h_n / c_n usually carry no gradient: null carries, no fills
         return out, h_n, c_n
 
     @staticmethod
@@ -729,6 +745,8 @@ class BiLSTMFn(torch.autograd.Function):
         H = ctx.H
         B, L, E = x.shape
         n = ctx.needs_input_grad
+        if dout is None and dh_n is None and dc_n is None:
+            return (None,) * 10
         if _BPTT.active and (not n[0] or _BPTT.dx):
             _BPTT.items.append(dict(x=x, lens=lens, out=out, sa=sa, sc=sc, params=ctx.params, needs=n,
                                     dout=dout.contiguous() if dout is not None else None,

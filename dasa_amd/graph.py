@@ -223,6 +223,7 @@ class _BridgeFn(torch.autograd.Function):
         nd = [o for o in outs if o is not None and not o.is_floating_point()]
         if nd:
             ctx.mark_non_differentiable(*nd)
+        ctx.set_materialize_grads(False)    # an output nobody differentiates arrives as None, not zeros
         return outs
 
     @staticmethod
