@@ -1115,7 +1115,7 @@ bool bad_common(const float* q, const float* ctx, int64_t ldn, int B, int N, int
 }  // namespace
 
 extern "C" int dasa_attn_set_mode(int32_t mode) {
-  if (mode < 0 || mode > 3) return (int)hipErrorInvalidValue;
+  if (mode < 0 || mode > 4) return (int)hipErrorInvalidValue;
   g_attn_mode = mode;
   return 0;
 }
@@ -1188,7 +1188,8 @@ extern "C" int dasa_shift_attn_fwd(const float* q, const float* ctx, int64_t ldn
     return (int)hipErrorInvalidValue;
   FwdArgs a{q, ctx, (long)ldn, nullptr, shift_logits, K, nullptr, attn, shifted, wsm, wctx, N, D};
   if (rows_ok(B, N, D)) return launch_rows(a, B, (hipStream_t)stream);
-  if (split2_ok(B, N, D)) return launch_split2_fwd(a, B, ws, (hipStream_t)stream);
+  // (A/B) 4: the row-split kernel instead of the two-launch D-split form
+  if (g_attn_mode != 4 && split2_ok(B, N, D)) return launch_split2_fwd(a, B, ws, (hipStream_t)stream);
   return launch_fwd<12>(a, B, ws, (hipStream_t)stream);
 }
 

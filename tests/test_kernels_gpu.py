@@ -236,13 +236,14 @@ def test_mha_bwd_vs_autograd(dev, Lq, Lk, p):
         assert (got - ref).abs().max() < 1e-4 * max(1.0, ref.abs().max().item())
 
 
-@pytest.fixture(params=["split", "rowsplit", "split2"])
+@pytest.fixture(params=["split", "rowsplit", "split2", "rowsplit_fwd"])
 def attn_mode(request, dev):
     """The attention implementations (include/dasa_hip.h dasa_attn_set_mode): the D-split forms the
-    decision step uses at small B (mode 0), the row-split form (large B, N > 80; mode 1), and mode 2:
-    the two-launch D-split forward for SoftDot as well (masks, N up to 80, strided rows)."""
+    decision step uses at small B (mode 0), the row-split form (large B, N > 80; mode 1), mode 2: the
+    two-launch D-split forward for SoftDot as well (masks, N up to 80, strided rows), mode 4: the shift
+    forward on the row-split kernel too."""
     from dasa_amd import ops
-    ops.attn_set_mode({"split": 0, "rowsplit": 1, "split2": 2}[request.param])
+    ops.attn_set_mode({"split": 0, "rowsplit": 1, "split2": 2, "rowsplit_fwd": 4}[request.param])
     yield request.param
     ops.attn_set_mode(0)
 

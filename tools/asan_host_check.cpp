@@ -118,8 +118,8 @@ int main() {
                              nullptr) == kInval, "shift K > 15", 16);
   expect(dasa_shift_attn_bwd(fp(0x10), fp(0x20), 2176, nullptr, nullptr, nullptr, fp(0x50), nullptr, nullptr, fp(0x60), 0,
                              2, 2176, 5, ws, nullptr) == kInval, "shift_bwd no attn", 0);
-  for (int m : {0, 1, 2, 3}) expect(dasa_attn_set_mode(m) == 0, "dasa_attn_set_mode", m);
-  expect(dasa_attn_set_mode(4) == kInval, "dasa_attn_set_mode 4", 4);
+  for (int m : {0, 1, 2, 3, 4}) expect(dasa_attn_set_mode(m) == 0, "dasa_attn_set_mode", m);
+  expect(dasa_attn_set_mode(5) == kInval, "dasa_attn_set_mode 5", 5);
   expect(dasa_attn_set_mode(-1) == kInval, "dasa_attn_set_mode -1", -1);
   dasa_attn_set_mode(0);
   expect(dasa_attn_debug_buffer(fp(0x10), 16) == kInval, "debug buffer too small", 16);
