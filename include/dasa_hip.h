@@ -173,7 +173,8 @@ int dasa_mha_bwd(const float* Q, int64_t ldq, const float* K, int64_t ldk, const
  * kernel, the r04 row-split failure), and every form is bitwise reproducible under that load.
  * dasa_attn_set_mode: 0 = automatic (the default; DASA_ATTN_SPLIT=0 in the environment starts in
  * mode 1), 1 = row-split only, 2 = 0 with the D-split SoftDot forward, 3 = row-split only with
- * the r04 per-row-address loads (diagnosis, tools/rowsplit_diag.py). Host-only setting.            */
+ * the r04 per-row-address loads (diagnosis, tools/rowsplit_diag.py), 4 = 0 with the shift forward on
+ * the row-split kernel as well (A/B, tools/attn_mode_ab.py). Host-only setting.                     */
 int64_t dasa_attn_workspace(int32_t B, int32_t N, int32_t D);
 int dasa_attn_set_mode(int32_t mode);
 /* Diagnosis hook (r05, tools/rowsplit_diag.py): arm a device buffer of `bytes` (16-B aligned) that the
