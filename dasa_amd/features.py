@@ -128,6 +128,54 @@ class DeviceFeatureStore:
         B = len(obs)
         return a_t, f_t, d_t, cf.view(B, C, -1), cd.view(B, C, -1), leng
 
+    def _step_arrays(self, obs, base):
+        """One step's host-side index blocks, vectorised over the batch (the per-observation loop was
+        ≈0.2 ms of host time per decision step, all of it GPU idle in the sampled rollout, which waits on
+        it after every action sync): candidate gather rows iac / ibc [B, C] (-1 = padding), candidate
+        angles cang [B, C, A], own-angle rows a_t [B, A], viewpoint rows, view indices, C, lengths."""
+        A, V = self.A, 36
+        B = len(obs)
+        vp = np.fromiter((self._row(ob) for ob in obs), np.int64, B)
+        view = np.fromiter((ob["viewIndex"] for ob in obs), np.int64, B)
+        cand = [self._cand_arrays(ob["candidate"]) for ob in obs]
+        ns = np.fromiter((len(p) for p, _ in cand), np.int64, B)
+        leng = (ns + 1).tolist()
+        C = int(ns.max()) + 1 if B else 1
+        a_t = np.stack([self._angle(ob["heading"], ob["elevation"]) for ob in obs]).astype(np.float32, copy=False)
+        iac = np.full((B, C), -1, np.int32)
+        ibc = np.full((B, C), -1, np.int32)
+        cang = np.zeros((B, C, A), np.float32)
+        tot = int(ns.sum())
+        if tot:
+            rows = np.repeat(np.arange(B), ns)
+            cols = np.arange(tot) - np.repeat(np.cumsum(ns) - ns, ns)
+            iac[rows, cols] = (vp[rows] * V + np.concatenate([p for p, _ in cand])).astype(np.int32)
+            ibc[rows, cols] = (base + rows * C + cols).astype(np.int32)
+            cang[rows, cols] = np.concatenate([a for _, a in cand if len(a)])
+        return iac, ibc, cang, a_t, vp, view, C, leng
+
+    def _step_arrays_loop(self, obs, base):
+        """The per-observation form of _step_arrays (test reference)."""
+        A = self.A
+        B = len(obs)
+        leng = [len(ob["candidate"]) + 1 for ob in obs]
+        C = max(leng)
+        vp = np.array([self._row(ob) for ob in obs], np.int64)
+        view = np.array([ob["viewIndex"] for ob in obs], np.int64)
+        iac = np.full((B, C), -1, np.int32)
+        ibc = np.full((B, C), -1, np.int32)
+        cang = np.zeros((B, C, A), np.float32)
+        a_t = np.zeros((B, A), np.float32)
+        for i, ob in enumerate(obs):
+            a_t[i] = self._angle(ob["heading"], ob["elevation"])
+            pts, angs = self._cand_arrays(ob["candidate"])
+            n = len(pts)
+            if n:
+                iac[i, :n] = vp[i] * 36 + pts
+                ibc[i, :n] = base + i * C + np.arange(n, dtype=np.int32)
+                cang[i, :n] = angs
+        return iac, ibc, cang, a_t, vp, view, C, leng
+
     def input_feat_steps(self, obs_steps):
         """The input blocks of several rollout steps stacked along the batch (step-major): a_t [T*B, A],
         panoramas f_t / d_t [T*B, 36, F+A], and the candidates of every step as flat rows cf / cd [R, F+A]
@@ -142,24 +190,9 @@ class DeviceFeatureStore:
         base = 0
         for obs in obs_steps:
             B = len(obs)
-            leng = [len(ob["candidate"]) + 1 for ob in obs]
-            C = max(leng)
-            vp = np.array([self._row(ob) for ob in obs], np.int64)
-            view = np.array([ob["viewIndex"] for ob in obs], np.int64)
+            iac, ibc, cang, a_t, vp, view, C, leng = self._step_arrays(obs, base)
             ia_v.append((vp[:, None] * V + rv[None]).astype(np.int32).reshape(-1))
             ib_v.append((view[:, None] * V + rv[None]).astype(np.int32).reshape(-1))
-            iac = np.full((B, C), -1, np.int32)
-            ibc = np.full((B, C), -1, np.int32)
-            cang = np.zeros((B, C, A), np.float32)
-            a_t = np.zeros((B, A), np.float32)
-            for i, ob in enumerate(obs):
-                a_t[i] = self._angle(ob["heading"], ob["elevation"])
-                pts, angs = self._cand_arrays(ob["candidate"])
-                n = len(pts)
-                if n:
-                    iac[i, :n] = vp[i] * V + pts
-                    ibc[i, :n] = base + i * C + np.arange(n, dtype=np.int32)
-                    cang[i, :n] = angs
             base += B * C
             ia_c.append(iac.reshape(-1))
             ib_c.append(ibc.reshape(-1))

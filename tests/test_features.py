@@ -119,3 +119,24 @@ def test_device_store_matches_host_assembly(dev):
         assert torch.equal(f_t[t * B:(t + 1) * B].cpu(), torch.from_numpy(want[1]))
         assert torch.equal(cd[off:off + B * C].view(B, C, -1).cpu(), torch.from_numpy(want[4]))
         assert leng == want[5]
+
+
+def test_step_arrays_vectorised_matches_loop():
+    """DeviceFeatureStore._step_arrays (the batch-vectorised host index blocks of one decision step) equals
+    the per-observation loop it replaced, including observations with no candidates and ragged C."""
+    img, keys, vals = GI.io_tables()
+    depth = {f"{a}_{b}": vals[i] for i, (a, b) in enumerate(keys)}
+    both = sorted(set(img) & set(depth))
+    img = {k: img[k] for k in both}
+    store = FE.DeviceFeatureStore.from_features(img, depth, torch.device("cpu"))
+    rng = np.random.default_rng(7)
+    for t in range(4):
+        obs = _obs(img, depth, [both[(i * 3 + t) % len(both)] for i in range(6)], rng)
+        if t == 2:
+            obs[1]["candidate"] = []
+        base = 17 * t
+        got = store._step_arrays(obs, base)
+        want = store._step_arrays_loop(obs, base)
+        for g, w in zip(got[:6], want[:6]):
+            assert g.dtype == w.dtype and np.array_equal(g, w), t
+        assert got[6:] == want[6:]
