@@ -162,7 +162,7 @@ class StepGraphs:
 
 # ------------------------------------------------------------------ training-mode (autograd) regions
 class _Slot:
-    __slots__ = ("graph", "static_in", "static_out", "counter", "pkey", "fills", "shapes", "leaves", "bwd", "owner")
+    __slots__ = ("graph", "static_in", "static_out", "counter", "pkey", "fills", "shapes", "leaves", "bwd", "owner", "pool")
 
 
 class _Bwd:
@@ -334,7 +334,6 @@ class AutogradGraphs:
         self.slots = {}
         self.uses = {}
         self.stream = None
-        self.pool = None
         self._alias = {}
         self.captures = 0
         self.captures_bwd = 0
@@ -384,8 +383,12 @@ class AutogradGraphs:
         dev = next(x for x in inputs if x is not None).device
         if self.stream is None:
             self.stream = torch.cuda.Stream(device=dev)
-            self.pool = torch.cuda.graph_pool_handle()
         slot = _Slot()
+        # a memory pool of the slot's own, shared only by its forward and backward graphs: those replay in
+        # their capture order every iteration (forward, then backward). One pool across slots would let a
+        # slot captured later (a new key mid-rollout) place its saved tensors in an earlier-captured slot's
+        # freed temporaries, which that slot's next replay overwrites before the backward reads them
+        slot.pool = torch.cuda.graph_pool_handle()
         slot.counter = torch.zeros(1, dtype=torch.int64, device=dev)
         slot.fills, slot.shapes = {}, {}
         static_in = []
@@ -416,7 +419,7 @@ class AutogradGraphs:
             ctr = ctypes.c_void_p(slot.counter.data_ptr())
             L.dasa_set_seed_source(ctr)
             try:
-                with self._aliased(), _no_gc(), _graph(g, pool=self.pool, stream=self.stream), \
+                with self._aliased(), _no_gc(), _graph(g, pool=slot.pool, stream=self.stream), \
                         torch.enable_grad():
                     _lib.check(L.dasa_seed_bump(ctr, ctypes.c_void_p(self.stream.cuda_stream)), "dasa_seed_bump")
                     out = fn(*static_in)
@@ -452,7 +455,7 @@ class AutogradGraphs:
         ops._FRESH_PLANES[0] += 1
         L.dasa_set_seed_source(ctypes.c_void_p(slot.counter.data_ptr()))
         try:
-            with _no_gc(), _graph(g, pool=self.pool, stream=self.stream):
+            with _no_gc(), _graph(g, pool=slot.pool, stream=self.stream):
                 gl = torch.autograd.grad(outs, slot.leaves, bw.gin, retain_graph=True, allow_unused=True)
         finally:
             L.dasa_set_seed_source(None)

@@ -182,3 +182,37 @@ def test_captured_backward_regenerates_replay_masks(dev, monkeypatch, bwd_graph)
         lin.bias.grad = None
     assert g.captures == 1 and g.captures_bwd == (1 if bwd_graph else 0)
     assert not torch.equal(seen[0], seen[1])        # fresh masks per replay
+
+
+@pytest.mark.parametrize("bwd_graph", [True, False])
+def test_slot_captured_mid_iteration_keeps_saved_tensors(dev, monkeypatch, bwd_graph):
+    """A slot captured in a later iteration between replays of earlier slots (a new step key mid-rollout)
+    keeps the tensors its backward saved. Each region saves tanh(x) and frees a same-sized temporary at
+    the end of its capture; with one memory pool across slots, the new slot's saved tensor could land in an
+    earlier slot's freed temporary, which that slot's next replay overwrites before the backward reads it.
+    Gradients are checked against the region's closed form."""
+    from dasa_amd import graph
+    monkeypatch.setattr(graph, "BWD_GRAPH", bwd_graph)
+    torch.manual_seed(11)
+    g = graph.AutogradGraphs([])
+
+    def fn(x):
+        h = torch.tanh(x)                           # saved by tanh's backward
+        with torch.no_grad():
+            s = (h.abs() + 1.0).sum(1, keepdim=True)    # temporary freed at the end of the capture
+        return (h * s,)
+
+    def expect(x, gy):
+        h = torch.tanh(x.detach())
+        s = (h.abs() + 1.0).sum(1, keepdim=True)
+        return (1 - h * h) * s * gy
+
+    for keys in (("a", "b"), ("a", "c", "b"), ("a", "c", "b")):
+        g.new_iteration()
+        xs = [torch.randn(64, 256, device=dev, requires_grad=True) for _ in keys]
+        ys = [g.run(k, fn, (x,))[0] for k, x in zip(keys, xs)]
+        gys = [torch.randn_like(y) for y in ys]
+        torch.autograd.backward(ys, gys)
+        for k, x, gy in zip(keys, xs, gys):
+            torch.testing.assert_close(x.grad, expect(x, gy), rtol=1e-5, atol=1e-5, msg=lambda m: f"{keys} {k}: {m}")
+    assert g.captures == 3
