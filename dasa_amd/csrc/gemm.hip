@@ -1442,6 +1442,148 @@ void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
   store_tile_mf<16, TM, TN, BM, BN>(p, big, b, 0, m0, n0, wm, wn, lane);
 }
 
+// Register-A form (forms 21, 22): LDS holds only the pre-split W planes. Each wave reads its own A
+// fragments from global memory straight into registers in the 16x16x32 operand layout (lane l: row
+// l & 15 of the fragment, the 8 fp32 of K group l >> 4 — 16 rows x 128 contiguous bytes per fragment) and
+// splits them into hi / mid / lo in registers. Form 8 per 32-deep K step moves, per CU, 48 KB into LDS
+// (A's three planes + W's) and 18 ds_read_b128 per wave out of it: ~1200 LDS cycles against 768 MFMA
+// cycles per SIMD — LDS-bound. Here the A planes never touch LDS: 24 KB in and 12 reads per wave out.
+// The cost moves to VALU (each of the WAVES_N waves sharing an A row splits it) and to L1/L2 (each
+// A row fetched by WAVES_N waves). Same products in the same order with the same two accumulators as
+// form 8: bitwise equal to it. Ring: W(t+1) sits in registers while tile t computes and goes to the
+// other LDS stage after it; A(t+2) is loaded into the register stage tile t has just consumed.
+// MEASURED AND REJECTED (sweeps only, profiles/r05/x6_register_a_forms.log): 0.75-0.85x form 8 / 20 for
+// 128 x 128 with 8 waves (form 22), 0.55-0.6x with 4 waves of 64 x 64 (form 21) on the many-tile shapes —
+// the LDS budget above is not what bounds form 8; the per-wave fragment loads (one K step of lookahead,
+// half-sector 16-B accesses) and the duplicated split cost more than the LDS traffic they remove.
+template <int BM, int BN, int WAVES_M, int WAVES_N, int OCC = 2>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) __attribute__((amdgpu_waves_per_eu(1, OCC)))
+void gemm_f32x6_ra_kernel(GemmP p, long plane) {
+  constexpr int NT = 64 * WAVES_M * WAVES_N;
+  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N, TM = WM / 16, TN = WN / 16;
+  constexpr int NB = BN * 4 / NT;
+  static_assert((BN * 4) % NT == 0 && WM % 16 == 0 && WN % 16 == 0, "tile must split evenly");
+  constexpr int PB = BN * 4;                 // uint4 per W plane image
+  constexpr int STAGE = 3 * PB;
+  __shared__ uint4 smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave / WAVES_N) * WM, wn = (wave % WAVES_N) * WN;
+  const int wgid = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+  int m0, n0;
+  if (p.group_m > 1) {
+    const int gm = p.group_m, per = gm * gridDim.x, grp = wgid / per;
+    const int rows = min(gm, (int)gridDim.y - grp * gm), r = wgid - grp * per;
+    m0 = (grp * gm + r % rows) * BM;
+    n0 = (r / rows) * BN;
+  } else if (p.group_m < -1) {
+    const int gn = -p.group_m, per = gn * gridDim.y, grp = wgid / per;
+    const int cols = min(gn, (int)gridDim.x - grp * gn), r = wgid - grp * per;
+    n0 = (grp * gn + r % cols) * BN;
+    m0 = (r / cols) * BM;
+  } else {
+    n0 = (wgid % gridDim.x) * BN;
+    m0 = (wgid / gridDim.x) * BM;
+  }
+  const int b = blockIdx.z;
+  const float* A = p.A + (long)b * p.sA;
+  const unsigned short* W = reinterpret_cast<const unsigned short*>(p.B) + (long)b * p.sB;
+
+  floatx4 big[TM][TN], small[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) big[i][j] = small[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  struct ARegs {
+    u32x4 a[TM][2];
+    __device__ __forceinline__ void load(const GemmP& p, const float* A, int m0, int wm, int lane, int k0) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const float* src = A + (long)min(m0 + wm + 16 * i + (lane & 15), p.M - 1) * p.lda + k0 + 8 * (lane >> 4);
+        a[i][0] = *reinterpret_cast<const u32x4*>(src);
+        a[i][1] = *reinterpret_cast<const u32x4*>(src + 4);
+      }
+    }
+  } ra0, ra1;
+  struct WRegs {
+    u32x4 w[3][NB];
+    __device__ __forceinline__ void load(const GemmP& p, const unsigned short* W, long plane, int n0, int k0, int tid) {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const int u = tid + NT * i, q = (u >> 3) & 3, row = (u & 7) + 8 * (u >> 5);
+        const unsigned short* src = W + (long)min(n0 + row, p.N - 1) * p.ldb + k0 + 8 * q;
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) w[pl][i] = *reinterpret_cast<const u32x4*>(src + pl * plane);
+      }
+    }
+    __device__ __forceinline__ void store(uint4* S, int tid) const {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const int u = tid + NT * i, q = (u >> 3) & 3, row = (u & 7) + 8 * (u >> 5);
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) S[pl * PB + q * BN + row] = __builtin_bit_cast(uint4, w[pl][i]);
+      }
+    }
+  } rw;
+
+  auto compute = [&](const uint4* S, const ARegs& ar) {
+    const int q = lane >> 4;
+    bf16x8_t bf[3][TN];
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bf[pl][j] = __builtin_bit_cast(bf16x8_t, S[pl * PB + q * BN + wn + 16 * j + (lane & 15)]);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      uint4 h, m, l;
+      split3_quad(__builtin_bit_cast(float4, ar.a[i][0]), __builtin_bit_cast(float4, ar.a[i][1]), h, m, l);
+      const bf16x8_t af[3] = {__builtin_bit_cast(bf16x8_t, h), __builtin_bit_cast(bf16x8_t, m),
+                              __builtin_bit_cast(bf16x8_t, l)};
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        floatx4& sm = small[i][j];
+        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bf[1][j], sm, 0, 0, 0);
+        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[2][j], sm, 0, 0, 0);
+        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2], bf[0][j], sm, 0, 0, 0);
+        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[1][j], sm, 0, 0, 0);
+        sm = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bf[0][j], sm, 0, 0, 0);
+        big[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[0][j], big[i][j], 0, 0, 0);
+      }
+    }
+  };
+
+  const int nk = p.K / 32;
+  rw.load(p, W, plane, n0, 0, tid);
+  ra0.load(p, A, m0, wm, lane, 0);
+  rw.store(smem, tid);
+  __syncthreads();
+  const int k1 = 32 * min(1, nk - 1);
+  rw.load(p, W, plane, n0, k1, tid);
+  ra1.load(p, A, m0, wm, lane, k1);
+  for (int t = 0; t < nk; t += 2) {
+    compute(smem, ra0);
+    rw.store(smem + STAGE, tid);                       // W(t + 1) -> the stage tile t - 1 used
+    int kn = 32 * min(t + 2, nk - 1);                  // clamped re-reads past the end
+    rw.load(p, W, plane, n0, kn, tid);
+    ra0.load(p, A, m0, wm, lane, kn);
+    __syncthreads();
+    if (t + 1 >= nk) break;
+    compute(smem + STAGE, ra1);
+    rw.store(smem, tid);
+    kn = 32 * min(t + 3, nk - 1);
+    rw.load(p, W, plane, n0, kn, tid);
+    ra1.load(p, A, m0, wm, lane, kn);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) big[i][j] += small[i][j];
+  store_tile_mf<16, TM, TN, BM, BN>(p, big, b, 0, m0, n0, wm, wn, lane);
+}
+
 // All-DMA form (form 16, sweeps only: 0.80-0.90x form 8 on the 12800-row shapes, profiles/r03/
 // x6_dma_form.txt): the same tile, products, product order and epilogue as form 8 (bitwise equal),
 // but nothing is staged through VGPRs or written by ds_write: A (fp32) and the pre-split W planes go
@@ -2590,6 +2732,8 @@ static int x6_run(const dasa_gemm_desc* d, X6Plan pl, int64_t plane, void* ws, i
     case 15: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, false, 2>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
     case 16: hipLaunchKernelGGL((gemm_f32x6_dma_kernel<128, 128, 4, 2>), grid, dim3(512), 0, st, p, (long)plane); break;
     case 20: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true, -1>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
+    case 21: hipLaunchKernelGGL((gemm_f32x6_ra_kernel<128, 128, 2, 2>), grid, dim3(256), 0, st, p, (long)plane); break;
+    case 22: hipLaunchKernelGGL((gemm_f32x6_ra_kernel<128, 128, 4, 2>), grid, dim3(512), 0, st, p, (long)plane); break;
     default: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
   }
   DASA_CHECK_LAUNCH();
