@@ -219,6 +219,8 @@ class _BridgeFn(torch.autograd.Function):
         slot.graph.replay()
         ctx.slot = slot
         ctx.shapes = [x.shape if x is not None else None for x in inputs]
+        # a leaf input may keep the returned gradient as its .grad: it gets a copy, not the static buffer
+        ctx.leaf = [x is not None and x.is_leaf and x.requires_grad for x in inputs]
         outs = _copies(slot.static_out)
         nd = [o for o in outs if o is not None and not o.is_floating_point()]
         if nd:
@@ -260,9 +262,13 @@ class _BridgeFn(torch.autograd.Function):
             got = {id(v): g for v, g in zip(slot.leaves, gl) if g is not None}
             _accumulate_params(slot, got)
         res = []
-        for s, shape in zip(slot.static_in, ctx.shapes):
+        for s, shape, leaf in zip(slot.static_in, ctx.shapes, ctx.leaf):
             g = got.get(id(s)) if s is not None and s.requires_grad else None
-            res.append(_lead(g, shape) if g is not None else None)
+            if g is not None:
+                g = _lead(g, shape)
+                res.append(g.clone() if leaf else g)
+            else:
+                res.append(None)
         return (None,) + tuple(res)
 
 

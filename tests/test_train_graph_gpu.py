@@ -207,6 +207,7 @@ def test_slot_captured_mid_iteration_keeps_saved_tensors(dev, monkeypatch, bwd_g
         s = (h.abs() + 1.0).sum(1, keepdim=True)
         return (1 - h * h) * s * gy
 
+    kept = []
     for keys in (("a", "b"), ("a", "c", "b"), ("a", "c", "b")):
         g.new_iteration()
         xs = [torch.randn(64, 256, device=dev, requires_grad=True) for _ in keys]
@@ -215,4 +216,7 @@ def test_slot_captured_mid_iteration_keeps_saved_tensors(dev, monkeypatch, bwd_g
         torch.autograd.backward(ys, gys)
         for k, x, gy in zip(keys, xs, gys):
             torch.testing.assert_close(x.grad, expect(x, gy), rtol=1e-5, atol=1e-5, msg=lambda m: f"{keys} {k}: {m}")
+            kept.append((x, gy))
     assert g.captures == 3
+    for x, gy in kept:      # a leaf's .grad is its own tensor, not a static buffer later replays rewrite
+        torch.testing.assert_close(x.grad, expect(x, gy), rtol=1e-5, atol=1e-5)
