@@ -403,7 +403,9 @@ struct PBwd {
 // rec[b][j] = sum_n dgates_prev[b][n] W_hh[n][j] with v_mfma_f32_16x16x4_f32: rows b (two 16-row
 // tiles), cols j (the workgroup's 8 units, padded to 16), K = 4H split over the 16 waves (4H/16 each,
 // NGB = 4H/256 K-groups of 16). W_hh[:, j-slice] lives in VGPRs in the K-permuted B-operand layout.
-template <int NGB>
+// T2 = false (B <= 16, the finetune rollout's B = 2): one row tile — half the hand-off loads and MFMAs, and
+// the loads of eight K-groups (not four) in flight per round trip, so a step waits on half as many.
+template <int NGB, bool T2 = true>
 __global__ __launch_bounds__(1024) void bilstm_persist_bwd_kernel(PBwd a) {
   __shared__ __attribute__((aligned(16))) float smem[PW * 512 + 4];
   const int H = a.H, B = a.B, L = a.L, G = H / PU, G4 = 4 * H;
@@ -463,6 +465,20 @@ __global__ __launch_bounds__(1024) void bilstm_persist_bwd_kernel(PBwd a) {
       const int tp = dir == 0 ? t + 1 : t - 1;   // the step processed just before (BPTT order)
       const int base0 = (((b0 * L + tp) * 2 + dir) * G4 + k0 + 4 * kq) * 4;
       const int base1 = (((b1 * L + tp) * 2 + dir) * G4 + k0 + 4 * kq) * 4;
+      if constexpr (!T2) {
+        constexpr int CH = NGB % 8 == 0 ? 8 : 4;
+#pragma unroll
+        for (int g0 = 0; g0 < NGB; g0 += CH) {
+          float4 x0[CH];
+#pragma unroll
+          for (int g = 0; g < CH; ++g) x0[g] = selz(v0, ld_sc1(rs, base0 + 64 * (g0 + g)));
+#pragma unroll
+          for (int g = 0; g < CH; ++g)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(f4e(x0[g], e), f4e(wf[g0 + g], e), acc0, 0, 0, 0);
+        }
+      } else {
 #pragma unroll
       for (int g0 = 0; g0 < NGB; g0 += 4) {
         float4 x0[4], x1[4];
@@ -478,6 +494,7 @@ __global__ __launch_bounds__(1024) void bilstm_persist_bwd_kernel(PBwd a) {
             acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(f4e(x0[g], e), f4e(wf[g0 + g], e), acc0, 0, 0, 0);
             acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(f4e(x1[g], e), f4e(wf[g0 + g], e), acc1, 0, 0, 0);
           }
+      }
       }
     }
     // 16x16 C map: col = lane & 15 (unit), row = 4 * (lane >> 4) + reg (batch within the tile)
@@ -658,12 +675,29 @@ int bilstm_persist_fwd(const float* xproj, const float* whh_fwd, const float* wh
   }
 }
 
+// the persistent BPTT's one-row-tile form at B <= 16 (dasa_bilstm_bptt_one_tile; env DASA_BPTT_ONE_TILE=0
+// starts at 0: the two-tile form at every B)
+static int g_bwd_one_tile = -1;
+static bool bwd_one_tile() {
+  if (g_bwd_one_tile < 0) {
+    const char* e = getenv("DASA_BPTT_ONE_TILE");
+    g_bwd_one_tile = !(e && e[0] == '0');
+  }
+  return g_bwd_one_tile != 0;
+}
+extern "C" int dasa_bilstm_bptt_one_tile(int32_t on) {
+  const int prev = bwd_one_tile() ? 1 : 0;
+  if (on >= 0) g_bwd_one_tile = on ? 1 : 0;
+  return prev;
+}
+
 int bilstm_persist_bwd(const float* whh_fwd, const float* whh_bwd, const int32_t* lengths, const float* save_act,
                        const float* save_c, const float* dout, const float* dh_n, const float* dc_n, float* dgates,
                        int B, int L, int H, unsigned* sync, hipStream_t st) {
   PBwd a{whh_fwd, whh_bwd, lengths, save_act, save_c, dout, dh_n, dc_n, dgates, sync, g_err_word, g_force_tmo,
          B, L, H};
   const int grid = 2 * H / PU;
+  if (B <= 16 && H == 1024 && bwd_one_tile()) return launch_persistent(bilstm_persist_bwd_kernel<16, false>, grid, a, st);
   switch (H / 64) {   // NGB = 4H / 256
     case 4: return launch_persistent(bilstm_persist_bwd_kernel<4>, grid, a, st);
     case 8: return launch_persistent(bilstm_persist_bwd_kernel<8>, grid, a, st);

@@ -240,6 +240,11 @@ int dasa_bilstm_set_mode(int mode);
  * pre-split per call (default; env DASA_BPTT_X6=0 or DASA_GEMM_EMU=0 start at 0), 0 = dasa_gemm_f32;
  * < 0 only queries. Returns the previous setting. Host-only.                                     */
 int dasa_bilstm_bptt_x6(int32_t on);
+/* Persistent BPTT (B <= 32) at H = 1024, B <= 16: 1 = one 16-row tile of the recurrent product (half the
+ * hand-off loads and MFMAs of the two-tile form, the same products in the same order: bitwise equal;
+ * default; env DASA_BPTT_ONE_TILE=0 starts at 0), 0 = the two-tile form; < 0 only queries. Returns the
+ * previous setting. Host-only.                                                                     */
+int dasa_bilstm_bptt_one_tile(int32_t on);
 /* Persistent forward recurrence at H = 1024, B <= 64: 1 = recurrent product as bf16x6 (three exact bf16 planes of
  * h and W_hh, six products on bf16 MFMA; fp32-accurate; default; env DASA_LSTM_X6=0 or DASA_GEMM_EMU=0
  * start at 0), 0 = native fp32 MFMA; < 0 only queries. Returns the previous setting. Host-only.   */

@@ -78,7 +78,7 @@ def test_x6_plan_and_lstm_switches_are_host_only():
     assert L.dasa_gemm_f32x6_workspace(ctypes.byref(d)) > 0          # 36 tiles: K split over workgroups
     d.M, d.N, d.K = 12800, 3072, 768
     assert L.dasa_gemm_f32x6_workspace(ctypes.byref(d)) == 0         # 2400 tiles: one workgroup per tile
-    for hook in (L.dasa_bilstm_bptt_x6, L.dasa_bilstm_fwd_x6):
+    for hook in (L.dasa_bilstm_bptt_x6, L.dasa_bilstm_fwd_x6, L.dasa_bilstm_bptt_one_tile):
         prev = hook(-1)
         assert prev in (0, 1)
         assert hook(0) == prev and hook(-1) == 0

@@ -460,6 +460,37 @@ def test_bilstm_bptt_x6_vs_native(dev, B, L):
     assert (dg6 - dgn).abs().max().item() < 2e-5 * scale
 
 
+@pytest.mark.parametrize("B,L", [(2, 80), (16, 23), (5, 1)])
+def test_bilstm_bptt_one_tile_bitwise(dev, B, L):
+    """The persistent BPTT's one-row-tile form (B <= 16, the finetune rollout's B = 2) runs the two-tile
+    form's products in the same order: its dgates equal the two-tile form's bitwise, ragged lengths and a
+    one-step sequence included."""
+    from dasa_amd import _lib, ops
+    lib = _lib.lib()
+    torch.manual_seed(B * 100 + L)
+    H = 1024
+    whh_f, whh_b = [(torch.rand(4 * H, H, device=dev) - 0.5) * 0.1 for _ in range(2)]
+    xproj = torch.randn(B, L, 2, 4 * H, device=dev)
+    li = torch.randint(1, L + 1, (B,)).sort(descending=True)[0].to(torch.int32)
+    li[0] = L
+    li = li.to(dev)
+    assert lib.dasa_bilstm_set_mode(2) == 0
+    prev = lib.dasa_bilstm_bptt_one_tile(1)
+    try:
+        out, h_n, c_n, saved = ops.bilstm_fwd(xproj, whh_f, whh_b, li, H, save=True)
+        gout = torch.randn(B, L, 2 * H, device=dev)
+        ghn, gcn = torch.randn(2, B, H, device=dev), torch.randn(2, B, H, device=dev)
+        dg1 = ops.bilstm_bwd(whh_f, whh_b, li, saved, gout, ghn, gcn, H)
+        lib.dasa_bilstm_bptt_one_tile(0)
+        dg2 = ops.bilstm_bwd(whh_f, whh_b, li, saved, gout, ghn, gcn, H)
+    finally:
+        lib.dasa_bilstm_bptt_one_tile(prev)
+        lib.dasa_bilstm_set_mode(0)
+    torch.cuda.synchronize()
+    assert torch.isfinite(dg1).all()
+    assert torch.equal(dg1, dg2)
+
+
 @pytest.mark.parametrize("input_grads", [False, True])
 def test_bilstm_deferred_input_grads(dev, input_grads):
     """defer_bilstm_backward(input_grads=True) (optim_step's path when the language stack trains, cfg4): three
