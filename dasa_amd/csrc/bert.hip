@@ -476,18 +476,23 @@ __global__ __launch_bounds__(256) void mha_bwd_kernel(MhaArgs a, const float* dO
 // as register-blocked 4x4 outer products over LDS rows (two float4 reads per 16 FMAs). No atomics: the
 // previous form accumulated dK / dV with per-element LDS atomics row by row (0.64 ms per launch at the
 // finetune shapes, B = 2; bench.py cfg4 leg).
+// `parts` workgroups per (b, h) (r05; B x heads far below the CU count, e.g. 24 at the finetune's B = 2):
+// every part computes the whole dS (dP, its row sums, dS — the row sums need whole rows), then only its
+// share of the 4-row blocks of dV / dK (key rows) and dQ (query rows). Each output element is still
+// computed by one workgroup with the same loop order: bitwise equal to parts = 1.
 constexpr int kBwdMaxL = 80;
 constexpr int kBwdLd = kBwdMaxL + 4;   // row stride of [.][Lq] / [.][Lk] tiles
 constexpr int kBwdLdD = kDh + 4;       // row stride of [.][64] tiles
 constexpr int kBwdBufA = (kDh * kBwdLd > kBwdMaxL * kBwdLdD) ? kDh * kBwdLd : kBwdMaxL * kBwdLdD;
 constexpr int kBwdBufL = kBwdMaxL * kBwdLd;
 
-// C[m][n] = sum_k A[k][m] B[k][n] over 4x4 register blocks (A, B row-major in LDS, m / n multiples of 4).
+// C[m][n] = sum_k A[k][m] B[k][n] over 4x4 register blocks (A, B row-major in LDS, m / n multiples of 4),
+// m-blocks mb0 .. mb0 + MB - 1.
 template <typename Epi>
-__device__ __forceinline__ void lds_tn_blocks(const float* A, int lda, const float* B, int ldb, int K, int MB, int NB,
-                                              Epi epi) {
+__device__ __forceinline__ void lds_tn_blocks(const float* A, int lda, const float* B, int ldb, int K, int mb0, int MB,
+                                              int NB, Epi epi) {
   for (int blk = threadIdx.x; blk < MB * NB; blk += blockDim.x) {
-    const int m0 = (blk / NB) * 4, n0 = (blk % NB) * 4;
+    const int m0 = (mb0 + blk / NB) * 4, n0 = (blk % NB) * 4;
     float acc[4][4];
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -507,7 +512,7 @@ __device__ __forceinline__ void lds_tn_blocks(const float* A, int lda, const flo
 }
 
 __global__ __launch_bounds__(256) void mha_bwd_lds_kernel(MhaArgs a, const float* dO, long lddo, float* dQ, float* dK,
-                                                          float* dV) {
+                                                          float* dV, int parts) {
   __shared__ float bufA[kBwdBufA];   // dO^T [64][Lq]; then Q [Lq][64]
   __shared__ float bufB[kBwdBufA];   // V^T [64][Lk]; then K [Lk][64]
   __shared__ float sP[kBwdBufL];     // P [Lq][Lk]; then P_dropped
@@ -516,27 +521,47 @@ __global__ __launch_bounds__(256) void mha_bwd_lds_kernel(MhaArgs a, const float
   __shared__ float sdST[kBwdBufL];   // dS^T [Lk][Lq]
   __shared__ float rowdot[kBwdMaxL];
   const uint64_t sdk = a.p > 0.f ? eff_seed(a.seed, a.seed_src) : 0;   // dropout seed of this launch
-  const int bh = blockIdx.x, b = bh / a.heads, h = bh % a.heads, t = threadIdx.x;
+  const int bh = blockIdx.x / parts, part = blockIdx.x % parts, b = bh / a.heads, h = bh % a.heads, t = threadIdx.x;
   const int Lq = a.Lq, Lk = a.Lk, Lq4 = (Lq + 3) & ~3, Lk4 = (Lk + 3) & ~3;
+  const int kper = (Lk4 / 4 + parts - 1) / parts, kb0 = part * kper, kbn = max(0, min(kper, Lk4 / 4 - kb0));
+  const int qper = (Lq4 / 4 + parts - 1) / parts, qb0 = part * qper, qbn = max(0, min(qper, Lq4 / 4 - qb0));
   const long pbase = ((long)b * a.heads + h) * Lq * Lk;
   const bool drop = a.p > 0.f;
-  for (int idx = t; idx < Lq4 * kDh; idx += blockDim.x) {
-    const int i = idx / kDh, d = idx % kDh;
-    const float v = i < Lq ? dO[((long)b * Lq + i) * lddo + h * kDh + d] : 0.f;
-    sdO[i * kBwdLdD + d] = v;
-    bufA[d * kBwdLd + i] = v;
-  }
-  for (int idx = t; idx < Lk4 * kDh; idx += blockDim.x) {
-    const int j = idx / kDh, d = idx % kDh;
-    bufB[d * kBwdLd + j] = j < Lk ? a.V[((long)b * Lk + j) * a.ldv + h * kDh + d] : 0.f;
-  }
-  for (int idx = t; idx < Lq4 * Lk4; idx += blockDim.x) {
-    const int i = idx / Lk4, j = idx % Lk4;
-    sP[i * kBwdLd + j] = (i < Lq && j < Lk) ? a.probs[pbase + (long)i * Lk + j] : 0.f;
+  // staging: every global load of dO, V and P issued before the first LDS store (fixed trip counts, fully
+  // unrolled: 65 loads in flight per thread, one memory round trip instead of one per loop iteration)
+  constexpr int NR = kBwdMaxL * kDh / 256, NP = kBwdMaxL * kBwdMaxL / 256;
+  static_assert(NR * 256 == kBwdMaxL * kDh && NP * 256 == kBwdMaxL * kBwdMaxL, "staging trip counts");
+  {
+    float vo[NR], vv[NR], vp[NP];
+#pragma unroll
+    for (int it = 0; it < NR; ++it) {
+      const int idx = t + 256 * it, i = idx / kDh, d = idx % kDh;
+      vo[it] = i < Lq ? dO[((long)b * Lq + i) * lddo + h * kDh + d] : 0.f;
+      vv[it] = i < Lk ? a.V[((long)b * Lk + i) * a.ldv + h * kDh + d] : 0.f;
+    }
+#pragma unroll
+    for (int it = 0; it < NP; ++it) {
+      const int idx = t + 256 * it, i = idx / Lk4, j = idx % Lk4;
+      vp[it] = (i < Lq && j < Lk) ? a.probs[pbase + (long)i * Lk + j] : 0.f;
+    }
+#pragma unroll
+    for (int it = 0; it < NR; ++it) {
+      const int idx = t + 256 * it, i = idx / kDh, d = idx % kDh;
+      if (i < Lq4) {
+        sdO[i * kBwdLdD + d] = vo[it];
+        bufA[d * kBwdLd + i] = vo[it];
+      }
+      if (i < Lk4) bufB[d * kBwdLd + i] = vv[it];
+    }
+#pragma unroll
+    for (int it = 0; it < NP; ++it) {
+      const int idx = t + 256 * it, i = idx / Lk4, j = idx % Lk4;
+      if (idx < Lq4 * Lk4) sP[i * kBwdLd + j] = vp[it];
+    }
   }
   __syncthreads();
   // dP (masked by the forward's dropout scale) into sdS
-  lds_tn_blocks(bufA, kBwdLd, bufB, kBwdLd, kDh, Lq4 / 4, Lk4 / 4, [&](int m0, int n0, float (&acc)[4][4]) {
+  lds_tn_blocks(bufA, kBwdLd, bufB, kBwdLd, kDh, 0, Lq4 / 4, Lk4 / 4, [&](int m0, int n0, float (&acc)[4][4]) {
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -569,17 +594,24 @@ __global__ __launch_bounds__(256) void mha_bwd_lds_kernel(MhaArgs a, const float
       const int i = idx / Lk, j = idx % Lk;
       sP[i * kBwdLd + j] *= dasa_dropout_scale(a.p, sdk, (uint64_t)(pbase + idx));
     }
-  for (int idx = t; idx < Lq4 * kDh; idx += blockDim.x) {
-    const int i = idx / kDh, d = idx % kDh;
-    bufA[i * kBwdLdD + d] = i < Lq ? a.Q[((long)b * Lq + i) * a.ldq + h * kDh + d] : 0.f;
-  }
-  for (int idx = t; idx < Lk4 * kDh; idx += blockDim.x) {
-    const int j = idx / kDh, d = idx % kDh;
-    bufB[j * kBwdLdD + d] = j < Lk ? a.K[((long)b * Lk + j) * a.ldk + h * kDh + d] : 0.f;
+  {
+    float vq[NR], vk[NR];
+#pragma unroll
+    for (int it = 0; it < NR; ++it) {
+      const int idx = t + 256 * it, i = idx / kDh, d = idx % kDh;
+      vq[it] = i < Lq ? a.Q[((long)b * Lq + i) * a.ldq + h * kDh + d] : 0.f;
+      vk[it] = i < Lk ? a.K[((long)b * Lk + i) * a.ldk + h * kDh + d] : 0.f;
+    }
+#pragma unroll
+    for (int it = 0; it < NR; ++it) {
+      const int idx = t + 256 * it, i = idx / kDh, d = idx % kDh;
+      if (i < Lq4) bufA[i * kBwdLdD + d] = vq[it];
+      if (i < Lk4) bufB[i * kBwdLdD + d] = vk[it];
+    }
   }
   __syncthreads();
   // dV[j][d] = sum_i Pd[i][j] dO[i][d]
-  lds_tn_blocks(sP, kBwdLd, sdO, kBwdLdD, Lq, Lk4 / 4, kDh / 4, [&](int m0, int n0, float (&acc)[4][4]) {
+  lds_tn_blocks(sP, kBwdLd, sdO, kBwdLdD, Lq, kb0, kbn, kDh / 4, [&](int m0, int n0, float (&acc)[4][4]) {
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       if (m0 + r < Lk)
@@ -587,7 +619,7 @@ __global__ __launch_bounds__(256) void mha_bwd_lds_kernel(MhaArgs a, const float
             make_float4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
   });
   // dQ[i][d] = sum_j dS[i][j] K[j][d]
-  lds_tn_blocks(sdST, kBwdLd, bufB, kBwdLdD, Lk, Lq4 / 4, kDh / 4, [&](int m0, int n0, float (&acc)[4][4]) {
+  lds_tn_blocks(sdST, kBwdLd, bufB, kBwdLdD, Lk, qb0, qbn, kDh / 4, [&](int m0, int n0, float (&acc)[4][4]) {
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       if (m0 + r < Lq)
@@ -595,7 +627,7 @@ __global__ __launch_bounds__(256) void mha_bwd_lds_kernel(MhaArgs a, const float
             make_float4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
   });
   // dK[j][d] = sum_i dS[i][j] Q[i][d]
-  lds_tn_blocks(sdS, kBwdLd, bufA, kBwdLdD, Lq, Lk4 / 4, kDh / 4, [&](int m0, int n0, float (&acc)[4][4]) {
+  lds_tn_blocks(sdS, kBwdLd, bufA, kBwdLdD, Lq, kb0, kbn, kDh / 4, [&](int m0, int n0, float (&acc)[4][4]) {
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       if (m0 + r < Lk)
@@ -828,6 +860,14 @@ extern "C" int dasa_mha_fwd(const float* Q, int64_t ldq, const float* K, int64_t
   return 0;
 }
 
+// workgroups per (batch, head) of the Lq, Lk <= 80 attention backward: 0 = automatic, n >= 1 forced
+static int g_mha_bwd_parts = 0;
+extern "C" int dasa_mha_bwd_split(int32_t parts) {
+  const int prev = g_mha_bwd_parts;
+  if (parts >= 0) g_mha_bwd_parts = parts > 16 ? 16 : parts;
+  return prev;
+}
+
 extern "C" int dasa_mha_bwd(const float* Q, int64_t ldq, const float* K, int64_t ldk, const float* V, int64_t ldv,
                             const float* probs, const float* dout, int64_t lddo, float* dQ, float* dK, float* dV,
                             int32_t B, int32_t heads, int32_t Lq, int32_t Lk, int32_t dh, float scale, float drop_p,
@@ -837,10 +877,15 @@ extern "C" int dasa_mha_bwd(const float* Q, int64_t ldq, const float* K, int64_t
   MhaArgs a{Q, ldq, K, ldk, V, ldv, nullptr, nullptr, 0, const_cast<float*>(probs), B, heads, Lq, Lk, scale, drop_p,
             seed, drop_p > 0.f ? dasa_seed_src_host() : nullptr};
   const bool vec = ((ldq | ldk | ldv) & 3) == 0 && (((uintptr_t)dQ | (uintptr_t)dK | (uintptr_t)dV) & 15) == 0;
-  if (Lq <= kBwdMaxL && Lk <= kBwdMaxL && vec)
-    hipLaunchKernelGGL(mha_bwd_lds_kernel, dim3(B * heads), dim3(256), 0, (hipStream_t)stream, a, dout, (long)lddo, dQ,
-                       dK, dV);
-  else
+  if (Lq <= kBwdMaxL && Lk <= kBwdMaxL && vec) {
+    int parts = g_mha_bwd_parts;
+    if (parts <= 0) {   // auto: up to 4 parts while B x heads x parts stays within one round of 256 CUs
+      parts = 256 / (B * heads);
+      parts = parts < 1 ? 1 : parts > 4 ? 4 : parts;
+    }
+    hipLaunchKernelGGL(mha_bwd_lds_kernel, dim3(B * heads * parts), dim3(256), 0, (hipStream_t)stream, a, dout,
+                       (long)lddo, dQ, dK, dV, parts);
+  } else
     hipLaunchKernelGGL(mha_bwd_kernel, dim3(B * heads), dim3(256), 0, (hipStream_t)stream, a, dout, (long)lddo, dQ, dK,
                        dV);
   DASA_CHECK_LAUNCH();

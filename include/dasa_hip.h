@@ -150,6 +150,11 @@ int dasa_mha_bwd(const float* Q, int64_t ldq, const float* K, int64_t ldk, const
                  const float* probs, const float* dout, int64_t lddo,
                  float* dQ, float* dK, float* dV, int32_t B, int32_t heads, int32_t Lq, int32_t Lk,
                  int32_t dh, float scale, float drop_p, uint64_t seed, void* stream);
+/* Workgroups per (batch, head) of the LDS-staged backward (Lq, Lk <= 80): each recomputes the whole dS
+ * and writes its share of dQ / dK / dV rows (bitwise equal for every count). 0 = automatic (up to 4
+ * while B x heads x parts <= 256; the finetune's B = 2), n >= 1 forced (at most 16), < 0 only
+ * queries. Returns the previous setting. Host-only.                                               */
+int dasa_mha_bwd_split(int32_t parts);
 
 /* ---- SoftDot / ShiftSoftDot attention (model.py:253-353) ------------------------------------
  * q [B][D] is linear_in(h) (computed by dasa_gemm_f32); ctx [B][N][ldn] (ldn >= D, batch stride

@@ -86,6 +86,10 @@ def test_x6_plan_and_lstm_switches_are_host_only():
         hook(prev)
     B, H = 700, 1024
     assert L.dasa_bilstm_bwd_workspace(B, H) >= (6 * B * H + 20 * H * H) * 4
+    prev = L.dasa_mha_bwd_split(-1)                                   # attention backward split (0 = auto)
+    assert L.dasa_mha_bwd_split(3) == prev and L.dasa_mha_bwd_split(-1) == 3
+    assert L.dasa_mha_bwd_split(99) == 3 and L.dasa_mha_bwd_split(-1) == 16
+    L.dasa_mha_bwd_split(prev)
 
 
 def test_product_schema_matches_reference():

@@ -236,6 +236,30 @@ def test_mha_bwd_vs_autograd(dev, Lq, Lk, p):
         assert (got - ref).abs().max() < 1e-4 * max(1.0, ref.abs().max().item())
 
 
+@pytest.mark.parametrize("Lq,Lk,p", [(80, 80, 0.1), (36, 80, 0.0), (7, 13, 0.1)])
+def test_mha_bwd_parts_bitwise(dev, Lq, Lk, p):
+    """The LDS-staged attention backward split over 1-7 workgroups per (batch, head) (dasa_mha_bwd_split;
+    the default at the finetune's B = 2 is 4): every split writes the same dQ / dK / dV bitwise."""
+    from dasa_amd import _lib, ops
+    g = torch.Generator().manual_seed(Lq * Lk)
+    B, h, scale, seed = 2, 12, 1 / 8.0, 99
+    Q, K, V, dO = (_rand(B, L_, 768, g=g).to(dev) for L_ in (Lq, Lk, Lk, Lq))
+    m = torch.zeros(B, Lk, device=dev)
+    m[1, Lk // 2:] = -10000.0
+    _, probs = ops.mha(Q, K, V, m, h, scale, p, seed, save_probs=True)
+    lib = _lib.lib()
+    prev = lib.dasa_mha_bwd_split(1)
+    try:
+        ref = [t.clone() for t in ops.mha_bwd(Q, K, V, probs, dO, h, scale, p, seed)]
+        for parts in (2, 3, 4, 7):
+            lib.dasa_mha_bwd_split(parts)
+            got = ops.mha_bwd(Q, K, V, probs, dO, h, scale, p, seed)
+            for a_, b_ in zip(got, ref):
+                assert torch.equal(a_, b_), parts
+    finally:
+        lib.dasa_mha_bwd_split(prev)
+
+
 @pytest.fixture(params=["split", "rowsplit", "split2", "rowsplit_fwd"])
 def attn_mode(request, dev):
     """The attention implementations (include/dasa_hip.h dasa_attn_set_mode): the D-split forms the
