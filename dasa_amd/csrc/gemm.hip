@@ -1379,15 +1379,31 @@ void gemm_f32x6_nt_kernel(GemmP p, long plane, X6Split xs) {
     stg2.load(p, A, W, plane, m0, n0, 32 * min(1, nk - 1), tid);
         stg.store(smem, tid);
     __syncthreads();
+    // PRIO == 3 (A/B form 26): the next stage's split + ds_write interleaved between the MFMA groups
+    // (sched_group_barrier: loads, fragment reads, then 6 x {8 MFMA, 8 VALU, 1 ds_write})
+    auto interleave = [&]() {
+      if constexpr (PRIO == 3) {
+        __builtin_amdgcn_sched_group_barrier(0x020, 5, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 18, 0);
+#pragma unroll
+        for (int r = 0; r < 6; ++r) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
+          __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+        }
+      }
+    };
     for (int t = 0; t < nk; t += 2) {
       stg.load(p, A, W, plane, m0, n0, 32 * min(t + 2, nk - 1), tid);
       compute(smem);
             stg2.store(smem + STAGE, tid);
+      interleave();
       __syncthreads();
       if (t + 1 >= nk) break;
       stg2.load(p, A, W, plane, m0, n0, 32 * min(t + 3, nk - 1), tid);
       compute(smem + STAGE);
             stg.store(smem, tid);
+      interleave();
       __syncthreads();
     }
   }
@@ -2732,6 +2748,7 @@ static int x6_run(const dasa_gemm_desc* d, X6Plan pl, int64_t plane, void* ws, i
     case 15: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, false, 2>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
     case 16: hipLaunchKernelGGL((gemm_f32x6_dma_kernel<128, 128, 4, 2>), grid, dim3(512), 0, st, p, (long)plane); break;
     case 20: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true, -1>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
+    case 26: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true, 2, false, 3>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
     case 21: hipLaunchKernelGGL((gemm_f32x6_ra_kernel<128, 128, 2, 2>), grid, dim3(256), 0, st, p, (long)plane); break;
     case 22: hipLaunchKernelGGL((gemm_f32x6_ra_kernel<128, 128, 4, 2>), grid, dim3(512), 0, st, p, (long)plane); break;
     default: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true>), grid, dim3(512), 0, st, p, (long)plane, xs); break;

@@ -952,7 +952,7 @@ def test_gemm_f32x6(dev, M, N, K):
     err_nat = (out_nat.cpu().double() - ref).abs().max().item()
     try:
         outs = {}
-        for cfg in list(range(10)) + [15, 16, 20, 21, 22]:
+        for cfg in list(range(10)) + [15, 16, 20, 21, 22, 26]:
             lib.dasa_gemm_force_config((1 << 21) + cfg)
             y = torch.empty(M, N, device=dev)
             ops.gemm_f32x6(Ad, planes, y, M=M, N=N, K=K, lda=K + 8, ldc=N, bias=bias.to(dev))
@@ -971,7 +971,7 @@ def test_gemm_f32x6(dev, M, N, K):
         lib.dasa_gemm_force_config((1 << 21) + 8 + 32 * 1)
         y8 = torch.empty(M, N, device=dev)
         ops.gemm_f32x6(Ad, planes, y8, M=M, N=N, K=K, lda=K + 8, ldc=N, bias=bias.to(dev))
-        for cfg in (16, 20, 21, 22):   # all-DMA, one-LDS-stage, register-A forms: form 8's products and order
+        for cfg in (16, 20, 21, 22, 26):   # all-DMA, one-LDS-stage, register-A, interleaved forms: form 8 order
             assert torch.equal(outs[cfg], y8.cpu()), cfg
     finally:
         lib.dasa_gemm_force_config(-1)
