@@ -2617,13 +2617,20 @@ static X6Plan x6_plan(const dasa_gemm_desc* d) {
 // when the cost model (rounds x tile work) promises >= 10 % less; DASA_X6_TAIL=0 turns it off (A/B).
 struct X6Tail { int M1; X6Plan dp, rem; };
 
+static int g_x6_tail = -1;
 static bool x6_tail_on() {
-  static int on = -1;
-  if (on < 0) {
+  if (g_x6_tail < 0) {
     const char* e = getenv("DASA_X6_TAIL");
-    on = !(e && e[0] == '0');
+    g_x6_tail = !(e && e[0] == '0');
   }
-  return on != 0;
+  return g_x6_tail != 0;
+}
+
+// tests / A/B: 1 = whole rounds + split-K tail where the cost model takes it (the default), 0 = one launch
+extern "C" int dasa_gemm_x6_set_tail(int32_t on) {
+  if (on < 0 || on > 1) return (int)hipErrorInvalidValue;
+  g_x6_tail = on;
+  return 0;
 }
 
 static bool x6_tail_plan(const dasa_gemm_desc* d, const X6Plan& pl, X6Tail& tp) {

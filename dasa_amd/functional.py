@@ -166,6 +166,32 @@ def _bgrad(b, dz):
     return ops.colsum(dz)
 
 
+class _SumTermsFn(torch.autograd.Function):
+    """sum_t x_t of 0-dim tensors as ONE colsum GEMM over their stack (the rollout's per-step loss terms,
+    agent_dg.py:871-872 `total_forth_loss += ce`). The per-step `+=` ran torch's float add kernel, which carries
+    packed-FP32 VALU, while the language pipe's GEMMs run on another stream."""
+
+    @staticmethod
+    def forward(ctx, *ts):
+        x = torch.stack([t.detach().reshape(()) for t in ts]).view(-1, 1)
+        ctx.n = len(ts)
+        return ops.colsum(x).view(())
+
+    @staticmethod
+    def backward(ctx, g):
+        return (g,) * ctx.n
+
+
+def sum_terms(ts):
+    return _SumTermsFn.apply(*ts)
+
+
+def row_sums(x):
+    """[T, B] -> [T] row sums as one GEMM with a ones vector (no autograd; logging)."""
+    ones = torch.ones(x.shape[1], 1, dtype=torch.float32, device=x.device)
+    return ops.matmul_nn(x.float().contiguous(), ones).view(-1)
+
+
 def _cat_rows(ts):
     ts = [_flat(t) for t in ts]
     return ts[0] if len(ts) == 1 else torch.cat(ts, 0)
@@ -682,7 +708,7 @@ def _batched_bptt(grp):
     lens = torch.cat([it["lens"] for it in grp], 0)
     dgates = ops.bilstm_bwd(W_hh_f, W_hh_b, lens, (sa, sc), dout, carry("dh_n"), carry("dc_n"), H)
     del sa, sc, dout
-    hprev = ops.bilstm_hprev(torch.cat([it["out"] for it in grp], 0), H)    # [2][NB][L][H]
+    out_all = torch.cat([it["out"] for it in grp], 0)                       # [NB][L][2H]
     x2 = torch.cat([it["x"].detach() for it in grp], 0).reshape(NB * L, E)
     want_dx = any(it["needs"][0] for it in grp)
     dx = None
@@ -698,7 +724,7 @@ def _batched_bptt(grp):
         if n[iw]:
             _acc_grad(P[iw - 2], ops.matmul_tn(dg, x2))
         if n[ihh]:
-            _acc_grad(P[ihh - 2], ops.matmul_tn(dg, hprev[d].reshape(NB * L, H)))
+            _acc_grad(P[ihh - 2], ops.bilstm_dw_hh(dgates, out_all, d, H))
         if n[ibi] or n[ibh]:
             db = ops.colsum(dg)
             if n[ibi]:
@@ -756,7 +782,6 @@ class BiLSTMFn(torch.autograd.Function):
         if dout is None:
             dout = torch.zeros_like(out)
         dgates = ops.bilstm_bwd(W_hh_f, W_hh_b, lens, (sa, sc), dout, dh_n, dc_n, H)
-        hprev = ops.bilstm_hprev(out, H)
         x2 = x.reshape(B * L, E)
         grads = [None] * 10
         dx = None
@@ -765,7 +790,7 @@ class BiLSTMFn(torch.autograd.Function):
             if n[iw]:
                 grads[iw] = ops.matmul_tn(dg, x2)
             if n[ihh]:
-                grads[ihh] = ops.matmul_tn(dg, hprev[d].reshape(B * L, H))
+                grads[ihh] = ops.bilstm_dw_hh(dgates, out.contiguous(), d, H)
             if n[ibi] or n[ibh]:
                 db = ops.colsum(dg)
                 grads[ibi] = db if n[ibi] else None

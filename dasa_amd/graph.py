@@ -55,9 +55,10 @@ def _graph(g, pool=None, stream=None):
     driver, so the allocations after each capture go back to hipMalloc — with a capture per new slot of a
     small-batch finetune rollout (cfg4: candidate blocks / steps first seen in later iterations) the
     release-and-reallocate cycle cost up to 155 ms in one iteration (r05 trace). The device is synchronised
-    and the capture runs in torch's global error mode on `stream`, as torch.cuda.graph does."""
+    and the capture runs in torch's global error mode on `stream`, as torch.cuda.graph does — with Python's
+    garbage collection off throughout (_no_gc), whatever the caller does (tests/test_host_cpu.py)."""
     torch.cuda.synchronize()
-    with torch.cuda.stream(stream):
+    with _no_gc(), torch.cuda.stream(stream):
         g.capture_begin(*(() if pool is None else (pool,)), capture_error_mode="global")
         try:
             yield
@@ -239,9 +240,14 @@ class _BridgeFn(torch.autograd.Function):
         got = {}
         mask = tuple(o is not None and o.requires_grad and g is not None for o, g in zip(slot.static_out, gouts))
         if outs and slot.leaves and BWD_GRAPH and not prof.active():
-            bw = slot.bwd.get(mask)
+            from . import functional as DF
+            # a backward captured under defer_weight_grads computes only the dz products and queues the
+            # weight / bias GEMMs; a plain loss.backward() on the same slot needs the graph that computes
+            # them itself — one captured graph per (gradient pattern, deferral mode)
+            bkey = (mask, bool(DF._WG.active))
+            bw = slot.bwd.get(bkey)
             if bw is None:
-                bw = slot.bwd[mask] = slot.owner._capture_bwd(slot, outs, grads)
+                bw = slot.bwd[bkey] = slot.owner._capture_bwd(slot, outs, grads)
             else:
                 from . import ops
                 ops.copy_many([(g.detach(), s_) for s_, g in zip(bw.gin, grads)])
@@ -292,6 +298,8 @@ def _requeue(bw):
     """Queue the captured backward's deferred weight / bias gradient products again (the replay rewrote
     their dz buffers in place)."""
     from . import functional as DF
+    if (bw.wq or bw.bq) and not DF._WG.active:
+        raise _lib.DasaError("a backward graph captured under defer_weight_grads replayed outside it")
     for W, dz, x in bw.wq:
         e = DF._WG.w.get(id(W))
         if e is None:

@@ -891,6 +891,37 @@ def bilstm_hprev(out, H):
     return hprev
 
 
+def bilstm_dw_hh(dgates, out, d, H):
+    """dW_hh of direction d of a packed bi-LSTM (r2rmodel.py:2339-2343, nn.LSTM's weight_hh gradient):
+    sum over (sequence, t) of dgates[., t, d]ᵀ h_prev(t), with h_prev the direction's previous output —
+    fwd out[., t-1, :H], bwd out[., t+1, H:], zero at the sequence ends — read IN PLACE from `out` (VERDICT
+    r05 #6: no shifted copy; bilstm_hprev wrote 0.9 GB per flush for it). One TN GEMM over all rows with the
+    two operands offset by one row, then one small GEMM (alpha = -1, beta = 1) removing the NB - 1 pairs that
+    offset pairs across a sequence boundary (fwd: dgates[n, 0] with out[n-1, L-1]; bwd: dgates[n, L-1] with
+    out[n+1, 0]). Rows past a sequence's length carry zero dgates, as with the copy. dgates [NB, L, 2, 4H],
+    out [NB, L, 2H] (contiguous); returns [4H, H]."""
+    NB, L = dgates.shape[0], dgates.shape[1]
+    G = dgates.shape[-1]
+    assert dgates.is_contiguous() and out.is_contiguous() and tuple(out.shape) == (NB, L, 2 * H) and G == 4 * H
+    res = torch.empty(G, H, dtype=torch.float32, device=dgates.device)
+    if NB * L < 2:
+        return res.zero_()
+    dg = dgates.view(NB * L, 2, G)[:, d, :]           # [NB*L, 4H], row stride 8H
+    h = out.view(NB * L, 2 * H)[:, d * H:(d + 1) * H]  # [NB*L, H], row stride 2H
+    if d == 0:
+        matmul_tn(dg[1:], h[:-1], out=res)
+        if NB > 1:
+            A, B = dgates[1:, 0, 0, :], out[:-1, L - 1, :H]
+    else:
+        matmul_tn(dg[:-1], h[1:], out=res)
+        if NB > 1:
+            A, B = dgates[:-1, L - 1, 1, :], out[1:, 0, H:]
+    if NB > 1:
+        gemm(A, B, res, M=G, N=H, K=NB - 1, opA=1, opB=0, lda=A.stride(0), ldb=B.stride(0), ldc=H,
+             alpha=-1.0, beta=1.0)
+    return res
+
+
 def reverse_valid(x, lengths_i32):
     B, L, H = x.shape
     out = torch.empty_like(x)

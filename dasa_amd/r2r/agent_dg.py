@@ -813,8 +813,9 @@ class Seq2SeqAgent(BaseAgent):
         rewards, hidden_states, policy_log_probs, masks, entropys = [], [], [], [], []
         deferred = defaultdict(list)     # logs whose .item() is taken after the loop
         ml_loss = 0.0
-        total_forth_loss = 0.0
-        total_back_loss = 0.0
+        # per-step loss terms, summed once after the loop on the library's kernels (DF.sum_terms): a torch
+        # scalar add per step ran its packed-FP32 kernel beside the language pipe's GEMMs
+        forth_terms, back_terms, ent_terms = [], [], []
         consistent_drop = args.consistent_drop or (speaker is not None)
         if args.decoder_consistent_drop:
             self.decoder.init_noise((seq.shape[0], args.d_enc_hidden_size))
@@ -849,9 +850,9 @@ class Seq2SeqAgent(BaseAgent):
                     h_t, c_t, logit, h1, ce, _, _, _, back = self._decode(
                         t, "teacher", e, h0, h0 if t == 0 else h1, c0, ctx_mask, self._lens_dev(e["leng"]),
                         targets[i], None, consistent_drop, None, back_target)
-                    total_forth_loss += ce
+                    forth_terms.append(ce)
                     if back is not None:
-                        total_back_loss += back
+                        back_terms.append(back)
                     t += 1
                     ctx = e["ctx"]
                     hidden_states.append(h_t)
@@ -869,7 +870,7 @@ class Seq2SeqAgent(BaseAgent):
                     candidate_leng, (h_t, c_t, logit, h1, ce, lpa, a_t) = self._graph_step(
                         perm_obs, target, h_t, h1, c_t, *enc_args[:3], ctx_mask)
                     hidden_states.append(h_t)
-                    total_forth_loss += ce
+                    forth_terms.append(ce)
                     policy_log_probs.append(lpa.unsqueeze(1))
                     cpu_a_t = a_t.cpu().numpy().copy()      # the step's one device->host sync
                     for i, next_id in enumerate(cpu_a_t):
@@ -907,14 +908,14 @@ class Seq2SeqAgent(BaseAgent):
                         forced_fn(candidate_leng) if forced_fn is not None else None, consistent_drop, extra,
                         back_target)
                 hidden_states.append(h_t)
-                total_forth_loss += ce          # mask + CE + action + entropy / log-prob: one kernel (policy.hip)
+                forth_terms.append(ce)          # mask + CE + action + entropy / log-prob: one kernel (policy.hip)
                 if back is not None:
-                    total_back_loss += back
+                    back_terms.append(back)
                 if self.feedback == "argmax":
                     a_t = a_dev
                     policy_log_probs.append(lpa.unsqueeze(1))
                 elif self.feedback == "sample":
-                    deferred["entropy"].append(ent.sum().detach())
+                    ent_terms.append(ent.detach())
                     entropys.append(ent)
                     a_t = a_dev
                     policy_log_probs.append(lpa)
@@ -984,6 +985,10 @@ class Seq2SeqAgent(BaseAgent):
             self.loss += rl_loss
             deferred["normalized_rl_loss"].append(rl_loss.detach())
 
+        if ent_terms:      # the per-step entropy logs (agent_dg.py:916): row sums of the [T, B] stack, one GEMM
+            deferred["entropy"] = list(DF.row_sums(torch.stack(ent_terms)).unbind(0)) + deferred["entropy"]
+        total_forth_loss = DF.sum_terms(forth_terms) if forth_terms else 0.0
+        total_back_loss = DF.sum_terms(back_terms) if back_terms else 0.0
         ml_loss += total_forth_loss
         deferred["forth_loss"].append(total_forth_loss.detach())
         if args.pred_back:

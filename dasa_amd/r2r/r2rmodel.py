@@ -14,7 +14,7 @@ import torch.nn as nn
 from .. import functional as DF
 from .. import ops
 from .param import args
-from .vilmodel import BertConfig, DicModel
+from .vilmodel import BertConfig, DicModel, extended_mask
 
 
 class ReverseFn(torch.autograd.Function):
@@ -56,7 +56,7 @@ class _LangPipe:
     def __init__(self, bert, ids, att_mask, steps, chunk):
         self.bert = bert
         self.ids = ids
-        self.ext = ((1.0 - att_mask.float()) * -10000.0).unsqueeze(1).unsqueeze(2)
+        self.ext = extended_mask(att_mask)
         self.budget = steps
         self.chunk = chunk
         self.ready = []          # (output [B, L, H], event recorded on the pipe stream)
@@ -185,7 +185,7 @@ class DicEncoder(nn.Module):
             # encoder's T-fold repeated sequences reuse it T times
             R, rows = ids.shape[0], self._lang_rows or ids.shape[0]
             if self._lang_cache is None or self._lang_cache[0] != rows:
-                ext = ((1.0 - att_mask[:rows].float()) * -10000.0).unsqueeze(1).unsqueeze(2)
+                ext = extended_mask(att_mask[:rows])
                 with torch.no_grad():
                     self._lang_cache = (rows, bert.language(ids[:rows], ext))
             out = self._lang_cache[1]
@@ -193,7 +193,7 @@ class DicEncoder(nn.Module):
         if self._lang_cache_on and not bert.training:
             key = (ids.data_ptr(), tuple(ids.shape), ids._version, att_mask.data_ptr())
             if self._lang_cache is None or self._lang_cache[0] != key:
-                ext = ((1.0 - att_mask.float()) * -10000.0).unsqueeze(1).unsqueeze(2)
+                ext = extended_mask(att_mask)
                 with torch.no_grad():
                     self._lang_cache = (key, bert.language(ids, ext))
             return self._lang_cache[1]

@@ -112,6 +112,9 @@ int dasa_gemm_f32x6_ws(const dasa_gemm_desc* d, int64_t plane, void* ws, int64_t
  * how many kernels dasa_gemm_f32x6_ws launches for `d` with a workspace of ws_bytes (profiling: per-kernel
  * durations -> per-call rates). */
 int dasa_gemm_f32x6_kernels(const dasa_gemm_desc* d, int64_t ws_bytes);
+/* Test / A/B hook for that tail plan: 1 = on where the cost model takes it (the default unless DASA_X6_TAIL=0),
+ * 0 = every call one launch. Host-only setting; returns 0 (hipErrorInvalidValue outside {0, 1}). */
+int dasa_gemm_x6_set_tail(int32_t on);
 /* x [rows][ldx] fp32 -> y = three bf16 planes [3][rows][cols] (hi, mid, lo; plane stride rows*cols),
  * x = hi + mid + lo exactly for normal fp32 values; cols % 8 == 0, 16-B aligned x and y. */
 int dasa_f32_split3_bf16(const float* x, int64_t ldx, uint16_t* y, int32_t rows, int32_t cols, void* stream);

@@ -9,10 +9,10 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _cases(dev):
+def _cases(dev, bilstm=False):
     from tools.determinism_stress import cases
     g = torch.Generator(device=dev).manual_seed(0)
-    return [c for c in cases(dev, g) if not c[0].startswith("bilstm")]   # (B = 256 cases included)
+    return [c for c in cases(dev, g) if c[0].startswith("bilstm") == bilstm]   # (B = 256 cases included)
 
 
 def test_handoff_kernels_reproducible_beside_x6_gemm(dev):
@@ -37,5 +37,35 @@ def test_handoff_kernels_reproducible_beside_x6_gemm(dev):
         torch.cuda.synchronize()
         if int(cnt):
             bad[name] = int(cnt)
+    ops.check_device_errors()
+    assert not bad, bad
+
+
+def test_persistent_bilstm_reproducible_between_x6_gemms(dev):
+    """the persistent bi-LSTM kernels (forward at B = 20 / 160, BPTT at B = 2 / 20), whose
+    workgroups hand the recurrent state to each other every step, bitwise reproducible call to call with two
+    inputs alternating (a reader of the previous call's state words at the same workspace address shows up as
+    a mismatch) and a 12800-row bf16x6 GEMM between calls. The GEMM runs on the same stream, not beside: a
+    persistent launch needs every workgroup co-resident (the iteration runs it exclusively), so a
+    concurrent GEMM would only exercise the bounded barrier's timeout path."""
+    from dasa_amd import ops
+    A, W = torch.randn(12800, 768, device=dev), torch.randn(3072, 768, device=dev) * 0.02
+    y = torch.empty(12800, 3072, device=dev)
+    bad = {}
+    cs = _cases(dev, bilstm=True)
+    assert len(cs) == 4, [c[0] for c in cs]
+    for name, xs, fn in cs:
+        refs = [fn(x).clone() for x in xs]
+        torch.cuda.synchronize()
+        cnt = torch.zeros((), dtype=torch.int32, device=dev)
+        for i in range(16):
+            if i % 2 == 0:
+                ops.linear(A, W, out=y)
+            out = fn(xs[i & 1])
+            cnt += (~torch.eq(out, refs[i & 1])).any().int()
+        torch.cuda.synchronize()
+        if int(cnt):
+            bad[name] = int(cnt)
+        assert all(torch.isfinite(r).all() for r in refs), name
     ops.check_device_errors()
     assert not bad, bad

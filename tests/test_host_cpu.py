@@ -313,3 +313,62 @@ def test_copy_layout_collapse():
     assert _copy_layout(torch.zeros(3, 5, 7, 9)[:, 1:4, :, :8], torch.zeros(3, 3, 7, 8)) == (3, 21, 8, 315, 9, 168, 8)
     assert _copy_layout(torch.zeros(2, 3, 4, 5)[:, :, :, ::2], torch.zeros(2, 3, 4, 3)) == (24, 3, 1, 5, 2, 3, 1)
     assert _copy_layout(torch.zeros(3, 4, 5, 6)[:, ::2, ::2, ::2], torch.zeros(3, 2, 3, 3)) is None
+
+
+def test_graph_captures_run_with_gc_disabled(monkeypatch):
+    """VERDICT r05 hygiene: a Python garbage collection during a global-mode stream capture runs finalizers
+    whose HIP calls abort the capture (r05, `_no_gc` in dasa_amd/graph.py). (1) graph._graph — the capture
+    helper of every StepGraphs / AutogradGraphs capture — keeps GC off from capture_begin to capture_end
+    whatever its caller does (capture_begin / the body / capture_end record gc.isenabled() through a fake
+    graph); (2) every other capture site in the package (torch.cuda.graph / capture_begin outside _graph)
+    sits in a `with` whose items enter _no_gc() first."""
+    import ast
+    import contextlib
+    import gc
+    from dasa_amd import graph
+    seen = []
+
+    class FakeGraph:
+        def capture_begin(self, *a, **k):
+            seen.append(("begin", gc.isenabled()))
+
+        def capture_end(self):
+            seen.append(("end", gc.isenabled()))
+    monkeypatch.setattr(torch.cuda, "synchronize", lambda *a, **k: None)
+    monkeypatch.setattr(torch.cuda, "stream", lambda s=None: contextlib.nullcontext())
+    gc.enable()
+    with graph._graph(FakeGraph()):
+        seen.append(("body", gc.isenabled()))
+    assert seen == [("begin", False), ("body", False), ("end", False)], seen
+    assert gc.isenabled()
+    with pytest.raises(RuntimeError):                 # restored on an exception inside the capture too
+        with graph._graph(FakeGraph()):
+            raise RuntimeError("capture failed")
+    assert gc.isenabled()
+
+    pkg = os.path.join(ROOT, "dasa_amd")
+    bad, sites = [], 0
+    for fn in sorted(os.listdir(pkg)) + ["r2r/" + f for f in sorted(os.listdir(os.path.join(pkg, "r2r")))]:
+        if not fn.endswith(".py"):
+            continue
+        tree = ast.parse(open(os.path.join(pkg, fn)).read())
+        helper = [n for n in ast.walk(tree) if isinstance(n, ast.FunctionDef) and n.name == "_graph"]
+        inside_helper = {id(c) for h in helper for c in ast.walk(h)}
+        for node in ast.walk(tree):
+            if not isinstance(node, ast.With):
+                continue
+            funcs = [ast.unparse(it.context_expr.func) if isinstance(it.context_expr, ast.Call) else ""
+                     for it in node.items]
+            for i, f in enumerate(funcs):
+                if f in ("_graph", "graph._graph", "torch.cuda.graph"):
+                    sites += 1
+                    if f != "torch.cuda.graph" or id(node) in inside_helper:
+                        continue           # the helper itself disables GC
+                    if "_no_gc" not in [g.split(".")[-1] for g in funcs[:i]]:
+                        bad.append((fn, node.lineno, f))
+        for node in ast.walk(tree):
+            if isinstance(node, ast.Call) and ast.unparse(node.func).endswith("capture_begin") \
+                    and id(node) not in inside_helper:
+                bad.append((fn, node.lineno, "capture_begin outside graph._graph"))
+    assert sites >= 4, sites
+    assert not bad, bad

@@ -515,6 +515,38 @@ def test_bilstm_bptt_one_tile_bitwise(dev, B, L):
     assert torch.equal(dg1, dg2)
 
 
+@pytest.mark.parametrize("B,L", [(40, 9), (7, 23), (1, 5), (3, 1)])
+def test_bilstm_dw_hh_in_place(dev, B, L):
+    """ops.bilstm_dw_hh: dW_hh read from strided views of the bi-LSTM output, with the
+    cross-sequence pairs removed by one alpha = -1 GEMM, equals dgatesᵀ · h_prev built by the materialised
+    shifted copy (dasa_bilstm_hprev, zero at each direction's first step) — real dgates of a ragged batch
+    (rows past a sequence's length zero), against fp64 on the same operands."""
+    from dasa_amd import ops
+    torch.manual_seed(B * 31 + L)
+    H = 1024
+    whh_f, whh_b = [(torch.rand(4 * H, H, device=dev) - 0.5) * 0.1 for _ in range(2)]
+    xproj = torch.randn(B, L, 2, 4 * H, device=dev)
+    li = torch.randint(1, L + 1, (B,)).sort(descending=True)[0].to(torch.int32)
+    li[0] = L
+    li = li.to(dev)
+    out, h_n, c_n, saved = ops.bilstm_fwd(xproj, whh_f, whh_b, li, H, save=True)
+    gout = torch.randn(B, L, 2 * H, device=dev)
+    dgates = ops.bilstm_bwd(whh_f, whh_b, li, saved, gout, None, None, H)
+    hprev = ops.bilstm_hprev(out, H)
+    for d in range(2):
+        dg = dgates[:, :, d, :]
+        got = ops.bilstm_dw_hh(dgates, out.contiguous(), d, H)
+        want64 = dg.reshape(B * L, 4 * H).double().t() @ hprev[d].reshape(B * L, H).double()
+        copy = ops.matmul_tn(dg, hprev[d].reshape(B * L, H))
+        # the scale of the summed |products|, shifted pairs and cross-sequence pairs alike (those cancel exactly
+        # in exact arithmetic, to fp32 rounding here)
+        hd = out[:, :, d * H:(d + 1) * H].reshape(B * L, H)
+        scale = (dg.reshape(B * L, 4 * H).abs().double().t() @ hd.abs().double()).max().item() + 1e-30
+        err_copy = (copy.double() - want64).abs().max().item()
+        err = (got.double() - want64).abs().max().item()
+        assert err <= max(3 * err_copy, 1e-6 * scale), (d, err, err_copy, scale)
+
+
 @pytest.mark.parametrize("input_grads", [False, True])
 def test_bilstm_deferred_input_grads(dev, input_grads):
     """defer_bilstm_backward(input_grads=True) (optim_step's path when the language stack trains, cfg4): three
@@ -1026,6 +1058,58 @@ def _balanced_split_case(dev, M, N, K):
         lib.dasa_gemm_force_config(-1)
         ops._X6_WS_NEED.clear()
     assert err <= 1.1 * err_nat + 1e-7 and err <= 1.5 * err1 + 1e-7, (err, err_nat, err1)
+
+
+@pytest.mark.parametrize("M,N,K", [(12800, 768, 3072), (11200, 768, 768)])
+def test_gemm_f32x6_tail_plan(dev, M, N, K):
+    """the default plan's whole-rounds + split-K tail (two launches over row bands, offset A / C /
+    aux pointers for the second band) on the language-pipe shapes that take it, with every epilogue term (bias,
+    sigmoid, aux gate, column scale, beta 0.5). Against fp64 (at most the native fp32 kernel's error, +10 %)
+    and against the one-launch plan (dasa_gemm_x6_set_tail(0)) on the same inputs; bitwise-deterministic."""
+    from dasa_amd import _lib, ops
+    lib = _lib.lib()
+    g = torch.Generator(device=dev).manual_seed(M + N + K)
+    A = torch.randn(M, K, device=dev, generator=g)
+    W = torch.randn(N, K, device=dev, generator=g) * 0.05
+    bias = torch.randn(N, device=dev, generator=g) * 0.1
+    aux = torch.rand(M, N, device=dev, generator=g)
+    cs = torch.rand(N, device=dev, generator=g)
+    c0 = torch.randn(M, N, device=dev, generator=g)
+    planes = ops.split3_bf16(W)
+    lin = A.double() @ W.double().t() + bias.double()
+    want = torch.sigmoid(lin) * aux.double() * cs.double() + 0.5 * c0.double()
+    out_nat = torch.empty(M, N, device=dev)
+    ops.gemm(A, W, out_nat, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, bias=bias)
+    err_nat = (out_nat.double() - lin).abs().max().item()
+    d = ops.GemmDesc()
+    d.M, d.N, d.K, d.batch, d.opA, d.opB, d.lda, d.ldb, d.ldc = M, N, K, 1, 0, 1, K, K, N
+    res = {}
+    try:
+        for tail in (1, 0):
+            assert lib.dasa_gemm_x6_set_tail(tail) == 0
+            ops._X6_WS_NEED.clear()
+            ws = lib.dasa_gemm_f32x6_workspace(ctypes.byref(d))
+            assert lib.dasa_gemm_f32x6_kernels(ctypes.byref(d), ws) == (2 if tail else 1), tail
+            runs = []
+            for _ in range(2):
+                y = torch.full((M, N), float("nan"), device=dev)
+                ops.gemm_f32x6(A, planes, y, M=M, N=N, K=K, lda=K, ldc=N, bias=bias)
+                y2 = c0.clone()
+                ops.gemm_f32x6(A, planes, y2, M=M, N=N, K=K, lda=K, ldc=N, bias=bias, act="sigmoid", aux=aux,
+                               ld_aux=N, colscale=cs, beta=0.5)
+                runs.append((y, y2))
+            assert torch.equal(runs[0][0], runs[1][0]) and torch.equal(runs[0][1], runs[1][1]), tail
+            y, y2 = runs[0]
+            err = (y.double() - lin).abs().max().item()
+            assert err <= 1.1 * err_nat + 1e-7, (tail, err, err_nat)
+            assert (y2.double() - want).abs().max().item() < 1e-5, tail
+            res[tail] = (y, y2)
+    finally:
+        lib.dasa_gemm_x6_set_tail(1)
+        ops._X6_WS_NEED.clear()
+    # the two plans sum K in other orders: equal to fp32 rounding of the same products
+    for a, b in zip(res[0], res[1]):
+        assert (a - b).abs().max().item() <= 4 * err_nat + 1e-6
 
 
 @pytest.mark.parametrize("M,N,K", [(517, 200, 768), (720, 768, 768), (1600, 768, 3072), (100, 2048, 2048),

@@ -220,3 +220,39 @@ def test_slot_captured_mid_iteration_keeps_saved_tensors(dev, monkeypatch, bwd_g
     assert g.captures == 3
     for x, gy in kept:      # a leaf's .grad is its own tensor, not a static buffer later replays rewrite
         torch.testing.assert_close(x.grad, expect(x, gy), rtol=1e-5, atol=1e-5)
+
+
+def test_backward_graph_keyed_by_weight_grad_deferral(dev):
+    """a slot's backward captured under defer_weight_grads (as optim_step runs it) only queues the
+    weight / bias products. A later plain loss.backward() on the same slot must not replay that graph (its
+    products would be queued with nothing to flush them, and leak into the next flush): it captures its own
+    graph, which computes dW / db itself. Checked against the closed form dW = gyᵀx, db = Σ gy, in both modes
+    and alternating."""
+    from dasa_amd import functional as DF
+    from dasa_amd import graph
+    torch.manual_seed(13)
+    lin = torch.nn.Linear(256, 128).to(dev)
+    g = graph.AutogradGraphs([lin])
+
+    def fn(x):
+        return (DF.linear(x, lin.weight, lin.bias),)
+    for it, deferred in enumerate((True, False, True, False)):
+        g.new_iteration()
+        x = torch.randn(64, 256, device=dev, requires_grad=True)     # (the bridge links the region via its inputs)
+        (y,) = g.run("lin", fn, (x,))
+        gy = torch.randn_like(y)
+        lin.weight.grad = None
+        lin.bias.grad = None
+        if deferred:
+            with DF.defer_weight_grads():
+                y.backward(gy)
+            DF.flush_weight_grads()
+        else:
+            y.backward(gy)
+        assert not DF._WG.w and not DF._WG.b, it              # nothing left queued
+        want_w = gy.double().t() @ x.detach().double()
+        want_b = gy.double().sum(0)
+        torch.testing.assert_close(lin.weight.grad.double(), want_w, rtol=1e-5, atol=1e-4, msg=lambda m: f"{it}: {m}")
+        torch.testing.assert_close(lin.bias.grad.double(), want_b, rtol=1e-5, atol=1e-4, msg=lambda m: f"{it}: {m}")
+    if graph.BWD_GRAPH:
+        assert g.captures_bwd == 2, g.captures_bwd              # one per deferral mode

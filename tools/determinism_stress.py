@@ -92,6 +92,18 @@ def cases(dev, g):
     lens[5] = 37
     out.append(("bilstm B20", (rnd(20, 80, 2, 4 * H, scale=0.5), rnd(20, 80, 2, 4 * H, scale=0.5)),
                 lambda x: ops.bilstm_fwd(x, whf, whb, lens, H)[0]))
+    # teacher rollout's B = 160 forward (five 32-row tiles per workgroup)
+    lens160 = torch.full((160,), 12, dtype=torch.int32, device=dev)
+    lens160[100:] = 7
+    out.append(("bilstm B160", (rnd(160, 12, 2, 4 * H, scale=0.5), rnd(160, 12, 2, 4 * H, scale=0.5)),
+                lambda x: ops.bilstm_fwd(x, whf, whb, lens160, H)[0]))
+    # persistent BPTT: B = 2 (finetune, one-row tile) and B = 20 (two tiles), gradients of saved forwards
+    for Bb in (2, 20):
+        lb = torch.full((Bb,), 80, dtype=torch.int32, device=dev)
+        lb[-1] = 41
+        _, _, _, sv = ops.bilstm_fwd(rnd(Bb, 80, 2, 4 * H, scale=0.5), whf, whb, lb, H, save=True)
+        out.append((f"bilstm_bptt B{Bb}", (rnd(Bb, 80, 2 * H), rnd(Bb, 80, 2 * H)),
+                    lambda g_, sv=sv, lb=lb: ops.bilstm_bwd(whf, whb, lb, sv, g_, None, None, H)))
     return out
 
 
