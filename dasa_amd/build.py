@@ -105,6 +105,18 @@ def sources():
     return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
 
 
+def _includes(path, seen=None):
+    """The quoted #include files `path` pulls in, transitively (dependency check of build())."""
+    import re
+    seen = set() if seen is None else seen
+    for name in re.findall(r'^#include "([^"]+)"', open(path).read(), flags=re.M):
+        dep = os.path.normpath(os.path.join(os.path.dirname(path), name))
+        if dep not in seen and os.path.exists(dep):
+            seen.add(dep)
+            _includes(dep, seen)
+    return sorted(seen)
+
+
 def _needs_build():
     if not os.path.exists(OUT):
         return True
@@ -119,15 +131,11 @@ def build(force=False, verbose=True):
         return OUT
     os.makedirs(BUILD_DIR, exist_ok=True)
 
-    headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
-    headers.append(os.path.join(os.path.dirname(HERE), "include", "dasa_hip.h"))
-    newest_header = max(os.path.getmtime(h) for h in headers)
-
     def compile_one(src):
         obj = os.path.join(BUILD_DIR, os.path.basename(src) + ".o")
-        if (not force and os.path.exists(obj) and os.path.getmtime(obj) > os.path.getmtime(src)
-                and os.path.getmtime(obj) > newest_header):
-            return obj        # up to date (every source includes the headers, so a header edit rebuilds all)
+        if (not force and os.path.exists(obj)
+                and os.path.getmtime(obj) > max(os.path.getmtime(d) for d in [src] + _includes(src))):
+            return obj        # up to date with the source and every header it includes
         cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:

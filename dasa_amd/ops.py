@@ -393,8 +393,39 @@ def matmul_nn(A, B, out=None, beta=0.0):
     return out
 
 
-def matmul_tn(A, B, out=None, beta=0.0):
-    """out[M,N] = A[K,M]^T @ B[K,N] (weight gradients: dW = dY^T X)."""
+# TN weight-gradient GEMMs on the bf16x6 TN kernel (gemm_tn.hip) when K is long and the output has enough tiles
+# (profiles/r06/tn/probe.log: the bi-LSTM's 4096 x {768, 1024} x 112000 1.9x / 1.65x the native kernel, 4096 x
+# 2240 x 1400 1.4x, 2048 x 2176 x 1400 equal); DASA_X6_TN=0 keeps them on the native fp32 kernels (A/B)
+_X6_TN = {"on": os.environ.get("DASA_X6_TN", "1") != "0", "min_k": int(os.environ.get("DASA_X6_TN_MIN_K", "1024"))}
+
+
+def _tn_x6_ok(A, B, M, N, K, lda, ldb):
+    tiles = -(-M // 128) * -(-N // 128)
+    return (_X6_TN["on"] and _EMU["on"] and K >= _X6_TN["min_k"] and tiles >= (128 if K >= 8192 else 384)
+            and M % 2 == 0 and N % 2 == 0 and lda % 2 == 0 and ldb % 2 == 0 and A.data_ptr() % 8 == 0
+            and B.data_ptr() % 8 == 0)
+
+
+def gemm_f32x6_tn(A, B, out, *, M, N, K, lda, ldb, ldc, alpha=1.0, beta=0.0):
+    """out = alpha * A[K,M]^T B[K,N] + beta * out at fp32 accuracy on the bf16 matrix cores (dasa_gemm_f32x6_tn)."""
+    d = GemmDesc()
+    d.M, d.N, d.K, d.batch = int(M), int(N), int(K), 1
+    d.opA, d.opB = 1, 0
+    d.A, d.lda, d.strideA = _p(A), int(lda), 0
+    d.B, d.ldb, d.strideB = _p(B), int(ldb), 0
+    d.C, d.ldc, d.strideC = _p(out), int(ldc), 0
+    d.bias, d.act, d.aux, d.ld_aux, d.strideAux, d.colscale = None, 0, None, 0, 0, None
+    d.alpha, d.beta = float(alpha), float(beta)
+    L = _lib.lib()
+    need = L.dasa_gemm_f32x6_tn_workspace(ctypes.byref(d))
+    ws, ws_bytes = _gemm_ws(out.device, d, need) if need else (0, 0)
+    _call("dasa_gemm_f32x6_tn", "gemm_x6_tn", L.dasa_gemm_f32x6_tn, ctypes.byref(d), ws, ws_bytes, _stream(),
+          flops=2.0 * M * N * K, nbytes=4.0 * (M * K + K * N + M * N), detail=(int(M), int(N), int(K)))
+
+
+def matmul_tn(A, B, out=None, beta=0.0, alpha=1.0):
+    """out[M,N] = alpha * A[K,M]^T @ B[K,N] (+ beta * out) (weight gradients: dW = dY^T X). Long-K products
+    with enough output tiles (the bi-LSTM weight gradients, K = 112000) run on the bf16x6 TN kernel."""
     K, lda = _rows(A)
     M = A.shape[-1]
     Kb, ldb = _rows(B)
@@ -403,7 +434,10 @@ def matmul_tn(A, B, out=None, beta=0.0):
     if out is None:
         out = torch.empty(M, N, dtype=torch.float32, device=A.device)
     _, ldc = _rows(out)
-    gemm(A, B, out, M=M, N=N, K=K, opA=1, opB=0, lda=lda, ldb=ldb, ldc=ldc, beta=beta)
+    if K > 0 and _tn_x6_ok(A, B, M, N, K, lda, ldb):
+        gemm_f32x6_tn(A, B, out, M=M, N=N, K=K, lda=lda, ldb=ldb, ldc=ldc, alpha=alpha, beta=beta)
+        return out
+    gemm(A, B, out, M=M, N=N, K=K, opA=1, opB=0, lda=lda, ldb=ldb, ldc=ldc, alpha=alpha, beta=beta)
     return out
 
 

@@ -11,7 +11,7 @@ _REC = None
 # dense MFMA peaks other than fp32's 157.3 TFLOP/s (MI355X_MICROARCH.md: bf16 ~2.5 PF dense).
 # gemm_x6 (the bf16x6 fp32 emulation: six bf16 MFMAs per fp32 product) is priced in fp32-equivalent
 # FLOP/s against 2.5 PF / 6 = 416.7 TF, i.e. frac = its bf16 MFMA work / the bf16 dense peak.
-PEAK_TF = {"gemm_bf16": 2500.0, "gemm_x6": 2500.0 / 6}
+PEAK_TF = {"gemm_bf16": 2500.0, "gemm_x6": 2500.0 / 6, "gemm_x6_tn": 2500.0 / 6}
 
 
 # family -> (roofline bound, kernel name prefix in rocprof)
@@ -20,6 +20,7 @@ FAMILIES = {
     "gemm_skinny": ("hbm", "gemm_skinny_nt_kernel / gemm_skinny_nn_kernel (M <= 32)"),
     "gemm_bf16": ("mfma", "gemm_bf16_nt_kernel"),
     "gemm_x6": ("mfma", "gemm_f32x6_nt_kernel"),
+    "gemm_x6_tn": ("mfma", "gemm_f32x6_tn_kernel"),
     "bilstm": ("mfma", "bilstm_step_fused_kernel"),
     "bilstm_bptt": ("mfma", "bilstm_bptt_step_kernel"),
     "shift_attn": ("hbm", "attn_split_dots_kernel<5> + attn_split_ctx_kernel<5> (B < 128) / attn_rows_fwd_kernel<3>"),

@@ -115,6 +115,19 @@ int dasa_gemm_f32x6_kernels(const dasa_gemm_desc* d, int64_t ws_bytes);
 /* Test / A/B hook for that tail plan: 1 = on where the cost model takes it (the default unless DASA_X6_TAIL=0),
  * 0 = every call one launch. Host-only setting; returns 0 (hipErrorInvalidValue outside {0, 1}). */
 int dasa_gemm_x6_set_tail(int32_t on);
+/* fp32-accurate TN GEMM on the bf16 matrix cores (bf16x6, gemm_tn.hip) for long-K weight gradients:
+ * C = epilogue(alpha * A^T B) (+ beta C) with A fp32 [K][lda] (M contiguous) and B fp32 [K][ldb] (N contiguous),
+ * both split into bf16 planes on their way into LDS — the six products and accumulation order of
+ * dasa_gemm_f32x6. Only opA = 1, opB = 0, batch 1; M, N, lda, ldb even, 8-B aligned A / B; any K >= 1.
+ * Few-tile problems split K over workgroups (ws: zero-initialised once, >= dasa_gemm_f32x6_tn_workspace(d)
+ * bytes, counters re-armed by every call; without it one workgroup per tile). Replaces the weight-gradient
+ * products dW = dY^T X of the bi-LSTM (r2rmodel.py:2339-2343 nn.LSTM weight_ih / weight_hh) and of the
+ * decoder / critic linears (model.py) in the backward of agent_dg.py:1389-1405. */
+int dasa_gemm_f32x6_tn(const dasa_gemm_desc* d, void* ws, int64_t ws_bytes, void* stream);
+int64_t dasa_gemm_f32x6_tn_workspace(const dasa_gemm_desc* d);
+/* Sweep / test hook of that kernel: form (-1 plan, 0 one LDS stage with two workgroups per CU, 1 two stages)
+ * and split count (-1 plan, 1..16). Host-only setting; returns 0. */
+int dasa_gemm_x6_tn_config(int32_t form, int32_t splitk);
 /* x [rows][ldx] fp32 -> y = three bf16 planes [3][rows][cols] (hi, mid, lo; plane stride rows*cols),
  * x = hi + mid + lo exactly for normal fp32 values; cols % 8 == 0, 16-B aligned x and y. */
 int dasa_f32_split3_bf16(const float* x, int64_t ldx, uint16_t* y, int32_t rows, int32_t cols, void* stream);

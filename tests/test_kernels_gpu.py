@@ -1060,6 +1060,47 @@ def _balanced_split_case(dev, M, N, K):
     assert err <= 1.1 * err_nat + 1e-7 and err <= 1.5 * err1 + 1e-7, (err, err_nat, err1)
 
 
+@pytest.mark.parametrize("M,N,K", [(130, 200, 1000), (512, 768, 70001), (4096, 768, 9000), (6, 2, 33)])
+def test_gemm_f32x6_tn(dev, M, N, K):
+    """The bf16x6 TN weight-gradient GEMM (dasa_gemm_f32x6_tn: C = alpha AᵀB + beta C, both operands K-major and
+    split in-kernel), both forms, planned and forced split counts, ragged M / N tiles, K not a multiple of the
+    32-deep step, strided A / B: error against fp64 at most the native fp32 kernel's (+10 %), the alpha / beta
+    epilogue, every element of a NaN-filled C written, bitwise-deterministic repeats."""
+    from dasa_amd import _lib, ops
+    lib = _lib.lib()
+    g = torch.Generator(device=dev).manual_seed(M + N + K)
+    lda, ldb = M + 6, N + 4
+    A = (torch.randn(K, lda, device=dev, generator=g) * 0.1)[:, 2:2 + M]
+    B = torch.randn(K, ldb, device=dev, generator=g)[:, :N]
+    c0 = torch.randn(M, N, device=dev, generator=g)
+    ref = A.double().t() @ B.double()
+    y_nat = torch.empty(M, N, device=dev)
+    ops.gemm(A, B, y_nat, M=M, N=N, K=K, opA=1, opB=0, lda=lda, ldb=ldb, ldc=N)
+    err_nat = (y_nat.double() - ref).abs().max().item()
+    try:
+        for form in (0, 1):
+            for spl in (-1, 1, 3):
+                assert lib.dasa_gemm_x6_tn_config(form, spl) == 0
+                outs = []
+                for _ in range(2):
+                    y = torch.full((M, N), float("nan"), device=dev)
+                    ops.gemm_f32x6_tn(A, B, y, M=M, N=N, K=K, lda=lda, ldb=ldb, ldc=N)
+                    outs.append(y)
+                assert torch.equal(outs[0], outs[1]), (form, spl)
+                err = (outs[0].double() - ref).abs().max().item()
+                assert err <= 1.1 * err_nat + 1e-6, (form, spl, err, err_nat)
+                y2 = c0.clone()
+                ops.gemm_f32x6_tn(A, B, y2, M=M, N=N, K=K, lda=lda, ldb=ldb, ldc=N, alpha=-0.5, beta=0.25)
+                want = -0.5 * ref + 0.25 * c0.double()
+                assert (y2.double() - want).abs().max().item() <= 0.55 * err_nat + 1e-5, (form, spl)
+    finally:
+        lib.dasa_gemm_x6_tn_config(-1, -1)
+    # ops.matmul_tn takes the TN kernel for long K
+    if ops._tn_x6_ok(A, B, M, N, K, lda, ldb):
+        y3 = ops.matmul_tn(A, B)
+        assert (y3.double() - ref).abs().max().item() <= 1.1 * err_nat + 1e-6
+
+
 @pytest.mark.parametrize("M,N,K", [(12800, 768, 3072), (11200, 768, 768)])
 def test_gemm_f32x6_tail_plan(dev, M, N, K):
     """the default plan's whole-rounds + split-K tail (two launches over row bands, offset A / C /
