@@ -63,6 +63,24 @@ class _LangPipe:
         self.cur = None
         self.stream = _lang_stream(ids.device)
         self.stream.wait_stream(torch.cuda.current_stream())
+        # paced schedule (r06): chunk c's stack is needed at step c * chunk, so after the first chunk the
+        # pipe only has to keep one chunk ahead; spreading its units evenly up to the last chunk's first
+        # step (instead of two per step until it runs dry around step 20 of 35) leaves the early steps
+        # less contended and gives the late steps' host-bound gaps (action sync + env step, ~0.6 ms per
+        # step in the r06 trace) pipe work to overlap
+        nl = len(bert.lalayer) + 1
+        n_chunks = -(-steps // chunk)
+        self.units_total = nl * n_chunks
+        self.units_first = nl
+        self.pace_steps = max(1, chunk * (n_chunks - 1))
+        self.pumped = 0
+        self.calls = 0
+
+    def paced_units(self):
+        """Units to pump at this encoder call under the paced schedule."""
+        self.calls += 1
+        want = self.units_first + -(-(self.units_total - self.units_first) * self.calls // self.pace_steps)
+        return max(0, min(self.units_total, want) - self.pumped)
 
     def pump(self, units, gate=None):
         bert = self.bert
@@ -80,6 +98,7 @@ class _LangPipe:
                 x = bert.embeddings(ids) if k == 0 else bert.lalayer[k - 1](x, ext)[0]
                 k += 1
                 units -= 1
+                self.pumped += 1
                 if k == len(bert.lalayer) + 1:
                     B, L = self.ids.shape
                     ev = torch.cuda.Event()
@@ -145,7 +164,9 @@ class DicEncoder(nn.Module):
         self._lang_cache = None
         # train-mode language pipeline (see cache_language)
         self.lang_chunk = int(os.environ.get("DASA_LANG_CHUNK", "8"))
-        self.lang_units = int(os.environ.get("DASA_LANG_UNITS", "2"))   # pipe units pumped per encoder call
+        # pipe units pumped per encoder call; 0 = the paced schedule (_LangPipe.paced_units: within noise of
+        # the default in a same-box A/B, profiles/r06/pace/, so opt-in)
+        self.lang_units = int(os.environ.get("DASA_LANG_UNITS", "2"))
         self._lang_steps = 0
         self._lang_pipe = None
         self._lang_rows = None
@@ -230,7 +251,7 @@ class DicEncoder(nn.Module):
         if pipe is not None:
             gate = torch.cuda.Event()
             gate.record(torch.cuda.current_stream())
-            pipe.pump(self.lang_units, gate)
+            pipe.pump(pipe.paced_units() if self.lang_units <= 0 else self.lang_units, gate)
         h_t = torch.cat((h_n[1], h_n[0]), 1)          # (enc_h_t[-1], enc_h_t[-2]) = [bwd, fwd]
         c_t = torch.cat((c_n[1], c_n[0]), 1)
         decoder_init = DF.linear(h_t, self.encoder_lstm2decoder_ht.weight, self.encoder_lstm2decoder_ht.bias, "tanh")

@@ -128,6 +128,12 @@ int64_t dasa_gemm_f32x6_tn_workspace(const dasa_gemm_desc* d);
 /* Sweep / test hook of that kernel: form (-1 plan, 0 one LDS stage with two workgroups per CU, 1 two stages)
  * and split count (-1 plan, 1..16). Host-only setting; returns 0. */
 int dasa_gemm_x6_tn_config(int32_t form, int32_t splitk);
+/* bf16x6 NT GEMM with A ALSO pre-split into three bf16 planes (gemm_x6p.hip; the producer writes the planes):
+ * every operand byte goes to LDS by LDS-DMA, the MFMA loop is dasa_gemm_f32x6's (bitwise equal to its
+ * one-launch 128 x 128 form). d->A / d->B = the hi planes (bf16 elements, strides lda / ldb), the mid / lo
+ * planes aplane / wplane elements further on; form 3 = 128 x 128 tiles and a three-stage DMA ring, form 2 =
+ * 256 x 128 and two stages. K % 32 == 0, lda / ldb / planes % 8 == 0, 16-B aligned, batch 1. */
+int dasa_gemm_f32x6_pp(const dasa_gemm_desc* d, int64_t wplane, int64_t aplane, int32_t form, void* stream);
 /* x [rows][ldx] fp32 -> y = three bf16 planes [3][rows][cols] (hi, mid, lo; plane stride rows*cols),
  * x = hi + mid + lo exactly for normal fp32 values; cols % 8 == 0, 16-B aligned x and y. */
 int dasa_f32_split3_bf16(const float* x, int64_t ldx, uint16_t* y, int32_t rows, int32_t cols, void* stream);
