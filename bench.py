@@ -347,8 +347,11 @@ def aug_leg(a, steps=2):
 def _captures(agent):
     """Captured training regions + their backward graphs so far (graph.AutogradGraphs): a capture inside the
     timed region (a slot first seen there) is reported beside the number it slowed."""
-    tg = getattr(agent, "_train_graphs", None)
-    return 0 if tg is None else tg.captures + tg.captures_bwd
+    n = 0
+    for tg in (getattr(agent, "_train_graphs", None), getattr(agent.encoder.bert, "_tgraphs", None)):
+        if tg is not None:      # (the second: the finetune config's captured VisionEncoder + LXRT regions)
+            n += tg.captures + tg.captures_bwd
+    return n
 
 
 def _warm(agent, n, world=1, step=None):

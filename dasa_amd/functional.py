@@ -109,6 +109,7 @@ class _WGradDeferral:
         self.active = False
         self.w = {}      # id(param) -> [param, [dY], [X]]
         self.b = {}      # id(param) -> [param, [dY]]
+        self.gen = 0     # flush count: a captured backward replayed twice in one generation clones its queued dY
 
 
 _WG = _WGradDeferral()
@@ -201,6 +202,7 @@ def flush_weight_grads():
     """Run the queued weight / bias gradient products into .grad (one GEMM / column sum each)."""
     w, b = _WG.w, _WG.b
     _WG.w, _WG.b = {}, {}
+    _WG.gen += 1
     for P, dzs, xs in w.values():
         dz, x = _cat_rows(dzs), _cat_rows(xs)
         if P.grad is None:

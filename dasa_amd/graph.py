@@ -169,8 +169,9 @@ class _Slot:
 class _Bwd:
     """A captured backward of one slot for one pattern of incoming gradients: static grad-output buffers,
     the graph, its static leaf gradients, and the deferred weight-gradient products the capture queued
-    (functional.defer_weight_grads: re-queued on every replay, their dz buffers rewritten by it)."""
-    __slots__ = ("graph", "gin", "grads", "wq", "bq")
+    (functional.defer_weight_grads: re-queued on every replay, their dz buffers rewritten by it). qrefs / qgen:
+    where in the deferral queues the last queueing put its dz buffers, and in which flush generation."""
+    __slots__ = ("graph", "gin", "grads", "wq", "bq", "qrefs", "qgen")
 
 
 # DASA_TRAIN_GRAPH_BWD=0: a captured training region's backward runs its recorded autograd graph eagerly
@@ -250,6 +251,13 @@ class _BridgeFn(torch.autograd.Function):
                 bw = slot.bwd[bkey] = slot.owner._capture_bwd(slot, outs, grads)
             else:
                 from . import ops
+                if DF._WG.active and bw.qgen == DF._WG.gen and bw.qrefs:
+                    # a second backward through this slot before the queued weight gradients were flushed (the
+                    # bi-LSTM input-gradient continuation, functional.defer_bilstm_backward(input_grads=True),
+                    # reaches a captured encoder region twice): the earlier products still read the dz buffers
+                    # the replay below rewrites, so they keep copies
+                    for lst, i in bw.qrefs:
+                        lst[i] = lst[i].clone()
                 ops.copy_many([(g.detach(), s_) for s_, g in zip(bw.gin, grads)])
                 bw.graph.replay()
                 _requeue(bw)
@@ -300,16 +308,19 @@ def _requeue(bw):
     from . import functional as DF
     if (bw.wq or bw.bq) and not DF._WG.active:
         raise _lib.DasaError("a backward graph captured under defer_weight_grads replayed outside it")
+    bw.qrefs, bw.qgen = [], DF._WG.gen
     for W, dz, x in bw.wq:
         e = DF._WG.w.get(id(W))
         if e is None:
             e = DF._WG.w[id(W)] = [W, [], []]
+        bw.qrefs.append((e[1], len(e[1])))
         e[1].append(dz)
         e[2].append(x)
     for b, dz in bw.bq:
         e = DF._WG.b.get(id(b))
         if e is None:
             e = DF._WG.b[id(b)] = [b, []]
+        bw.qrefs.append((e[1], len(e[1])))
         e[1].append(dz)
 
 
@@ -478,6 +489,9 @@ class AutogradGraphs:
         bw.graph, bw.grads = g, tuple(gl)
         bw.wq = [(e[0], dz, x) for k, e in DF._WG.w.items() for dz, x in zip(e[1][wq0.get(k, 0):], e[2][wq0.get(k, 0):])]
         bw.bq = [(e[0], dz) for k, e in DF._WG.b.items() for dz in e[1][bq0.get(k, 0):]]
+        bw.qgen = DF._WG.gen     # where the capture queued its dz buffers (see _BridgeFn.backward)
+        bw.qrefs = ([(e[1], i) for k, e in DF._WG.w.items() for i in range(wq0.get(k, 0), len(e[1]))]
+                    + [(e[1], i) for k, e in DF._WG.b.items() for i in range(bq0.get(k, 0), len(e[1]))])
         g.replay()          # the capture launched nothing: compute this step's gradients now
         self.captures_bwd += 1
         return bw

@@ -1031,6 +1031,7 @@ class Seq2SeqAgent(BaseAgent):
         self.losses = []
         if self._train_graphs is not None:
             self._train_graphs.new_iteration()
+        self.encoder.bert.train_graphs_new_iteration()
         for m, opt in zip(self.models, self.optimizers):
             m.train()
             opt.zero_grad()
@@ -1073,6 +1074,7 @@ class Seq2SeqAgent(BaseAgent):
         DF.flush_weight_grads()
         if self._train_graphs is not None:
             self._train_graphs.new_iteration()     # every replayed step has had its backward
+        self.encoder.bert.train_graphs_new_iteration()
         # every kernel with a bounded inter-workgroup barrier (persistent bi-LSTM BPTT, D-split attention
         # backward) NaN-poisons its outputs and sets an error bit when the barrier times out: read the
         # error word (one host sync) before the gradients reach grad_sync, clipping and the optimizers;

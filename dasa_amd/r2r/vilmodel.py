@@ -377,6 +377,8 @@ class DicModel(nn.Module):
         self.addlayer = nn.ModuleList([LXRTXLayer(config) for _ in range(self.vl_layers)])
         self.vision_encoder = VisionEncoder(self.config.img_feature_dim, self.config)
         self._graphs = None     # captured forward-only VL stacks (dasa_amd/graph.py)
+        self._tgraphs = None    # captured TRAINING VL stacks with autograd (finetune: --d_update_add_layer)
+        self._dummy = None      # a grad-requiring leaf that links such a region into the caller's graph
         if args.d_v_layers > 0:
             self.vlayer = nn.ModuleList([BertLayer(config) for _ in range(args.d_v_layers)])
         self.init_weights()
@@ -406,6 +408,51 @@ class DicModel(nn.Module):
         for i, layer in enumerate(self.addlayer):
             lang, visn = layer(lang, ext, visn, img_mask, want_visn=want_visn or i < last)
         return lang, visn
+
+    def _train_region_ok(self, text_embeds, img_feats):
+        """The finetune configuration's VisionEncoder + LXRT stack (trained: --d_update_add_layer,
+        vilmodel.py:1408-1410) replays as a captured region with autograd (graph.AutogradGraphs) — forward
+        and backward one graph launch each instead of ~60 / ~100 host-issued launches per decision step,
+        which bound the B = 2 finetune iteration — unless the profiler brackets every
+        launch, an enclosing region is being captured, a module is hooked, or DASA_TRAIN_GRAPH=0."""
+        mods = [self.vision_encoder, self.addlayer] + ([self.vlayer] if args.d_v_layers > 0 else [])
+        # (the region detaches its inputs: only when neither the language stack nor the panorama trains)
+        return (graph.ENABLED and img_feats.is_cuda and os.environ.get("DASA_TRAIN_GRAPH", "1") != "0"
+                and not text_embeds.requires_grad and not img_feats.requires_grad
+                and os.environ.get("DASA_TRAIN_GRAPH_VL", "1") != "0" and not graph.capturing()
+                and not ops.prof.active()
+                and all(not m._forward_hooks and not m._forward_pre_hooks and "forward" not in m.__dict__
+                        for mm in mods for m in mm.modules())
+                and (self._tgraphs is None or len(self._tgraphs.slots) < 1024))
+
+    def _vl_train_region(self, text_embeds, ext, img_feats, want_visn):
+        """_vl_stack as one captured training region (one slot per use within an iteration: the caller calls
+        train_graphs_new_iteration() once every replayed region has had its backward). The language input is
+        padded to --maxInput tokens (rounded up to 16) with the padding masked (-10000: zero attention weight),
+        so one slot serves every batch; padded rows are computed and cut off. A zero-size leaf that requires
+        grad links the region into the caller's graph (its other inputs are detached), so the region's
+        parameters get their gradients when the caller's backward reaches it."""
+        if self._tgraphs is None:
+            mods = [self.vision_encoder, self.addlayer] + ([self.vlayer] if args.d_v_layers > 0 else [])
+            self._tgraphs = graph.AutogradGraphs(mods)
+        dev = img_feats.device
+        if self._dummy is None or self._dummy.device != dev:
+            self._dummy = torch.zeros(0, device=dev, requires_grad=True)
+        B, L, Hd = text_embeds.shape
+        Lp = -(-max(L, args.maxInput) // 16) * 16
+
+        def fn(t, e, f, _link):
+            lang, visn = self._vl_stack(t, e, f, want_visn)
+            return (lang, visn) if visn is not None else (lang,)
+        key = ("vl", B, Lp, Hd, tuple(img_feats.shape[1:]), bool(want_visn), self.training)
+        outs = self._tgraphs.run(key, fn, (text_embeds.detach(), ext, img_feats.detach(), self._dummy),
+                                 pads={0: ((B, Lp, Hd), 0.0), 1: ((B, 1, 1, Lp), -10000.0)})
+        lang = outs[0][:, :L]
+        return lang, (outs[1] if len(outs) > 1 else None)
+
+    def train_graphs_new_iteration(self):
+        if self._tgraphs is not None:
+            self._tgraphs.new_iteration()
 
     def language(self, input_ids, ext_mask):
         """Embeddings + the la_layers language BertLayers (vilmodel.py:1366-1372)."""
@@ -441,6 +488,8 @@ class DicModel(nn.Module):
                        self.training, bool(want_visn))
                 lang, visn = self._graphs.run(key, lambda t, e, f: self._vl_stack(t, e, f, want_visn),
                                               (text_embeds, ext, img_feats))
+            elif vl_grad and self._train_region_ok(text_embeds, img_feats):
+                lang, visn = self._vl_train_region(text_embeds, ext, img_feats, want_visn)
             else:
                 with torch.set_grad_enabled(vl_grad):
                     lang, visn = self._vl_stack(text_embeds, ext, img_feats, want_visn)

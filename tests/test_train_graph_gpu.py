@@ -256,3 +256,76 @@ def test_backward_graph_keyed_by_weight_grad_deferral(dev):
         torch.testing.assert_close(lin.bias.grad.double(), want_b, rtol=1e-5, atol=1e-4, msg=lambda m: f"{it}: {m}")
     if graph.BWD_GRAPH:
         assert g.captures_bwd == 2, g.captures_bwd              # one per deferral mode
+
+
+def test_finetune_vl_region_matches_eager(dev, monkeypatch):
+    """The finetune configuration's VisionEncoder + LXRT stack as a captured training region (vilmodel.py
+    DicModel._vl_train_region): two finetune iterations (README finetune flags, B = 2,
+    vl = 3, 4 + 4 steps, dropout 0, forced draws, RMSprop steps between) give the same losses and gradients —
+    the LXRT / VisionEncoder parameters' included — with the region captured and replayed as eagerly
+    (DASA_TRAIN_GRAPH_VL=0); the regions are captured in iteration 0 and only replayed in iteration 1."""
+    from dasa_amd.r2r import param
+    param.readme_finetune(["--d_vl_layers", "3", "--batchSize", "2", "--maxAction", "4"])
+    try:
+        res = {}
+        for mode in ("0", "1"):
+            monkeypatch.setenv("DASA_TRAIN_GRAPH_VL", mode)
+            torch.manual_seed(3)
+            from dasa_amd.r2r.agent_dg import Seq2SeqAgent
+            from dasa_amd.synth import SynthR2RBatch, SynthWorld, init_params
+            env = SynthR2RBatch(SynthWorld(32, 0, 5), 2, seed=701, mode="wander", instr_len=80, variable_len=True)
+            with contextlib.redirect_stdout(io.StringIO()):
+                ag = Seq2SeqAgent(env, "", None, 4, "Dic")
+            for m, s in ((ag.encoder, 1), (ag.decoder, 2), (ag.critic, 3), (ag.adaIn, 4)):
+                init_params(m, s)
+                for sub in m.modules():
+                    if isinstance(sub, torch.nn.Dropout):
+                        sub.p = 0.0
+            param.args.ml_weight = param.args.ml_weight_org
+            assert ag.encoder.bert.update_add_layer
+            out = []
+            from dasa_amd import functional as DF
+            for it in range(2):
+                table = GI.forced_table(4, 2, seed=GI.FORCED_SEED + it)
+                ag.force_action_fn = lambda t, lens, table=table: GI.forced_actions(table, t, lens, no_stop=True)
+                ag.zero_grad()
+                ag.accumulate_gradient("sample")
+                loss = ag.loss.item()
+                with DF.defer_bilstm_backward(), DF.defer_weight_grads():     # optim_step's backward,
+                    ag.loss.backward()                                        # gradients before clipping
+                    DF.flush_bilstm_backward()
+                DF.flush_weight_grads()
+                grads = {f"{i}.{k}": p.grad.detach().clone() for i, m in enumerate(ag.models)
+                         for k, p in m.named_parameters() if p.grad is not None}
+                for opt in ag.optimizers:
+                    opt.step()
+                if ag._train_graphs is not None:
+                    ag._train_graphs.new_iteration()
+                ag.encoder.bert.train_graphs_new_iteration()
+                out.append((loss, grads))
+                if mode == "1" and it == 0:
+                    tg = ag.encoder.bert._tgraphs
+                    assert tg is not None and tg.captures > 0
+                    n0 = (tg.captures, tg.captures_bwd)
+            if mode == "1":
+                tg = ag.encoder.bert._tgraphs
+                assert (tg.captures, tg.captures_bwd) == n0 and tg.replays > tg.captures   # iteration 1 replays
+            else:
+                assert ag.encoder.bert._tgraphs is None
+            res[mode] = out
+            del ag
+        for it in range(2):
+            (l0, g0), (l1, g1) = res["0"][it], res["1"][it]
+            assert abs(l0 - l1) <= 1e-5 * max(1.0, abs(l0)), (it, l0, l1)
+            assert sorted(g0) == sorted(g1)
+            assert any(k.startswith("0.bert.addlayer") for k in g0)      # the LXRT layers trained
+            ratios = {k: (g1[k].norm() / g0[k].norm()).item() for k in g0 if g0[k].norm() > 1e-6}   # (not the ~1e-10 noise of vanishing grads)
+            bad = {k: r for k, r in ratios.items() if abs(r - 1) > 1e-3}
+            assert not bad, (it, len(bad), sorted(bad.items())[:12])
+            for k in g0:
+                # (+1e-8: gradients that vanish analytically, e.g. the attention key biases — softmax is shift
+                # invariant — are fp32 rounding noise of ~1e-10 that the padded region sums in another order)
+                err = (g0[k] - g1[k]).abs().max().item()
+                assert err <= 2e-5 * g0[k].abs().max().item() + 1e-8, (it, k, err)
+    finally:
+        param.readme_train(["--d_vl_layers", "1", "--batchSize", "2", "--maxAction", "5"])

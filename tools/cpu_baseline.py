@@ -92,11 +92,13 @@ def oracle_workloads(viewpoints=64):
         return r["steps"] * B
 
     return {"cfg2_train": (train_cfg2, "teacher + sampled rollout + backward, B=20, vl=3, L=80, maxAction=2"),
+            "cfg2_train_35": (lambda: train_cfg2(35),
+                              "teacher + sampled rollout + backward, B=20, vl=3, L=80, maxAction=35 (the headline length)"),
             "cfg2_fwd": (lambda: fwd(W3e, env20, 3, 20), "eval rollout, B=20, vl=3, L=80, 5 steps"),
             "cfg1_fwd": (lambda: fwd(W1, env2, 1, 2), "eval rollout, B=2, vl=1, L=80, 5 steps")}
 
 
-def run(cores=None, which=("cfg2_train", "cfg2_fwd", "cfg1_fwd")):
+def run(cores=None, which=("cfg2_train", "cfg2_fwd", "cfg1_fwd"), reps=3):
     cores = cores or default_cores()
     prev = torch.get_num_threads()
     torch.set_num_threads(cores)
@@ -105,7 +107,7 @@ def run(cores=None, which=("cfg2_train", "cfg2_fwd", "cfg1_fwd")):
         res = {}
         for name in which:
             fn, desc = wl[name]
-            rate, times = _median_rate(fn)
+            rate, times = _median_rate(fn, reps)
             res[name] = {"value": round(rate, 3), "unit": "agent-decisions/s", "sample": desc,
                          "times_s": [round(t, 2) for t in times]}
         return {"cores": cores, "cpu_model": cpu_model(), "kind": "port", "workloads": res,
@@ -114,7 +116,7 @@ def run(cores=None, which=("cfg2_train", "cfg2_fwd", "cfg1_fwd")):
         torch.set_num_threads(prev)
 
 
-def reference_rates(cores):
+def reference_rates(cores, which=("cfg2_train", "cfg2_fwd", "cfg1_fwd"), reps=3):
     """Survey container only: the reference r2r_src itself (imported behind the offline shims) on the
     same bounded samples, to validate the restatement as a timing proxy."""
     import contextlib
@@ -136,16 +138,21 @@ def reference_rates(cores):
             init_params(m, s)
         return ag
 
-    ag = agent(20, 3, 2, 1000)
-    A.ml_weight = A.ml_weight_org
+    for name, T in (("cfg2_train", 2), ("cfg2_train_35", 35)):
+        if name not in which:
+            continue
+        ag = agent(20, 3, T, 1000)
+        A.ml_weight = A.ml_weight_org
 
-    def train():
-        ag.zero_grad()
-        ag.accumulate_gradient("sample")
-        ag.loss.backward()
-        return (ag.logs["viewsteps/teacher"][-1] + ag.logs["viewsteps/sample"][-1]) * 20
-    out["cfg2_train"] = _median_rate(train)[0]
+        def train(ag=ag):
+            ag.zero_grad()
+            ag.accumulate_gradient("sample")
+            ag.loss.backward()
+            return (ag.logs["viewsteps/teacher"][-1] + ag.logs["viewsteps/sample"][-1]) * 20
+        out[name] = _median_rate(train, reps)[0]
     for name, (B, vl) in (("cfg2_fwd", (20, 3)), ("cfg1_fwd", (2, 1))):
+        if name not in which:
+            continue
         agf = agent(B, vl, 5, 1001)
 
         def fwd(agf=agf, B=B):
@@ -156,7 +163,7 @@ def reference_rates(cores):
             with torch.no_grad():
                 agf.vl_rollout(train_ml=None, train_rl=False, reset=True)
             return agf.logs["viewsteps/argmax"][-1] * B
-        out[name] = _median_rate(fwd)[0]
+        out[name] = _median_rate(fwd, reps)[0]
     return {k: round(v, 3) for k, v in out.items()}
 
 
@@ -164,10 +171,13 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--cores", type=int, default=0)
     ap.add_argument("--reference", action="store_true")
+    ap.add_argument("--workloads", default="cfg2_train,cfg2_fwd,cfg1_fwd")
+    ap.add_argument("--reps", type=int, default=3)
     a = ap.parse_args()
-    res = run(a.cores or None)
+    which = tuple(a.workloads.split(","))
+    res = run(a.cores or None, which, a.reps)
     if a.reference:
-        res["reference"] = reference_rates(res["cores"])
+        res["reference"] = reference_rates(res["cores"], which, a.reps)
         res["restatement_over_reference"] = {k: round(res["workloads"][k]["value"] / v, 3)
                                              for k, v in res["reference"].items()}
     print(json.dumps(res, indent=1))
