@@ -379,6 +379,14 @@ def _warm(agent, n, world=1, step=None):
     return extra
 
 
+def _collect():
+    """Between bench legs: collect the previous leg's agent (reference cycles through its graphs and hooks)
+    and return its cached blocks, so each leg's host-bound loop starts without the others' live objects."""
+    import gc
+    gc.collect()
+    torch.cuda.empty_cache()
+
+
 def cfg4_leg(a, steps=3):
     """BASELINE configs[3] per rank: the README finetune iteration (README.md:104-116:
     --d_update_add_layer True, so the LXRT layers and the VisionEncoder train; d_vl_layers 3, batchSize 2,
@@ -522,14 +530,23 @@ def main():
                                    "(no host gaps); B=256 is BASELINE configs[4]'s batch; algorithmic bytes / time vs 8 TB/s")
     if rank == 0 and world == 1 and not a.no_hoist:
         out["hoist_language"] = hoist_leg(agent)
+    if rank == 0 and world == 1:
+        # the remaining legs build their own agents: free the cfg2 agent (and its captured graphs) first, so
+        # their host-bound iterations do not pay for its live objects in every GC pass or share its pools
+        del agent, env
+        _collect()
     if rank == 0 and world == 1 and not a.no_host_input:
         out["host_input"] = host_input_leg(a)
+        _collect()
     if rank == 0 and world == 1 and not a.no_aug:
         out["auglistener"] = aug_leg(a)
+        _collect()
     if rank == 0 and world == 1 and not a.no_cfg4:
         out["cfg4"] = cfg4_leg(a)
+        _collect()
     if rank == 0 and world == 1 and not a.no_cfg5:
         out["cfg5"] = cfg5_leg(a)
+        _collect()
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a)
     if rank == 0:
