@@ -66,6 +66,7 @@ SIGNATURES = {
     "dasa_gemm_f32x6_tn_workspace": (i64, [C.POINTER(GemmDesc)]),
     "dasa_gemm_x6_tn_config": (i32, [i32, i32]),
     "dasa_gemm_f32x6_pp": (i32, [C.POINTER(GemmDesc), i64, i64, i32, vp]),
+    "dasa_gemm_f32x6_k64": (i32, [C.POINTER(GemmDesc), i64, i32, vp]),
     "dasa_f32_split3_bf16": (i32, [vp, i64, vp, i32, i32, vp]),
     "dasa_gemm_force_config": (i32, [i32]),
     "dasa_gemm_x6_set_balance": (i32, [i32]),

@@ -180,12 +180,12 @@ def _timed_path_avg_us(workload, family):
 
 
 # rocprofv3 --kernel-trace --stats of the timed path per workload (tools/prof_round.sh)
-STATS_FILES = {"cfg2": "profiles/r05/prof_final/rocprof_kernel_stats_timed_path.csv"}
+STATS_FILES = {"cfg2": "profiles/r06/prof_final/rocprof_kernel_stats_timed_path.csv"}
 
 # the committed PMC summaries per workload the roofline's `traffic` / `mfma_busy` come from
 # (tools/prof_round.sh -> tools/pmc_summary.py); a workload without one reports no PMC values
-PMC_FILES = {"cfg2": "profiles/r05/prof_final/pmc_cfg2.json", "cfg5": "profiles/r05/prof_final/pmc_cfg5.json",
-             "cfg4": "profiles/r05/prof_final/pmc_cfg4.json"}
+PMC_FILES = {"cfg2": "profiles/r06/prof_final/pmc_cfg2.json", "cfg5": "profiles/r06/prof_final/pmc_cfg5.json",
+             "cfg4": "profiles/r06/prof_final/pmc_cfg4.json"}
 
 
 def active():

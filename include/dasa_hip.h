@@ -134,6 +134,12 @@ int dasa_gemm_x6_tn_config(int32_t form, int32_t splitk);
  * planes aplane / wplane elements further on; form 3 = 128 x 128 tiles and a three-stage DMA ring, form 2 =
  * 256 x 128 and two stages. K % 32 == 0, lda / ldb / planes % 8 == 0, 16-B aligned, batch 1. */
 int dasa_gemm_f32x6_pp(const dasa_gemm_desc* d, int64_t wplane, int64_t aplane, int32_t form, void* stream);
+/* bf16x6 NT GEMM with 64-deep K steps (gemm_k64.hip): one LDS stage holds a 64-deep slab, so every wave runs
+ * twice the MFMAs between barriers; bitwise equal to dasa_gemm_f32x6's one-launch 128 x 128 form. Same operands
+ * as dasa_gemm_f32x6 (A fp32, W pre-split with plane stride `plane`); form 1 = 128 x 128 tiles (one workgroup
+ * per CU), 2 = 128 x 64, 3 = 64 x 128 (two per CU). K % 64 == 0. Replaces the same nn.Linear calls as
+ * dasa_gemm_f32x6 (vilmodel.py:179-309). */
+int dasa_gemm_f32x6_k64(const dasa_gemm_desc* d, int64_t plane, int32_t form, void* stream);
 /* x [rows][ldx] fp32 -> y = three bf16 planes [3][rows][cols] (hi, mid, lo; plane stride rows*cols),
  * x = hi + mid + lo exactly for normal fp32 values; cols % 8 == 0, 16-B aligned x and y. */
 int dasa_f32_split3_bf16(const float* x, int64_t ldx, uint16_t* y, int32_t rows, int32_t cols, void* stream);

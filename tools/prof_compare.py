@@ -7,6 +7,7 @@ from collections import defaultdict
 
 FAMILY_PREFIX = [
     ("gemm_x6", ("gemm_f32x6_nt_kernel",)),
+    ("gemm_x6_tn", ("gemm_f32x6_tn_kernel",)),
     ("gemm_bf16", ("gemm_bf16_nt_kernel",)),
     ("gemm_skinny", ("gemm_skinny_nt_kernel", "gemm_skinny_nn_kernel")),
     ("gemm", ("gemm_f32_kernel", "gemm_nt_k64_kernel", "gemm_nt_glds_kernel")),   # (split-K reduce apart)
