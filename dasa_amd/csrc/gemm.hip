@@ -2409,9 +2409,9 @@ static bool x6_lds1() {
 // tile rows / columns of each bf16x6 form (the kernel instantiations of dasa_gemm_f32x6_ws)
 static int x6_form_bm(int cfg) {
   return (cfg == 1 || cfg == 3 || cfg == 6 || cfg == 7 || cfg == 12 || cfg == 13) ? 256
-         : (cfg == 4 || cfg == 5) ? 64 : 128;
+         : (cfg == 4 || cfg == 5 || cfg == 28) ? 64 : 128;
 }
-static int x6_form_bn(int cfg) { return cfg == 5 ? 64 : 128; }
+static int x6_form_bn(int cfg) { return (cfg == 5 || cfg == 27) ? 64 : 128; }
 
 static X6Plan x6_plan(const dasa_gemm_desc* d) {
   const int M = d->M, N = d->N, K = d->K, batch = d->batch < 1 ? 1 : d->batch;
@@ -2614,6 +2614,12 @@ static int x6_run(const dasa_gemm_desc* d, X6Plan pl, int64_t plane, void* ws, i
     case 15: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, false, 2>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
     case 16: hipLaunchKernelGGL((gemm_f32x6_dma_kernel<128, 128, 4, 2>), grid, dim3(512), 0, st, p, (long)plane); break;
     case 20: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true, -1>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
+    // forms 27 / 28 (r06 probe, sweep-only): form 20's one LDS stage at half the tile (36 KB, 4 waves) so FOUR
+    // workgroups share a CU and three keep their MFMAs going while one splits / stores (form 20: one of two).
+    // Bitwise form 8; measured 0.80-0.90x form 20 on the many-tile shapes (profiles/r06/k64/probe_quarter.log):
+    // twice the tiles re-read A / W through L2 and the 128-VGPR budget spills 3-9 registers
+    case 27: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 64, 2, 2, true, -1>), grid, dim3(256), 0, st, p, (long)plane, xs); break;
+    case 28: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<64, 128, 2, 2, true, -1>), grid, dim3(256), 0, st, p, (long)plane, xs); break;
     case 26: hipLaunchKernelGGL((gemm_f32x6_nt_kernel<128, 128, 4, 2, true, 2, false, 3>), grid, dim3(512), 0, st, p, (long)plane, xs); break;
     case 21: hipLaunchKernelGGL((gemm_f32x6_ra_kernel<128, 128, 2, 2>), grid, dim3(256), 0, st, p, (long)plane); break;
     case 22: hipLaunchKernelGGL((gemm_f32x6_ra_kernel<128, 128, 4, 2>), grid, dim3(512), 0, st, p, (long)plane); break;

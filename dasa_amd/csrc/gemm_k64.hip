@@ -154,7 +154,7 @@ void gemm_f32x6_k64_kernel(GemmP p, long plane) {
 
 // C = epilogue(A . W^T) at fp32 accuracy with 64-deep K steps; W pre-split (dasa_f32_split3_bf16: d->B = hi
 // plane, planes `plane` bf16 elements apart), A fp32. K % 64 == 0, lda % 4, ldb / plane % 8, 16-B aligned
-// A / W. form 1 / 2 / 3 as above. Probe and plan entry (gemm.hip's x6 plan routes here when it wins).
+// A / W. form 1 / 2 / 3 as above. Probe entry only (measured slower above: no plan routes here).
 extern "C" int dasa_gemm_f32x6_k64(const dasa_gemm_desc* d, int64_t plane, int32_t form, void* stream) {
   if (!d) return (int)hipErrorInvalidValue;
   const int M = d->M, N = d->N, K = d->K, batch = d->batch < 1 ? 1 : d->batch;

@@ -379,9 +379,25 @@ extern "C" int dasa_bilstm_set_mode(int mode) {
   return 0;
 }
 
+// Step path at B > 32 (configs[4]'s B = 256 rollout, or DASA_LSTM_MODE=1): W_hh of both directions is converted
+// ONCE per call into the workspace — three bf16 planes [dir][plane][4H][H] for the bf16x6 fp32 GEMM, or one bf16
+// copy [dir][4H][H] in bf16 mode (dasa_bilstm_fwd_bf16) — and each timestep's recurrent product of both
+// directions is ONE batched GEMM (batch = direction) instead of two native fp32 launches.
+static bool step_gemm_path(int B, int H) { return B > 32 && (lstm_mode() == 1 || !bilstm_persist_fwd_ok(B, H)); }
+static long step_planes_floats(int H) { return 12L * H * H; }   // 2 dirs x 3 planes x 4H x H bf16
+
+static int g_fwd_bf16 = 0;
+extern "C" int dasa_bilstm_fwd_bf16(int32_t on) {
+  const int prev = g_fwd_bf16;
+  if (on >= 0) g_fwd_bf16 = on ? 1 : 0;
+  return prev;
+}
+
 extern "C" int64_t dasa_bilstm_workspace(int32_t B, int32_t H) {
   const long base = 6L * B * H;
-  return (int64_t)((B <= 32 ? base : base + 8L * B * H) * sizeof(float));
+  long n = B <= 32 ? base : base + 8L * B * H;
+  if (step_gemm_path(B, H)) n += step_planes_floats(H);
+  return (int64_t)(n * sizeof(float));
 }
 
 extern "C" int dasa_bilstm_fwd(const float* xproj, const float* whh_fwd, const float* whh_bwd,
@@ -409,11 +425,39 @@ extern "C" int dasa_bilstm_fwd(const float* xproj, const float* whh_fwd, const f
     return (int)hipErrorInvalidValue;
   }
   SeqArgs a{xproj, whh_fwd, whh_bwd, lengths, out, h0, h1, c, save_act, save_c, nullptr, B, L, H};
+  // the batched recurrent product of the step path (above): planes after the recurrent-gate buffer
+  const bool bf = g_fwd_bf16 != 0, x6 = !bf && bilstm_fwd_x6_on();
+  const bool planes = step_gemm_path(B, H) && (bf || x6) && H % 64 == 0;
+  uint16_t* wp = reinterpret_cast<uint16_t*>(rec + 8L * B * H);
+  const long WH = 4L * H * H;   // elements of one direction's W_hh
+  if (planes) {
+    int rc = 0;
+    if (bf) {
+      rc = dasa_f32_to_bf16(whh_fwd, wp, WH, stream);
+      if (!rc) rc = dasa_f32_to_bf16(whh_bwd, wp + WH, WH, stream);
+    } else {
+      rc = dasa_f32_split3_bf16(whh_fwd, H, wp, 4 * H, H, stream);
+      if (!rc) rc = dasa_f32_split3_bf16(whh_bwd, H, wp + 3 * WH, 4 * H, H, stream);
+    }
+    if (rc) return rc;
+  }
   for (int s = 0; s < L; ++s) {
     a.hin = (s & 1) ? h1 : h0;
     a.hout = (s & 1) ? h0 : h1;
     if (B <= 32) {
       hipLaunchKernelGGL(bilstm_step_fused_kernel, dim3(H / kFwdUnits, 2), dim3(1024), 0, st, a, s);
+      DASA_CHECK_LAUNCH();
+    } else if (planes) {
+      dasa_gemm_desc d{};
+      d.M = B; d.N = 4 * H; d.K = H; d.batch = 2; d.opA = 0; d.opB = 1;
+      d.A = a.hin; d.lda = H; d.strideA = (long)B * H;
+      d.B = reinterpret_cast<const float*>(wp); d.ldb = H; d.strideB = bf ? WH : 3 * WH;
+      d.C = rec; d.ldc = 4 * H; d.strideC = 4L * B * H;
+      d.alpha = 1.f; d.beta = 0.f;
+      const int rc = bf ? dasa_gemm_bf16_ex(&d, 0, stream) : dasa_gemm_f32x6_ws(&d, WH, nullptr, 0, stream);
+      if (rc) return rc;
+      a.rec = rec;
+      hipLaunchKernelGGL(bilstm_step_cell_kernel, dim3(cdivi(S, 256)), dim3(256), 0, st, a, s);
       DASA_CHECK_LAUNCH();
     } else {
       for (int dir = 0; dir < 2; ++dir) {

@@ -635,6 +635,7 @@ static bool fwd_x6() {
   }
   return g_fwd_x6 != 0;
 }
+bool bilstm_fwd_x6_on() { return fwd_x6(); }
 extern "C" int dasa_bilstm_fwd_x6(int32_t on) {
   const int prev = fwd_x6() ? 1 : 0;
   if (on >= 0) g_fwd_x6 = on ? 1 : 0;

@@ -136,8 +136,9 @@ def gemm(A, B, C, *, M, N, K, opA=0, opB=1, lda, ldb, ldc, bias=None, act=None, 
 
 # bf16 matmul mode (BASELINE configs[4]: B = 256, bf16 weights/operands with fp32 accumulation).
 # Forward-only: nn.Linear forwards whose K % 64 == 0 run dasa_gemm_bf16 on a bf16 copy of the weight
-# (converted once per weight version); LayerNorm, softmax, attention cores, the LSTM recurrences and
-# every elementwise op stay fp32.
+# (converted once per weight version), and the bi-LSTM's per-timestep recurrent product at B > 192 runs on
+# bf16 W_hh / h with fp32 accumulation (dasa_bilstm_fwd_bf16); LayerNorm, softmax, attention cores, the
+# cell updates and every elementwise op stay fp32.
 _BF16 = {"on": False, "acts": os.environ.get("DASA_BF16_ACTS", "1") != "0"}
 _bf16_w = {}
 
@@ -150,10 +151,12 @@ class bf16_matmul:
             raise _lib.DasaError("bf16 matmul mode is forward-only: enter it under torch.no_grad()")
         self._prev = _BF16["on"]
         _BF16["on"] = True
+        self._prev_lstm = _lib.lib().dasa_bilstm_fwd_bf16(1)
         return self
 
     def __exit__(self, *exc):
         _BF16["on"] = self._prev
+        _lib.lib().dasa_bilstm_fwd_bf16(self._prev_lstm)
         if not self._prev:
             _bf16_w.clear()
         return False

@@ -250,7 +250,8 @@ int dasa_lstm_cell_bwd(const float* act_save, const float* c_prev, const float* 
  * whh_fwd/whh_bwd [4H][H] (weight_hh_l0 / weight_hh_l0_reverse); lengths [B] int32 (any order).
  * Writes out [B][L][2H] ([fwd,bwd]),
  * h_n/c_n [2][B][H], and (if save != NULL) save = {act [L][2][B][4H], c [L][2][B][H]}.
- * ws: dasa_bilstm_workspace(B, H) bytes (ping-pong state; + recurrent gates when B > 32).        */
+ * ws: dasa_bilstm_workspace(B, H) bytes (ping-pong state; + recurrent gates when B > 32; + the converted
+ * W_hh of the step path, dasa_bilstm_fwd_bf16).                                                   */
 int64_t dasa_bilstm_workspace(int32_t B, int32_t H);
 int dasa_bilstm_fwd(const float* xproj, const float* whh_fwd, const float* whh_bwd,
                     const int32_t* lengths, float* out, float* h_n, float* c_n, float* save_act,
@@ -269,6 +270,12 @@ int dasa_bilstm_bwd(const float* whh_fwd, const float* whh_bwd, const int32_t* l
  * per sequence when B <= 32 and H is a multiple of 256 up to 1024, else one launch per timestep),
  * 1 = per-timestep launches only, 2 = persistent only (error when not eligible). Host-only setting. */
 int dasa_bilstm_set_mode(int mode);
+/* Forward step path at B > 32 (one launch per timestep: B > 192, e.g. configs[4]'s B = 256, or mode 1): the
+ * recurrent product of both directions is one batched GEMM per timestep on W_hh converted once per call in
+ * the workspace — the bf16x6 fp32 GEMM (dasa_bilstm_fwd_x6 on, the default) or, with on = 1 here, bf16
+ * W_hh and h (rounded on load) with fp32 accumulation (configs[4]'s bf16 mode; ops.bf16_matmul sets it).
+ * < 0 only queries. Returns the previous setting. Host-only.                                      */
+int dasa_bilstm_fwd_bf16(int32_t on);
 /* B > 32 BPTT recurrent product (dgates_prev . W_hh per timestep): 1 = the bf16x6 fp32 GEMM on W_hh^T
  * pre-split per call (default; env DASA_BPTT_X6=0 or DASA_GEMM_EMU=0 start at 0), 0 = dasa_gemm_f32;
  * < 0 only queries. Returns the previous setting. Host-only.                                     */

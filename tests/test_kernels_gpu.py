@@ -443,6 +443,67 @@ def test_bilstm_persist_fwd_x6(dev, B, L, x6):
         lib.dasa_bilstm_set_mode(0)
 
 
+@pytest.mark.parametrize("x6", [1, 0])
+def test_bilstm_step_path_b256(dev, x6):
+    """B > 192 takes the per-timestep path: both directions' recurrent product as ONE batched GEMM per step on
+    W_hh converted once per call (bf16x6, fp32-accurate; x6 = 0: the native fp32 kernels, two launches)."""
+    from dasa_amd import _lib
+    lib = _lib.lib()
+    prev = lib.dasa_bilstm_fwd_x6(x6)
+    try:
+        _check_bilstm(dev, 256, 12)
+    finally:
+        lib.dasa_bilstm_fwd_x6(prev)
+
+
+def test_bilstm_step_path_bf16(dev):
+    """configs[4]'s bf16 mode (dasa_bilstm_fwd_bf16, set by ops.bf16_matmul): h and W_hh rounded to bf16 (RNE)
+    for the recurrent product, fp32 accumulation and cell. Against a float64 restatement that rounds the same
+    two operands per step: equal up to fp32 summation order (and the rare h element whose bf16 rounding flips
+    with it); against the fp32 LSTM: within bf16 precision."""
+    from dasa_amd import _lib, ops
+    lib = _lib.lib()
+    torch.manual_seed(5)
+    B, L, H = 256, 10, 1024
+    xproj = (torch.randn(B, L, 2, 4 * H) * 0.5).to(dev)
+    whh_f = (torch.rand(4 * H, H) * 0.1 - 0.05).to(dev)
+    whh_b = (torch.rand(4 * H, H) * 0.1 - 0.05).to(dev)
+    lengths = torch.randint(1, L + 1, (B,))
+    lengths[0] = L
+    li = lengths.to(torch.int32).to(dev)
+    with torch.no_grad(), ops.bf16_matmul():
+        assert lib.dasa_bilstm_fwd_bf16(-1) == 1
+        out, h_n, c_n, _ = ops.bilstm_fwd(xproj, whh_f, whh_b, li, H)
+    assert lib.dasa_bilstm_fwd_bf16(-1) == 0
+    out32, _, _, _ = ops.bilstm_fwd(xproj, whh_f, whh_b, li, H)
+
+    def ref(round_bf16):
+        xp, ln = xproj.cpu().double(), lengths
+        res = torch.zeros(B, L, 2 * H, dtype=torch.float64)
+        for d, W in enumerate((whh_f, whh_b)):
+            Wd = W.cpu()
+            Wd = (Wd.bfloat16() if round_bf16 else Wd).double()
+            h = torch.zeros(B, H, dtype=torch.float64)
+            c = torch.zeros(B, H, dtype=torch.float64)
+            for s in range(L):
+                t = s if d == 0 else L - 1 - s
+                hr = h.float().bfloat16().double() if round_bf16 else h
+                g = xp[:, t, d] + hr @ Wd.T
+                i, f, gg, o = g.split(H, 1)
+                c2 = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(gg)
+                h2 = torch.sigmoid(o) * torch.tanh(c2)
+                act = (t < ln).unsqueeze(1)
+                c = torch.where(act, c2, c)
+                h = torch.where(act, h2, h)
+                res[:, t, d * H:(d + 1) * H] = torch.where(act, h2, torch.zeros_like(h2))
+        return res
+    rb = ref(True)
+    err = (out.cpu().double() - rb).abs()
+    assert err.max() < 5e-3 and err.mean() < 1e-5, (err.max(), err.mean())
+    assert (out32.cpu().double() - ref(False)).abs().max() < 2e-5
+    assert (out.cpu() - out32.cpu()).abs().max() < 3e-2
+
+
 @pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("B,L", [(20, 80), (3, 11), (40, 9), (160, 12)])
 def test_bilstm(dev, B, L, mode):

@@ -1,8 +1,8 @@
-"""cProfile of the cfg2 training iteration's HOST side (bench.py's build_agent / train_step after warm-up):
-where the Python time of one iteration goes, to find the host work the GPU waits on (the idle gaps of
-tools/timeline.py). python tools/host_profile.py [iterations]"""
+"""cProfile of the cfg2 training iteration's HOST side (after warm-up): where the Python time between the
+kernel launches goes (the sampled rollout's host gap). cProfile's own overhead inflates
+every call; read the ratios, not the absolute times.
+    python tools/host_profile.py [iterations]"""
 import cProfile
-import io
 import os
 import pstats
 import sys
@@ -12,7 +12,7 @@ import bench  # noqa: E402
 
 
 def main():
-    n = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 1
     sys.argv = sys.argv[:1]
     a = bench.parse()
     import torch
@@ -26,14 +26,9 @@ def main():
         bench.train_step(agent)
     torch.cuda.synchronize()
     pr.disable()
-    s = io.StringIO()
-    st = pstats.Stats(pr, stream=s)
+    st = pstats.Stats(pr)
     st.sort_stats("tottime").print_stats(45)
-    print(s.getvalue())
-    s = io.StringIO()
-    st = pstats.Stats(pr, stream=s)
-    st.sort_stats("cumulative").print_stats(45)
-    print(s.getvalue())
+    st.sort_stats("cumulative").print_stats(60)
 
 
 if __name__ == "__main__":

@@ -1,4 +1,4 @@
-"""bf16x6 with 64-deep K steps (dasa_gemm_f32x6_k64, forms 1-3) against the default plan and forms 8 / 20 / 7 on
+"""bf16x6 with 64-deep K steps (dasa_gemm_f32x6_k64, forms 1-3; PROBE_SET=quarter: forms 27 / 28) against the default plan and forms 8 / 20 / 7 on
 the language-pipe, LXRT and vision shapes, graph-timed; bitwise check against form 8 (one launch, no split).
     python tools/k64_probe.py [reps]"""
 import ctypes
@@ -53,14 +53,21 @@ def main():
 
         line = f"{M:>5}x{N:>5}x{K:>5}"
         res = {}
-        for name, fn in (("default", run_default), ("f8", forced(8)), ("f20", forced(20)), ("f7", forced(7)),
-                         ("k64_1", k64(1)), ("k64_2", k64(2)), ("k64_3", k64(3))):
+        cases = (("default", run_default), ("f8", forced(8)), ("f20", forced(20)), ("f7", forced(7)),
+                 ("k64_1", k64(1)), ("k64_2", k64(2)), ("k64_3", k64(3)))
+        if os.environ.get("PROBE_SET") == "quarter":   # forms 27 / 28: four workgroups per CU
+            cases = (("default", run_default), ("f8", forced(8)), ("f20", forced(20)), ("f27", forced(27)),
+                     ("f28", forced(28)))
+        if os.environ.get("PROBE_SET") == "order":   # is the first case of a shape slower (order effect)?
+            cases = (("f20", forced(20)), ("default", run_default), ("f20b", forced(20)), ("default2", run_default))
+        for name, fn in cases:
             us = _time_graph(fn, reps)
             fn()
             torch.cuda.synchronize()
             res[name] = y.clone()
             line += f" | {name} {us:7.1f}us {fl / us / 1e6:5.1f}TF"
-        eq = {k: torch.equal(res[k], res["f8"]) for k in ("k64_1", "k64_2", "k64_3", "f20")}
+        ref = res.get("f8", res.get("f20"))
+        eq = {k: torch.equal(res[k], ref) for k in res if k not in ("default", "f8")}
         print(line + f" | bitwise==f8 {eq}", flush=True)
         del A, W, wp, y
         torch.cuda.empty_cache()

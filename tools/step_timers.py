@@ -45,6 +45,13 @@ def main():
             wrap(agent, name)
     wrap(agent.env, "_get_obs", "env._get_obs")
     wrap(agent.encoder, "forward", "encoder.forward")
+    wrap(agent.encoder.bert, "forward", "bert.forward (LXRT region)")
+    from dasa_amd.r2r import r2rmodel
+    from dasa_amd import functional as DF
+    wrap(r2rmodel._LangPipe, "pump", "_LangPipe.pump")
+    wrap(r2rmodel._LangPipe, "take", "_LangPipe.take")
+    wrap(DF.BiLSTMFn, "apply", "BiLSTMFn.apply")
+    wrap(agent.decoder, "forward", "decoder.forward")
     orig_cpu = torch.Tensor.cpu
 
     def cpu(self, *a, **k):
