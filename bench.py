@@ -239,7 +239,10 @@ def cpu_baseline(a):
                        f"{r['cpu_model']})"),
             "fwd_cfg2": w["cfg2_fwd"]["value"], "fwd_cfg1": w["cfg1_fwd"]["value"], "workloads": w,
             "validation": "profiles/r02/cpu_restatement_vs_reference.json (restatement / reference in the survey "
-                          "container, 8 threads: cfg2 train 0.97, cfg2 fwd 0.86, cfg1 fwd 0.70)"}
+                          "container, 8 threads: cfg2 train 0.97, cfg2 fwd 0.86, cfg1 fwd 0.70); at the headline "
+                          "length (maxAction 35) profiles/r06/cpu_baseline_t35_vs_reference.json: restatement 1.96, "
+                          "reference 4.82 decisions/s (0.41) - the sample above overstates the per-decision CPU "
+                          "rate of the full-length iteration"}
 
 
 class _HostInputEnv:

@@ -137,8 +137,8 @@ int dasa_gemm_f32x6_pp(const dasa_gemm_desc* d, int64_t wplane, int64_t aplane, 
 /* bf16x6 NT GEMM with 64-deep K steps (gemm_k64.hip): one LDS stage holds a 64-deep slab, so every wave runs
  * twice the MFMAs between barriers; bitwise equal to dasa_gemm_f32x6's one-launch 128 x 128 form. Same operands
  * as dasa_gemm_f32x6 (A fp32, W pre-split with plane stride `plane`); form 1 = 128 x 128 tiles (one workgroup
- * per CU), 2 = 128 x 64, 3 = 64 x 128 (two per CU). K % 64 == 0. Replaces the same nn.Linear calls as
- * dasa_gemm_f32x6 (vilmodel.py:179-309). */
+ * per CU), 2 = 128 x 64, 3 = 64 x 128 (two per CU). K % 64 == 0. Probe entry (measured 0.70-0.80x the
+ * dasa_gemm_f32x6 plan; no plan routes here) for the same nn.Linear calls (vilmodel.py:179-309). */
 int dasa_gemm_f32x6_k64(const dasa_gemm_desc* d, int64_t plane, int32_t form, void* stream);
 /* x [rows][ldx] fp32 -> y = three bf16 planes [3][rows][cols] (hi, mid, lo; plane stride rows*cols),
  * x = hi + mid + lo exactly for normal fp32 values; cols % 8 == 0, 16-B aligned x and y. */

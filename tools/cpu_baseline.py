@@ -111,7 +111,7 @@ def run(cores=None, which=("cfg2_train", "cfg2_fwd", "cfg1_fwd"), reps=3):
             res[name] = {"value": round(rate, 3), "unit": "agent-decisions/s", "sample": desc,
                          "times_s": [round(t, 2) for t in times]}
         return {"cores": cores, "cpu_model": cpu_model(), "kind": "port", "workloads": res,
-                "method": "1 warm-up + median of 3; torch.set_num_threads(cores); oracle/policy.py (CPU restatement)"}
+                "method": f"1 warm-up + median of {reps}; torch.set_num_threads(cores); oracle/policy.py (CPU restatement)"}
     finally:
         torch.set_num_threads(prev)
 
