@@ -73,6 +73,7 @@ SIGNATURES = {
     "dasa_gemm_x6_set_tail": (i32, [i32]),
     "dasa_gemm_skinny_tune": (i32, [i32, i32]),
     "dasa_layernorm_fwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, f32, f32, u64, vp]),
+    "dasa_layernorm_fwd_bf16": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, f32, f32, u64, vp]),
     "dasa_layernorm_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp]),
     "dasa_bert_embed_fwd": (i32, [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, f32, f32, u64, vp]),
     "dasa_mha_fwd": (i32, [vp, i64, vp, i64, vp, i64, vp, vp, i64, vp, i32, i32, i32, i32, i32, f32, f32, u64, vp]),

@@ -25,7 +25,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
                                                      float* __restrict__ y, float* __restrict__ mean_out,
                                                      float* __restrict__ rstd_out, float* __restrict__ xsum,
                                                      int M, int N, float eps, float p, uint64_t seed,
-                                                     const uint64_t* seed_src) {
+                                                     const uint64_t* seed_src, unsigned short* __restrict__ ybf) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= M) return;
   if (p > 0.f) seed = eff_seed(seed, seed_src);
@@ -95,6 +95,13 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
       o.z = (v[i].z - mean) * rstd * g.z + bb.z;
       o.w = (v[i].w - mean) * rstd * g.w + bb.w;
       y4[c] = o;
+      if (ybf) {   // the bf16 twin (RNE), bitwise what a bf16 GEMM rounding y on load would use
+        const uint2 u = {(unsigned)__builtin_bit_cast(unsigned short, (__bf16)o.x) |
+                             ((unsigned)__builtin_bit_cast(unsigned short, (__bf16)o.y) << 16),
+                         (unsigned)__builtin_bit_cast(unsigned short, (__bf16)o.z) |
+                             ((unsigned)__builtin_bit_cast(unsigned short, (__bf16)o.w) << 16)};
+        reinterpret_cast<uint2*>(ybf + (long)row * N)[c] = u;
+      }
     }
   }
   if (lane == 0) {
@@ -798,16 +805,22 @@ extern "C" const char* dasa_build_info(void) { return "libdasa_hip gfx950 (CDNA4
   } while (0)
 #define DASA_VPL_DISPATCH(N, KERNEL, GRID, ...) DASA_VPL_DISPATCH_B(N, KERNEL, GRID, 256, __VA_ARGS__)
 
+extern "C" int dasa_layernorm_fwd_bf16(const float* x, const float* res, const float* gamma, const float* beta,
+                                       float* y, uint16_t* ybf, float* mean, float* rstd, float* xsum, int32_t M,
+                                       int32_t N, float eps, float drop_p, uint64_t seed, void* stream) {
+  if (M <= 0) return 0;
+  if ((N & 3) || N > 8192 || ((uintptr_t)ybf & 7)) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  DASA_VPL_DISPATCH(N, ln_fwd_kernel, dim3(cdivi(M, 4)), x, res, gamma, beta, y, mean, rstd, xsum, M, N, eps, drop_p,
+                    seed, drop_p > 0.f ? dasa_seed_src_host() : nullptr, reinterpret_cast<unsigned short*>(ybf));
+  DASA_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int dasa_layernorm_fwd(const float* x, const float* res, const float* gamma, const float* beta, float* y,
                                   float* mean, float* rstd, float* xsum, int32_t M, int32_t N, float eps,
                                   float drop_p, uint64_t seed, void* stream) {
-  if (M <= 0) return 0;
-  if ((N & 3) || N > 8192) return (int)hipErrorInvalidValue;
-  hipStream_t st = (hipStream_t)stream;
-  DASA_VPL_DISPATCH(N, ln_fwd_kernel, dim3(cdivi(M, 4)), x, res, gamma, beta, y, mean, rstd, xsum, M, N, eps, drop_p,
-                    seed, drop_p > 0.f ? dasa_seed_src_host() : nullptr);
-  DASA_CHECK_LAUNCH();
-  return 0;
+  return dasa_layernorm_fwd_bf16(x, res, gamma, beta, y, nullptr, mean, rstd, xsum, M, N, eps, drop_p, seed, stream);
 }
 
 extern "C" int dasa_layernorm_bwd(const float* dy, const float* xsum, const float* gamma, const float* mean,

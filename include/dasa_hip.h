@@ -151,6 +151,11 @@ int dasa_f32_split3_bf16(const float* x, int64_t ldx, uint16_t* y, int32_t rows,
 int dasa_layernorm_fwd(const float* x, const float* res, const float* gamma, const float* beta,
                        float* y, float* mean, float* rstd, float* xsum, int32_t M, int32_t N, float eps,
                        float drop_p, uint64_t seed, void* stream);
+/* The same, also writing ybf = bf16(y) (RNE; 8-B aligned, [M][N]): configs[4]'s bf16 mode hands it to the next
+ * bf16 GEMM as its A operand — bitwise what that GEMM would round y to on load, at half the A bytes.       */
+int dasa_layernorm_fwd_bf16(const float* x, const float* res, const float* gamma, const float* beta,
+                            float* y, uint16_t* ybf, float* mean, float* rstd, float* xsum, int32_t M, int32_t N,
+                            float eps, float drop_p, uint64_t seed, void* stream);
 /* dx = dLN/d(xsum) (= grad of both x-after-dropout and res); dgamma/dbeta accumulated (+=) by a
  * fixed-order column reduction in the same launch (deterministic, no atomics). */
 int dasa_layernorm_bwd(const float* dy, const float* xsum, const float* gamma, const float* mean,

@@ -1001,6 +1001,30 @@ def test_gemm_bf16_activations(dev, M):
         ops.linear(hbf, W2, b2)
 
 
+@pytest.mark.parametrize("M", [300, 5120])
+def test_layernorm_bf16_twin(dev, M):
+    """configs[4]'s bf16 mode: LayerNorm also writes bf16(y) (dasa_layernorm_fwd_bf16) and the next bf16 GEMM takes
+    it as its A operand. y is bitwise the plain LayerNorm's, the twin is torch's RNE rounding of y bit for bit,
+    and the GEMM reading the twin equals the GEMM rounding the fp32 y on load bit for bit (both tile forms)."""
+    from dasa_amd import ops
+    g = torch.Generator().manual_seed(M + 1)
+    K, N = 768, 2304
+    x, r = _rand(M, K, g=g).to(dev), _rand(M, K, g=g).to(dev)
+    gam, bet = (1 + _rand(K, g=g, scale=0.1)).to(dev), _rand(K, g=g, scale=0.1).to(dev)
+    W, b = _rand(N, K, g=g, scale=0.05).to(dev), _rand(N, g=g).to(dev)
+    y_plain = ops.layernorm(x, gam, bet, 1e-12, res=r)
+    assert getattr(y_plain, "_dasa_bf16", None) is None
+    with torch.no_grad(), ops.bf16_matmul():
+        y = ops.layernorm(x, gam, bet, 1e-12, res=r)
+        twin = y._dasa_bf16[0]
+        z_twin = ops.linear(y, W, b)
+        z_load = ops.linear(y.clone(), W, b)       # no twin: A rounded on load
+    torch.cuda.synchronize()
+    assert torch.equal(y, y_plain)
+    assert torch.equal(twin.view(torch.int16), y.to(torch.bfloat16).view(torch.int16))
+    assert torch.equal(z_twin, z_load)
+
+
 def test_bf16_mode_is_forward_only(dev):
     from dasa_amd import ops, _lib
     with pytest.raises(_lib.DasaError):

@@ -28,7 +28,12 @@ def main():
         y = torch.empty(M, N, device=dev)
         with torch.no_grad(), ops.bf16_matmul():
             us = _time_graph(lambda: ops.linear(x, W, b, out=y), reps=20)
+            us = _time_graph(lambda: ops.linear(x, W, b, out=y), reps=20)   # (the first timing of a shape runs slow)
             line = f"{M:>6}x{N:>5}x{K:>5}  {us:8.1f} us  {2.0 * M * N * K / us / 1e6:6.1f} TF"
+            if "--abf" in sys.argv:   # the same GEMM with A already bf16 (a producer that rounded it)
+                xb = ops.to_bf16(x)
+                ub = _time_graph(lambda: ops.linear(xb, W, b, out=y), reps=20)
+                line += f" | bf16 A {ub:7.1f} us {2.0 * M * N * K / ub / 1e6:6.1f} TF"
             ref = y.clone()
             for f in forms:
                 lib.dasa_gemm_force_config((1 << 20) + f)
