@@ -227,6 +227,10 @@ class LinearFn(torch.autograd.Function):
         ctx.has_b = b is not None
         ctx.params = _Kept((W, b))
         need = any(ctx.needs_input_grad)
+        if need and x.dtype == torch.bfloat16:
+            # a bf16 activation (the bf16 GELU hand-off of configs[4]'s matmul mode) reaching a layer whose
+            # weight still trains: the fp32 weight-gradient GEMM takes the same values widened to fp32
+            x = x.float()
         if need and act == "gelu":
             z = ops.linear(x, W, b)
             y = ops.act_fwd(z, "gelu")

@@ -34,6 +34,10 @@ def main():
                 xb = ops.to_bf16(x)
                 ub = _time_graph(lambda: ops.linear(xb, W, b, out=y), reps=20)
                 line += f" | bf16 A {ub:7.1f} us {2.0 * M * N * K / ub / 1e6:6.1f} TF"
+            if "--torch" in sys.argv:   # hipBLASLt (torch bf16 linear, bf16 out) on the same shape: what a library reaches
+                xb16, Wb16, bb16 = x.to(torch.bfloat16), W.to(torch.bfloat16), b.to(torch.bfloat16)
+                ut = _time_graph(lambda: torch.nn.functional.linear(xb16, Wb16, bb16), reps=20)
+                line += f" | torch {ut:7.1f} us {2.0 * M * N * K / ut / 1e6:6.1f} TF"
             ref = y.clone()
             for f in forms:
                 lib.dasa_gemm_force_config((1 << 20) + f)

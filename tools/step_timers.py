@@ -51,7 +51,24 @@ def main():
     wrap(r2rmodel._LangPipe, "pump", "_LangPipe.pump")
     wrap(r2rmodel._LangPipe, "take", "_LangPipe.take")
     wrap(DF.BiLSTMFn, "apply", "BiLSTMFn.apply")
-    wrap(agent.decoder, "forward", "decoder.forward")
+    # (not agent.decoder.forward: a wrapped forward makes the agent run the decoder eagerly, _train_graph_ok)
+    store = getattr(agent.env, "_store", None)
+    if store is not None:   # the device feature store's host staging (DeviceFeatureEnv)
+        wrap(store, "_step_arrays", "store._step_arrays")
+        wrap(store, "input_feat_steps", "store.input_feat_steps")
+    from dasa_amd import ops
+    wrap(ops, "gather_rows", "ops.gather_rows")
+    orig_pin = torch.Tensor.pin_memory
+
+    def pin(self, *a, **k):
+        t0 = time.perf_counter()
+        try:
+            return orig_pin(self, *a, **k)
+        finally:
+            e = ACC["Tensor.pin_memory"]
+            e[0] += 1
+            e[1] += time.perf_counter() - t0
+    torch.Tensor.pin_memory = pin
     orig_cpu = torch.Tensor.cpu
 
     def cpu(self, *a, **k):
@@ -69,6 +86,7 @@ def main():
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     torch.Tensor.cpu = orig_cpu
+    torch.Tensor.pin_memory = orig_pin
     print(f"{n} iterations, {wall / n * 1e3:.1f} ms each")
     print(f"{'phase':42s} {'calls/it':>9s} {'ms/it':>8s} {'us/call':>8s}")
     for k, (c, s) in sorted(ACC.items(), key=lambda kv: -kv[1][1]):
