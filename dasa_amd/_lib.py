@@ -77,6 +77,7 @@ SIGNATURES = {
     "dasa_layernorm_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp]),
     "dasa_bert_embed_fwd": (i32, [vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, f32, f32, u64, vp]),
     "dasa_mha_fwd": (i32, [vp, i64, vp, i64, vp, i64, vp, vp, i64, vp, i32, i32, i32, i32, i32, f32, f32, u64, vp]),
+    "dasa_mha_fwd_bf16": (i32, [vp, i64, vp, i64, vp, i64, vp, vp, i64, i32, i32, i32, i32, i32, i32, f32, f32, u64, vp]),
     "dasa_mha_bwd": (i32, [vp, i64, vp, i64, vp, i64, vp, vp, i64, vp, vp, vp, i32, i32, i32, i32, i32, f32, f32, u64,
                            vp]),
     "dasa_softdot_fwd": (i32, [vp, vp, i64, vp, vp, vp, vp, i32, i32, i32, vp, vp]),

@@ -785,6 +785,144 @@ __global__ __launch_bounds__(256) void adain_musigma_bwd_kernel(const float* __r
   }
 }
 
+// ---- bf16 attention core (BASELINE configs[4]'s bf16 mode: bf16 activations, fp32 accumulation) ------
+// mha_fwd_kernel's structure on v_mfma_f32_32x32x16_bf16: Q / K / V arrive as bf16 (the fused QKV GEMM's
+// bf16 output), S^T = K Q^T and O = P V accumulate in fp32, the scale / mask / softmax run in fp32 on the
+// accumulator and P is rounded to bf16 (RNE) as the P V operand. One workgroup per (batch, head), one wave
+// per 32-query tile. K is staged in LDS row-major ([key][64] bf16, 144-B rows: conflict-free 16-B fragment
+// reads); V is staged TRANSPOSED ([dim][key], 272-B rows), because the P V B-operand of lane (dim d, half
+// hh) is 8 keys of one dim: with the probability accumulator as the A operand, k-slot i of half hh is key
+// 16u + (i & 3) + 8 (i >> 2) + 4 hh of the 32-key tile (u = 0, 1: the tile's two 16-key MFMAs) — the
+// accumulator rows acc_row(8u + i, hh) — i.e. two runs of 4 consecutive keys: two ds_read_b64 per MFMA.
+// The output is fp32, or bf16 (RNE) for a bf16 consumer (the attention output projection).
+typedef short mha_bf16x8 __attribute__((ext_vector_type(8)));
+constexpr int kKLdH = kDh + 8;     // K rows in LDS (bf16 elements)
+constexpr int kVtLdH = kMaxLk + 8;  // V^T rows in LDS (bf16 elements)
+
+struct MhaBfArgs {
+  const unsigned short* Q; long ldq; const unsigned short* K; long ldk; const unsigned short* V; long ldv;
+  const float* mask; void* out; long ldo;
+  int B, heads, Lq, Lk; float scale; float p; uint64_t seed; const uint64_t* seed_src;
+};
+
+__device__ __forceinline__ unsigned short bf16_rne(float x) { return __builtin_bit_cast(unsigned short, (__bf16)x); }
+
+template <int NKT, bool OBF>
+__global__ __launch_bounds__(256) void mha_fwd_bf16_kernel(MhaBfArgs a, int nqt) {
+  __shared__ __attribute__((aligned(16))) unsigned short ks[NKT * 32 * kKLdH];
+  __shared__ __attribute__((aligned(16))) unsigned short vt[kDh * kVtLdH];
+  __shared__ float ms[NKT * 32];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int bh = blockIdx.x, h = bh % a.heads, b = bh / a.heads;
+  const int Lq = a.Lq, Lk = a.Lk;
+  const uint64_t seed = a.p > 0.f ? eff_seed(a.seed, a.seed_src) : 0;
+  const int q0 = w * 32, j = lane & 31, hh = lane >> 5;
+  // every global load first: this wave's Q fragments (B operand of S^T: lane (query j, half hh) holds
+  // Q[q0 + j][16 s + 8 hh .. +7]), the K / V rows of the head (16-B pieces, rows clamped) and the mask
+  const unsigned short* qp = a.Q + ((long)b * Lq + min(q0 + j, Lq - 1)) * a.ldq + h * kDh + 8 * hh;
+  mha_bf16x8 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = *reinterpret_cast<const mha_bf16x8*>(qp + 16 * s);
+  uint4 kx[NKT], vx[NKT];   // NKT * 32 rows x 8 pieces over 256 threads
+#pragma unroll
+  for (int i = 0; i < NKT; ++i) {
+    const int idx = threadIdx.x + 256 * i, row = min(idx >> 3, Lk - 1), c = idx & 7;
+    kx[i] = *reinterpret_cast<const uint4*>(a.K + ((long)b * Lk + row) * a.ldk + h * kDh + 8 * c);
+    vx[i] = *reinterpret_cast<const uint4*>(a.V + ((long)b * Lk + row) * a.ldv + h * kDh + 8 * c);
+  }
+  const int mk = min((int)threadIdx.x, Lk - 1);
+  const float mv = a.mask ? a.mask[(long)b * Lk + mk] : 0.f;
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < NKT; ++i) {
+    const int idx = threadIdx.x + 256 * i, row = idx >> 3, c = idx & 7;
+    const unsigned z = row < Lk ? 0xffffffffu : 0u;
+    *reinterpret_cast<uint4*>(ks + row * kKLdH + 8 * c) = uint4{kx[i].x & z, kx[i].y & z, kx[i].z & z, kx[i].w & z};
+    const unsigned vv[4] = {vx[i].x & z, vx[i].y & z, vx[i].z & z, vx[i].w & z};
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      vt[(8 * c + e) * kVtLdH + row] = (unsigned short)(vv[e >> 1] >> (16 * (e & 1)));
+  }
+  if (threadIdx.x < NKT * 32) ms[threadIdx.x] = (int)threadIdx.x < Lk ? mv : -INFINITY;
+  __syncthreads();
+  if (w >= nqt) return;   // (no barrier below)
+  floatx16 st[NKT];
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt) {
+    const unsigned short* kp = ks + (kt * 32 + j) * kKLdH + 8 * hh;
+    floatx16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const mha_bf16x8*>(kp + 16 * s), qf[s], acc, 0,
+                                                   0, 0);
+    st[kt] = acc;
+  }
+  float m = -INFINITY;
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float v = st[kt][r] * a.scale + ms[kt * 32 + acc_row(r, hh)];
+      st[kt][r] = v;
+      m = fmaxf(m, v);
+    }
+  m = fmaxf(m, __shfl_xor(m, 32));
+  float sum = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float e = __expf(st[kt][r] - m);
+      st[kt][r] = e;
+      sum += e;
+    }
+  sum += __shfl_xor(sum, 32);
+  const float inv = 1.f / sum;
+  const long prow = ((long)bh * Lq + q0 + j) * (long)Lk;   // dropout index base of this query row
+  floatx16 o0, o1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { o0[r] = 0.f; o1[r] = 0.f; }
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      mha_bf16x8 pa;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float pv = st[kt][8 * u + i] * inv;
+        if (a.p > 0.f) pv *= dasa_dropout_scale(a.p, seed, (uint64_t)(prow + kt * 32 + acc_row(8 * u + i, hh)));
+        pa[i] = (short)bf16_rne(pv);
+      }
+      const unsigned short* v0 = vt + j * kVtLdH + kt * 32 + 16 * u + 4 * hh;
+      const unsigned short* v1 = v0 + 32 * kVtLdH;
+      const uint2 a0 = *reinterpret_cast<const uint2*>(v0), b0 = *reinterpret_cast<const uint2*>(v0 + 8);
+      const uint2 a1 = *reinterpret_cast<const uint2*>(v1), b1 = *reinterpret_cast<const uint2*>(v1 + 8);
+      o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, __builtin_bit_cast(mha_bf16x8, uint4{a0.x, a0.y, b0.x, b0.y}),
+                                                  o0, 0, 0, 0);
+      o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, __builtin_bit_cast(mha_bf16x8, uint4{a1.x, a1.y, b1.x, b1.y}),
+                                                  o1, 0, 0, 0);
+    }
+  // O tile: column = dim j (+32), row = query q0 + acc_row(r, hh)
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int qq = q0 + acc_row(r, hh);
+    if (qq < Lq) {
+      const long o = ((long)b * Lq + qq) * a.ldo + h * kDh + j;
+      if (OBF) {
+        unsigned short* op = reinterpret_cast<unsigned short*>(a.out) + o;
+        op[0] = bf16_rne(o0[r]);
+        op[32] = bf16_rne(o1[r]);
+      } else {
+        float* op = reinterpret_cast<float*>(a.out) + o;
+        op[0] = o0[r];
+        op[32] = o1[r];
+      }
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int dasa_version(void) { return 2; }
@@ -869,6 +1007,35 @@ extern "C" int dasa_mha_fwd(const float* Q, int64_t ldq, const float* K, int64_t
     case 3: hipLaunchKernelGGL(mha_fwd_kernel<3>, grid, block, 0, st, a, nqt); break;
     default: hipLaunchKernelGGL(mha_fwd_kernel<4>, grid, block, 0, st, a, nqt); break;
   }
+  DASA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dasa_mha_fwd_bf16(const void* Q, int64_t ldq, const void* K, int64_t ldk, const void* V, int64_t ldv,
+                                 const float* addmask, void* out, int64_t ldo, int32_t out_bf16, int32_t B,
+                                 int32_t heads, int32_t Lq, int32_t Lk, int32_t dh, float scale, float drop_p,
+                                 uint64_t seed, void* stream) {
+  if (B <= 0 || Lq <= 0) return 0;
+  if (dh != kDh || Lk <= 0 || Lk > kMaxLk || ((ldq | ldk | ldv) & 7) ||
+      (((uintptr_t)Q | (uintptr_t)K | (uintptr_t)V) & 15) || !out)
+    return (int)hipErrorInvalidValue;
+  const int nqt = cdivi(Lq, 32);
+  if (nqt > 4) return (int)hipErrorInvalidValue;   // one wave per 32-query tile, Lq <= 128
+  MhaBfArgs a{(const unsigned short*)Q, ldq, (const unsigned short*)K, ldk, (const unsigned short*)V, ldv, addmask,
+              out, ldo, B, heads, Lq, Lk, scale, drop_p, seed, drop_p > 0.f ? dasa_seed_src_host() : nullptr};
+  const dim3 grid(B * heads), block(256);
+  hipStream_t st = (hipStream_t)stream;
+  const int nkt = cdivi(Lk, 32);
+#define DASA_MHA_BF(NKT)                                                                      \
+  if (out_bf16) hipLaunchKernelGGL((mha_fwd_bf16_kernel<NKT, true>), grid, block, 0, st, a, nqt); \
+  else hipLaunchKernelGGL((mha_fwd_bf16_kernel<NKT, false>), grid, block, 0, st, a, nqt);
+  switch (nkt) {
+    case 1: DASA_MHA_BF(1) break;
+    case 2: DASA_MHA_BF(2) break;
+    case 3: DASA_MHA_BF(3) break;
+    default: DASA_MHA_BF(4) break;
+  }
+#undef DASA_MHA_BF
   DASA_CHECK_LAUNCH();
   return 0;
 }

@@ -139,7 +139,13 @@ def gemm(A, B, C, *, M, N, K, opA=0, opB=1, lda, ldb, ldc, bias=None, act=None, 
 # (converted once per weight version), and the bi-LSTM's per-timestep recurrent product at B > 192 runs on
 # bf16 W_hh / h with fp32 accumulation (dasa_bilstm_fwd_bf16); LayerNorm, softmax, attention cores, the
 # cell updates and every elementwise op stay fp32.
-_BF16 = {"on": False, "acts": os.environ.get("DASA_BF16_ACTS", "1") != "0"}
+_BF16 = {"on": False, "acts": os.environ.get("DASA_BF16_ACTS", "1") != "0",
+         "attn": os.environ.get("DASA_BF16_ATTN", "1") != "0"}   # DASA_BF16_ATTN=0: fp32 attention core (A/B)
+
+
+def bf16_attn_on():
+    """Under bf16_matmul with bf16 activations: Q/K/V stored bf16 and the bf16 attention core."""
+    return _BF16["on"] and _BF16["acts"] and _BF16["attn"]
 _bf16_w = {}
 
 
@@ -646,6 +652,17 @@ def mha(Q, K, V, addmask, heads, scale, drop_p=0.0, seed=0, save_probs=False):
     dh = Hd // heads
     for t in (Q, K, V):   # rows may be strided views of a fused QKV buffer, heads contiguous inside a row
         assert t.stride(2) == 1 and t.stride(0) == t.shape[1] * t.stride(1)
+    if Q.dtype == torch.bfloat16 or K.dtype == torch.bfloat16 or V.dtype == torch.bfloat16:
+        # configs[4]'s bf16 mode: the bf16 attention core, bf16 output (its consumer, the attention output
+        # projection, is a bf16 GEMM that takes a bf16 A operand)
+        if not (_BF16["on"] and Q.dtype == K.dtype == V.dtype == torch.bfloat16) or save_probs:
+            raise _lib.DasaError("bf16 attention: bf16_matmul mode, bf16 Q/K/V, forward only")
+        out = torch.empty(B, Lq, Hd, dtype=torch.bfloat16, device=Q.device)
+        _call("dasa_mha_fwd_bf16", "mha", _lib.lib().dasa_mha_fwd_bf16, _p(Q), Q.stride(1), _p(K), K.stride(1), _p(V),
+              V.stride(1), _p(addmask.contiguous() if addmask is not None else None), _p(out), Hd, 1, B, heads, Lq,
+              Lk, dh, float(scale), float(drop_p), int(seed) & (2**64 - 1), _stream(),
+              flops=4.0 * B * Lq * Lk * Hd, nbytes=2.0 * B * (2 * Lq + 2 * Lk) * Hd)
+        return out
     out = torch.empty(B, Lq, Hd, dtype=torch.float32, device=Q.device)
     probs = torch.empty(B, heads, Lq, Lk, dtype=torch.float32, device=Q.device) if save_probs else None
     _call("dasa_mha_fwd", "mha", _lib.lib().dasa_mha_fwd, _p(Q), Q.stride(1), _p(K), K.stride(1), _p(V), V.stride(1),

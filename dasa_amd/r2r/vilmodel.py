@@ -73,6 +73,13 @@ def _needs_grad(*ts):
     return torch.is_grad_enabled() and any(t.requires_grad for t in ts)
 
 
+def _attn_dtype(x, N, ctx=None):
+    """Storage dtype of Q/K/V on a no-grad path: bf16 under ops.bf16_matmul with bf16 activations (the bf16
+    attention core then runs), else None (fp32)."""
+    ok = ops.bf16_acts_ok(x, N) and (ctx is None or ops.bf16_acts_ok(ctx, N))
+    return torch.bfloat16 if ok and ops.bf16_attn_on() else None
+
+
 def _fused_weights(owner, mods):
     """Concatenated [W_1; W_2; ...] / [b_1; ...] of several nn.Linear (one wide MFMA GEMM instead of
     several narrow ones), cached until any of the parameters changes (data_ptr or in-place version).
@@ -141,7 +148,8 @@ class BertSelfAttention(nn.Module):
             q, k, v = _lin(hidden_states, self.query), _lin(hidden_states, self.key), _lin(hidden_states, self.value)
         else:   # one [M, 3H] GEMM; Q/K/V are row-strided views the attention kernel reads in place
             W, b = _fused_weights(self, (self.query, self.key, self.value))
-            qkv = ops.linear(hidden_states, W, b)
+            # configs[4]'s bf16 mode: Q/K/V stored bf16 for the bf16 attention core (ops.mha)
+            qkv = ops.linear(hidden_states, W, b, out_dtype=_attn_dtype(hidden_states, W.shape[0]))
             Hs = self.all_head_size
             q, k, v = qkv[..., :Hs], qkv[..., Hs:2 * Hs], qkv[..., 2 * Hs:]
         ctx = DF.mha(q, k, v, _addmask(attention_mask, q.shape[0]), self.num_attention_heads,
@@ -248,12 +256,17 @@ class BertOutAttention(nn.Module):
         self.dropout = nn.Dropout(config.attention_probs_dropout_prob)
 
     def forward(self, hidden_states, context, attention_mask=None):
-        q = _lin(hidden_states, self.query)
-        if _needs_grad(context, self.key.weight, self.value.weight):
+        nq = _needs_grad(hidden_states, self.query.weight)
+        nkv = _needs_grad(context, self.key.weight, self.value.weight)
+        # bf16 Q/K/V for the bf16 attention core in configs[4]'s bf16 mode (no-grad only)
+        dt = None if (nq or nkv) else _attn_dtype(hidden_states, self.all_head_size, context)
+        q = _lin(hidden_states, self.query) if nq else ops.linear(hidden_states, self.query.weight, self.query.bias,
+                                                                   out_dtype=dt)
+        if nkv:
             k, v = _lin(context, self.key), _lin(context, self.value)
         else:
             W, b = _fused_weights(self, (self.key, self.value))
-            kv = ops.linear(context, W, b)
+            kv = ops.linear(context, W, b, out_dtype=dt)
             Hs = self.all_head_size
             k, v = kv[..., :Hs], kv[..., Hs:]
         return DF.mha(q, k, v, _addmask(attention_mask, q.shape[0]), self.num_attention_heads,

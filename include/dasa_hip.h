@@ -176,6 +176,13 @@ int dasa_mha_fwd(const float* Q, int64_t ldq, const float* K, int64_t ldk, const
                  const float* addmask, float* out, int64_t ldo, float* probs,
                  int32_t B, int32_t heads, int32_t Lq, int32_t Lk, int32_t dh, float scale,
                  float drop_p, uint64_t seed, void* stream);
+/* The same attention core with bf16 Q/K/V (BASELINE configs[4]'s bf16 mode, forward only): bf16 operands
+ * on v_mfma_f32_32x32x16_bf16, fp32 accumulation / scale / mask / softmax, P rounded to bf16 (RNE) for
+ * P V. Q/K/V/out are bf16 element pointers with ld in elements (ld % 8 == 0, 16-B aligned); out is bf16
+ * (RNE) when out_bf16 != 0, else fp32. No saved probabilities (no backward).                          */
+int dasa_mha_fwd_bf16(const void* Q, int64_t ldq, const void* K, int64_t ldk, const void* V, int64_t ldv,
+                      const float* addmask, void* out, int64_t ldo, int32_t out_bf16, int32_t B, int32_t heads,
+                      int32_t Lq, int32_t Lk, int32_t dh, float scale, float drop_p, uint64_t seed, void* stream);
 /* Backward; probs are the forward's saved pre-dropout softmax [B][heads][Lq][Lk], the dropout mask
  * is regenerated from (drop_p, seed). dQ/dK/dV are written with the ld of Q/K/V. Lq, Lk <= 80 with
  * 16-B aligned dQ/dK/dV take the LDS-staged form (no atomics); larger shapes the row-streaming one. */

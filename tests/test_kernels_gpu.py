@@ -1025,6 +1025,51 @@ def test_layernorm_bf16_twin(dev, M):
     assert torch.equal(z_twin, z_load)
 
 
+@pytest.mark.parametrize("B,Lq,Lk", [(3, 80, 80), (5, 36, 80), (4, 80, 36), (2, 128, 117), (7, 1, 5)])
+def test_mha_bf16(dev, B, Lq, Lk):
+    """configs[4]'s bf16 attention core (dasa_mha_fwd_bf16) through ops.mha under bf16_matmul: Q/K/V are
+    strided views of a fused bf16 QKV buffer, a -10000 key-padding mask. Against a float64 restatement that
+    takes the same bf16 Q/K/V and rounds the softmax P to bf16 (RNE) before P V, as the kernel does: within
+    2e-3 (P's rounding can flip at a tie boundary; the fp32 QK^T / softmax differ from float64 by ~1e-7);
+    the bf16 output is bitwise the fp32 output rounded (RNE)."""
+    from dasa_amd import ops, _lib
+    heads, dh = 12, 64
+    Hd = heads * dh
+    g = torch.Generator().manual_seed(B * 1000 + Lq + Lk)
+    if Lq == Lk:
+        qkv = torch.randn(B, Lq, 3 * Hd, generator=g).to(torch.bfloat16).to(dev)
+        Q, K, V = qkv[..., :Hd], qkv[..., Hd:2 * Hd], qkv[..., 2 * Hd:]
+    else:
+        Q = torch.randn(B, Lq, Hd, generator=g).to(torch.bfloat16).to(dev)
+        kv = torch.randn(B, Lk, 2 * Hd, generator=g).to(torch.bfloat16).to(dev)
+        K, V = kv[..., :Hd], kv[..., Hd:]
+    mask = torch.zeros(B, Lk)
+    for b in range(B):
+        mask[b, max(1, Lk - 3 * b):] = -10000.0
+    mask = mask.to(dev)
+    scale = 1.0 / 8.0
+    with torch.no_grad(), ops.bf16_matmul():
+        out_bf = ops.mha(Q, K, V, mask, heads, scale)
+        out32 = torch.empty(B, Lq, Hd, device=dev)
+        rc = _lib.lib().dasa_mha_fwd_bf16(Q.data_ptr(), Q.stride(1), K.data_ptr(), K.stride(1), V.data_ptr(),
+                                          V.stride(1), mask.data_ptr(), out32.data_ptr(), Hd, 0, B, heads, Lq, Lk, dh,
+                                          scale, 0.0, 0, torch.cuda.current_stream().cuda_stream)
+        assert rc == 0
+    torch.cuda.synchronize()
+    assert out_bf.dtype == torch.bfloat16
+    q = Q.double().view(B, Lq, heads, dh).transpose(1, 2)
+    k = K.double().view(B, Lk, heads, dh).transpose(1, 2)
+    v = V.double().view(B, Lk, heads, dh).transpose(1, 2)
+    s = q @ k.transpose(-1, -2) * scale + mask.double()[:, None, None, :]
+    p = torch.softmax(s, -1).float().to(torch.bfloat16).double()
+    ref = (p @ v).transpose(1, 2).reshape(B, Lq, Hd)
+    err = (out32.double() - ref).abs().max().item()
+    assert err < 2e-3, err
+    assert torch.equal(out_bf.view(torch.int16), out32.to(torch.bfloat16).view(torch.int16))
+    with torch.no_grad(), pytest.raises(_lib.DasaError):   # bf16 operands only in bf16 matmul mode
+        ops.mha(Q, K, V, mask, heads, scale)
+
+
 def test_bf16_mode_is_forward_only(dev):
     from dasa_amd import ops, _lib
     with pytest.raises(_lib.DasaError):
