@@ -57,6 +57,7 @@ SIGNATURES = {
     "dasa_gemm_bf16": (i32, [C.POINTER(GemmDesc), vp]),
     "dasa_copy_segments": (i32, [C.POINTER(CopySeg), i32, vp]),
     "dasa_gemm_bf16_ex": (i32, [C.POINTER(GemmDesc), i32, vp]),
+    "dasa_gemm_bf16_dma": (i32, [i32]),
     "dasa_f32_to_bf16": (i32, [vp, vp, i64, vp]),
     "dasa_gemm_f32x6": (i32, [C.POINTER(GemmDesc), i64, vp]),
     "dasa_gemm_f32x6_workspace": (i64, [C.POINTER(GemmDesc)]),

@@ -1930,6 +1930,154 @@ __global__ __launch_bounds__(256, 2) void gemm_skinny_nn_kernel(GemmP p, SkinnyP
   skinny_store<16 * MT>(p, mm, nn, v);
 }
 
+
+// ---- bf16 NT GEMM with both operands by LDS-DMA (configs[4]'s bf16 mode, A already bf16) -------------
+// gemm_bf16_nt_kernel stages A and W through VGPRs (global load -> ds_write, a __syncthreads per K tile):
+// 0.55-0.70x hipBLASLt on the configs[4] shapes (profiles/r06/bf16_vs_hipblaslt.log). With A already bf16
+// (a producer rounded it: the LayerNorm twin, the GELU / attention outputs) both operands can go HBM / L2 ->
+// LDS by global_load_lds_dwordx4 with no VGPR staging: a ring of NSTAGE = 3 LDS stages of 64-deep K tiles,
+// DMAs two tiles ahead, ONE s_barrier per K tile after a counted vmcnt that leaves the next tile's DMAs in
+// flight (MI355X guide §5 "glds with >1 tile in flight across the barrier"; the DMAs are inline asm, so
+// hipcc's own waits never drain them early). LDS image per stage and operand: gemm_bf16_nt_kernel's
+// swizzled rows (128-B row r holds K group q at 16-B slot q ^ bswz(r)); a DMA wave-instruction fills 8
+// whole rows (full 128-B lines; the swizzle is applied to the per-lane SOURCE address), the 16x16x32
+// fragment reads of a 16-lane group hit 16 distinct slots. (A [q][row] image, 64 rows of one K group per
+// instruction, reads 16 B of 64 different lines per DMA: 0.55-0.65x the register-staged kernel.) Wave tiles
+// 64 x 64 (256 x 128 tiles) or 32 x 64 (128 x 128). fp32 or bf16 C through gemm_bf16_nt_kernel's epilogues.
+__device__ __forceinline__ void dma16(const void* g, unsigned lds_base) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(lds_base)
+               : "memory", "m0");
+}
+__device__ __forceinline__ unsigned lds_u32(const void* p) {
+  return (unsigned)(size_t)((const __attribute__((address_space(3))) void*)p);
+}
+
+template <int BM, int BN, int WAVES_M, int WAVES_N, bool CBF>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) __attribute__((amdgpu_waves_per_eu(1, 2)))
+void gemm_bf16_dma_kernel(GemmP p) {
+  constexpr int NWV = WAVES_M * WAVES_N, NSTAGE = 3;
+  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N, TM = WM / 16, TN = WN / 16;
+  constexpr int PA = BM * 8, PB = BN * 8, STAGE = PA + PB;   // 16-B units per operand image / stage
+  constexpr int IA = PA / 64 / NWV, IW = PB / 64 / NWV;        // DMA wave-instructions per wave per stage
+  static_assert(IA * 64 * NWV == PA && IW * 64 * NWV == PB && BM % 64 == 0 && BN % 64 == 0,
+                "stage units must split evenly over the waves, 64 rows per instruction");
+  static_assert(IA + IW == 6 || IA + IW == 4, "the vmcnt immediates below count 4 or 6 DMAs per stage");
+  __shared__ uint4 smem[NSTAGE * STAGE];   // ONE shared array (a second one can de-pipeline the DMA waits)
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave / WAVES_N) * WM, wn = (wave % WAVES_N) * WN;
+  const int wgid = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+  int m0, n0;
+  if (p.group_m > 1) {
+    const int gm = p.group_m, per = gm * gridDim.x, grp = wgid / per;
+    const int rows = min(gm, (int)gridDim.y - grp * gm), r = wgid - grp * per;
+    m0 = (grp * gm + r % rows) * BM;
+    n0 = (r / rows) * BN;
+  } else {
+    n0 = (wgid % gridDim.x) * BN;
+    m0 = (wgid / gridDim.x) * BM;
+  }
+  const unsigned short* A = reinterpret_cast<const unsigned short*>(p.A);
+  const unsigned short* W = reinterpret_cast<const unsigned short*>(p.B);
+  // per-lane DMA sources (rows past M / N re-read the last row; their outputs are never stored) and the
+  // wave-uniform LDS bases of its DMA slots in stage 0
+  const unsigned short* asrc[IA];
+  unsigned adst[IA];
+#pragma unroll
+  for (int j = 0; j < IA; ++j) {
+    const int row = 8 * (wave * IA + j) + (lane >> 3), q = (lane & 7) ^ bswz(row);
+    asrc[j] = A + (long)min(m0 + row, p.M - 1) * p.lda + 8 * q;
+    adst[j] = __builtin_amdgcn_readfirstlane(lds_u32(&smem[(wave * IA + j) * 64]));
+  }
+  const unsigned short* wsrc[IW];
+  unsigned wdst[IW];
+#pragma unroll
+  for (int j = 0; j < IW; ++j) {
+    const int row = 8 * (wave * IW + j) + (lane >> 3), q = (lane & 7) ^ bswz(row);
+    wsrc[j] = W + (long)min(n0 + row, p.N - 1) * p.ldb + 8 * q;
+    wdst[j] = __builtin_amdgcn_readfirstlane(lds_u32(&smem[PA + (wave * IW + j) * 64]));
+  }
+  floatx4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int nk = p.K / 64;
+  auto dma = [&](int stage, int t) {   // tile t's slice of this wave, unconditional (clamped re-read)
+    const int k0 = 64 * min(t, nk - 1);
+#pragma unroll
+    for (int j = 0; j < IA; ++j) dma16(asrc[j] + k0, adst[j] + stage * STAGE * 16);
+#pragma unroll
+    for (int j = 0; j < IW; ++j) dma16(wsrc[j] + k0, wdst[j] + stage * STAGE * 16);
+  };
+  auto compute = [&](const uint4* S) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int q = 4 * s + (lane >> 4);
+      bf16x8_t bf[TN];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn + 16 * j + (lane & 15);
+        bf[j] = __builtin_bit_cast(bf16x8_t, S[PA + row * 8 + (q ^ bswz(row))]);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm + 16 * i + (lane & 15);
+        const bf16x8_t af = __builtin_bit_cast(bf16x8_t, S[row * 8 + (q ^ bswz(row))]);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  };
+  dma(0, 0);
+  dma(1, 1);
+  int stage = 0;
+  for (int t = 0; t < nk; ++t) {
+    // own tile-t DMAs landed (tile t+1's may still fly), then everyone's; stage t-1 is free again
+    if constexpr (IA + IW == 6) asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+    dma(stage == 0 ? 2 : stage - 1, t + 2);
+    compute(smem + stage * STAGE);
+    stage = stage == 2 ? 0 : stage + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA into LDS outlives the loop
+  if constexpr (CBF) {
+    // bf16 C through LDS (gemm_bf16_nt_kernel's CBF epilogue): each wave rounds its WM x WN sub-tile into its
+    // own LDS region, then stores 16-B row chunks
+    static_assert(NWV * WM * WN * 2 <= (int)sizeof(smem), "bf16 tile must fit the LDS stages");
+    __syncthreads();
+    unsigned short* T = reinterpret_cast<unsigned short*>(smem) + wave * (WM * WN);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int cl = 16 * j + (lane & 15), col = min(n0 + wn + cl, p.N - 1);
+      const float bj = p.bias ? p.bias[col] : 0.f, cs = p.colscale ? p.colscale[col] : 1.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int rl = 16 * i + 4 * (lane >> 4) + r;
+          float v = apply_act(p.alpha * acc[i][j][r] + bj, p.act);
+          if (p.aux) v *= p.aux[(long)min(m0 + wm + rl, p.M - 1) * p.ld_aux + col];
+          T[rl * WN + cl] = __builtin_bit_cast(unsigned short, (__bf16)(v * cs));
+        }
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes landed (wave-private region)
+    __builtin_amdgcn_wave_barrier();
+    constexpr int CPR = WN / 8;           // 16-B chunks per row
+    unsigned short* C = reinterpret_cast<unsigned short*>(p.C);
+#pragma unroll
+    for (int it = 0; it < WM * CPR / 64; ++it) {
+      const int q = lane + 64 * it, rl = q / CPR, c8 = (q % CPR) * 8;
+      const int row = m0 + wm + rl, col = n0 + wn + c8;
+      const uint4 u = *reinterpret_cast<const uint4*>(T + rl * WN + c8);
+      if (row < p.M && col < p.N) *reinterpret_cast<uint4*>(C + (long)row * p.ldc + col) = u;
+    }
+  } else {
+    store_tile_mf<16, TM, TN, BM, BN>(p, acc, 0, 0, m0, n0, wm, wn, lane);
+  }
+}
+
 }  // namespace
 
 struct Plan { int cfg, splitk, kchunk; int64_t ws; int sk_grid, sk_dp, sk_tiles, sk_ipt; int group_m; };
@@ -2315,6 +2463,17 @@ constexpr int kX6Force = 1 << 21;   // dasa_gemm_force_config(kX6Force + cfg): b
 
 extern "C" int dasa_gemm_bf16(const dasa_gemm_desc* d, void* stream) { return dasa_gemm_bf16_ex(d, 0, stream); }
 
+static int g_bf16_dma = -1;   // the LDS-DMA bf16 probe form: -1 = not read from DASA_BF16_DMA yet
+extern "C" int dasa_gemm_bf16_dma(int32_t on) {
+  if (g_bf16_dma < 0) {
+    const char* e = getenv("DASA_BF16_DMA");
+    g_bf16_dma = (e && e[0] == '1') ? 1 : 0;
+  }
+  const int prev = g_bf16_dma;
+  if (on >= 0) g_bf16_dma = on ? 1 : 0;
+  return prev;
+}
+
 extern "C" int dasa_gemm_bf16_ex(const dasa_gemm_desc* d, int32_t flags, void* stream) {
   if (!d) return (int)hipErrorInvalidValue;
   const int M = d->M, N = d->N, K = d->K, batch = d->batch < 1 ? 1 : d->batch;
@@ -2351,6 +2510,24 @@ extern "C" int dasa_gemm_bf16_ex(const dasa_gemm_desc* d, int32_t flags, void* s
   p.group_m = cdiv(M, bm) >= 8 ? 4 : 1;
   dim3 grid((unsigned)cdiv(N, bn), (unsigned)cdiv(M, bm), batch);
   hipStream_t st = (hipStream_t)stream;
+  // DASA_BF16_DMA=1 (probe, off by default): A already bf16, one batch -> both operands by LDS-DMA
+  // (gemm_bf16_dma_kernel), 256 x 128 tiles when there are >= 240 of them, else 128 x 128. Bitwise equal to
+  // the register-staged forms below but 0.8-1.2x them on the configs[4] shapes (profiles/r06/bf16_dma/)
+  if (abf && batch == 1 && dasa_gemm_bf16_dma(-1) && !(g_force_cfg >= kBf16Force && g_force_cfg < kX6Force) && (d->ldb & 7) == 0) {
+    const bool wide = cdiv(M, 256) * cdiv(N, 128) >= 240;
+    p.group_m = cdiv(M, wide ? 256 : 128) >= 8 ? 4 : 1;
+    const dim3 gw((unsigned)cdiv(N, 128), (unsigned)cdiv(M, 256)), gs((unsigned)cdiv(N, 128), (unsigned)cdiv(M, 128));
+    hipStream_t s2 = (hipStream_t)stream;
+    if (wide) {
+      if (cbf) hipLaunchKernelGGL((gemm_bf16_dma_kernel<256, 128, 4, 2, true>), gw, dim3(512), 0, s2, p);
+      else hipLaunchKernelGGL((gemm_bf16_dma_kernel<256, 128, 4, 2, false>), gw, dim3(512), 0, s2, p);
+    } else {
+      if (cbf) hipLaunchKernelGGL((gemm_bf16_dma_kernel<128, 128, 4, 2, true>), gs, dim3(512), 0, s2, p);
+      else hipLaunchKernelGGL((gemm_bf16_dma_kernel<128, 128, 4, 2, false>), gs, dim3(512), 0, s2, p);
+    }
+    DASA_CHECK_LAUNCH();
+    return 0;
+  }
   if (abf || cbf) {   // the bf16-activation forms: the two tile shapes of the default plan
     const dim3 g9((unsigned)cdiv(N, 256), (unsigned)cdiv(M, 256), batch), g2((unsigned)cdiv(N, 128), (unsigned)cdiv(M, 128), batch);
     const bool big = cfg == 9;

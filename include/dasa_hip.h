@@ -89,6 +89,9 @@ int dasa_gemm_bf16(const dasa_gemm_desc* d, void* stream);
 #define DASA_BF16_A 1
 #define DASA_BF16_C 2
 int dasa_gemm_bf16_ex(const dasa_gemm_desc* d, int32_t flags, void* stream);
+/* LDS-DMA probe form of the bf16 GEMM with a bf16 A (both operands by global_load_lds, a 3-stage ring): 1 on,
+ * 0 off (default; DASA_BF16_DMA=1 starts it on), < 0 only queries. Returns the previous setting. Host-only. */
+int dasa_gemm_bf16_dma(int32_t on);
 /* y[i] = bf16(x[i]) (round to nearest even), n even; weight copies for dasa_gemm_bf16. */
 int dasa_f32_to_bf16(const float* x, uint16_t* y, int64_t n, void* stream);
 /* fp32 nn.Linear forward at fp32 accuracy on the bf16 matrix cores ("bf16x6"): every fp32 operand is

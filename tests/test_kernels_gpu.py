@@ -1001,6 +1001,34 @@ def test_gemm_bf16_activations(dev, M):
         ops.linear(hbf, W2, b2)
 
 
+@pytest.mark.parametrize("M,N,K,cbf", [(777, 200, 192, False), (300, 3072, 768, True), (9216, 768, 3072, False),
+                                       (20480, 2304, 768, True), (65, 64, 64, False)])
+def test_gemm_bf16_dma_matches_register_staged(dev, M, N, K, cbf):
+    """The LDS-DMA bf16 GEMM probe form (A already bf16: gemm_bf16_dma_kernel, 256 x 128 / 128 x 128 tiles,
+    switched on by dasa_gemm_bf16_dma) against the register-staged default (forced through a bf16 tile form): the same MFMAs over
+    the same K order, so bitwise equal - row / column tails, bias + activation epilogue, fp32 and bf16 C."""
+    from dasa_amd import ops, _lib
+    g = torch.Generator().manual_seed(M + N + K)
+    x = _rand(M, K, g=g).to(dev)
+    W, b = _rand(N, K, g=g, scale=0.05).to(dev), _rand(N, g=g).to(dev)
+    od = torch.bfloat16 if cbf else None
+    with torch.no_grad(), ops.bf16_matmul():
+        xb = ops.to_bf16(x)
+        prev = _lib.lib().dasa_gemm_bf16_dma(1)
+        try:
+            y_dma = ops.linear(xb, W, b, act="gelu", out_dtype=od)
+        finally:
+            _lib.lib().dasa_gemm_bf16_dma(prev)
+        lib = _lib.lib()
+        lib.dasa_gemm_force_config((1 << 20) + (9 if M * N >= 200 * 256 * 256 else 2))
+        try:
+            y_reg = ops.linear(xb, W, b, act="gelu", out_dtype=od)
+        finally:
+            lib.dasa_gemm_force_config(-1)
+    torch.cuda.synchronize()
+    assert torch.equal(y_dma.view(torch.int16) if cbf else y_dma, y_reg.view(torch.int16) if cbf else y_reg)
+
+
 @pytest.mark.parametrize("M", [300, 5120])
 def test_layernorm_bf16_twin(dev, M):
     """configs[4]'s bf16 mode: LayerNorm also writes bf16(y) (dasa_layernorm_fwd_bf16) and the next bf16 GEMM takes
