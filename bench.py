@@ -457,8 +457,10 @@ def cfg5_leg(a):
                     if key in summ["roofline"]:
                         ent["roofline"][key] = summ["roofline"][key]
         res[mode] = ent
-    res["dtype_note"] = ("bf16: nn.Linear operands rounded to bf16 (weights once, activations on load), fp32 "
-                         "accumulation and epilogue; attention cores, LayerNorm, softmax, LSTM recurrences fp32")
+    res["dtype_note"] = ("bf16: nn.Linear operands bf16 (weights converted once; activations handed on as bf16 by "
+                         "their producers - LayerNorm twin, GELU, attention core - or rounded on load), Q/K/V and the "
+                         "attention core bf16 (P rounded to bf16), the B=256 bi-LSTM recurrence on bf16 W_hh / h; "
+                         "fp32 accumulation, epilogues, softmax, LayerNorm statistics and the residual stream")
     del agent
     torch.cuda.empty_cache()
     return res
