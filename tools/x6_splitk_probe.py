@@ -20,6 +20,9 @@ FORMS = [(8, 0), (8, 2), (8, 4), (8, 8), (4, 1), (4, 2), (4, 3), (4, 4), (4, 6),
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+    global SHAPES
+    if len(sys.argv) > 2:   # MxNxK[xbatch],... (e.g. the 5760-row vision-token shapes of a teacher chunk)
+        SHAPES = [tuple(int(v) for v in (s.split("x") + ["1"])[:4]) for s in sys.argv[2].split(",")]
     dev = torch.device("cuda", 0)
     L = _lib.lib()
     g = torch.Generator(device=dev).manual_seed(0)
