@@ -26,7 +26,12 @@ __device__ __forceinline__ unsigned lds_u32(const void* p) {
   return (unsigned)(size_t)((const __attribute__((address_space(3))) void*)p);
 }
 
-template <int BM, int BN, int WAVES_M, int WAVES_N, int NSTAGE>
+// IMG = 1 (r06, forms 4 / 5): each plane image row-major, 128-row x 64-B rows of four 16-B K groups, group q
+// of row r at slot q ^ ((r >> 2) & 3): a DMA wave-instruction fills 16 whole 64-B row slices (16 lines
+// instead of 64), the fragment reads of a 16-lane group still hit 16 distinct bank slots.
+__device__ __forceinline__ int pswz(int row) { return (row >> 2) & 3; }
+
+template <int BM, int BN, int WAVES_M, int WAVES_N, int NSTAGE, int IMG = 0>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N) __attribute__((amdgpu_waves_per_eu(1, 2)))
 void gemm_f32x6_pp_kernel(GemmP p, long wplane, long aplane) {
   constexpr int NWV = WAVES_M * WAVES_N;
@@ -67,7 +72,8 @@ void gemm_f32x6_pp_kernel(GemmP p, long wplane, long aplane) {
   unsigned adst[IA];
 #pragma unroll
   for (int j = 0; j < IA; ++j) {
-    const int u = (wave * IA + j) * 64 + lane, pl = u / PA, rem = u % PA, q = rem / BM, row = rem % BM;
+    const int u = (wave * IA + j) * 64 + lane, pl = u / PA, rem = u % PA;
+    const int row = IMG ? rem / 4 : rem % BM, q = IMG ? (rem % 4) ^ pswz(row) : rem / BM;
     asrc[j] = A + pl * aplane + (long)min(m0 + row, p.M - 1) * p.lda + 8 * q;
     adst[j] = __builtin_amdgcn_readfirstlane(lds_u32(&smem[(wave * IA + j) * 64]));
   }
@@ -75,7 +81,8 @@ void gemm_f32x6_pp_kernel(GemmP p, long wplane, long aplane) {
   unsigned wdst[IW];
 #pragma unroll
   for (int j = 0; j < IW; ++j) {
-    const int u = (wave * IW + j) * 64 + lane, pl = u / PB, rem = u % PB, q = rem / BN, row = rem % BN;
+    const int u = (wave * IW + j) * 64 + lane, pl = u / PB, rem = u % PB;
+    const int row = IMG ? rem / 4 : rem % BN, q = IMG ? (rem % 4) ^ pswz(row) : rem / BN;
     wsrc[j] = W + pl * wplane + (long)min(n0 + row, p.N - 1) * p.ldb + 8 * q;
     wdst[j] = __builtin_amdgcn_readfirstlane(lds_u32(&smem[3 * PA + (wave * IW + j) * 64]));
   }
@@ -93,14 +100,18 @@ void gemm_f32x6_pp_kernel(GemmP p, long wplane, long aplane) {
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl)
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-        bf[pl][j] = __builtin_bit_cast(bf16x8_t, S[3 * PA + pl * PB + q * BN + wn + 16 * j + (lane & 15)]);
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn + 16 * j + (lane & 15);
+        bf[pl][j] = __builtin_bit_cast(bf16x8_t, S[3 * PA + pl * PB + (IMG ? row * 4 + (q ^ pswz(row)) : q * BN + row)]);
+      }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       bf16x8_t af[3];
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl)
-        af[pl] = __builtin_bit_cast(bf16x8_t, S[pl * PA + q * BM + wm + 16 * i + (lane & 15)]);
+      for (int pl = 0; pl < 3; ++pl) {
+        const int row = wm + 16 * i + (lane & 15);
+        af[pl] = __builtin_bit_cast(bf16x8_t, S[pl * PA + (IMG ? row * 4 + (q ^ pswz(row)) : q * BM + row)]);
+      }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         floatx4& sm = small[i][j];
@@ -145,7 +156,8 @@ void gemm_f32x6_pp_kernel(GemmP p, long wplane, long aplane) {
 
 // C = epilogue(A . W^T) at fp32 accuracy, A and W both as three bf16 planes (dasa_f32_split3_bf16 layout):
 // d->A / d->B = the hi planes (bf16 elements, row strides lda / ldb), the mid / lo planes aplane / wplane
-// elements further on. form 3: 128 x 128 tiles, three-stage DMA ring; form 2: 256 x 128, two stages.
+// elements further on. form 3: 128 x 128 tiles, three-stage DMA ring; form 2: 256 x 128, two stages; forms 4 / 5:
+// forms 3 / 2 with the row-major plane images (IMG = 1).
 // K % 32 == 0; lda, ldb, planes % 8 == 0; 16-B aligned planes; batch 1. Probe entry.
 extern "C" int dasa_gemm_f32x6_pp(const dasa_gemm_desc* d, int64_t wplane, int64_t aplane, int32_t form,
                                   void* stream) {
@@ -153,7 +165,7 @@ extern "C" int dasa_gemm_f32x6_pp(const dasa_gemm_desc* d, int64_t wplane, int64
   const int M = d->M, N = d->N, K = d->K;
   if (M <= 0 || N <= 0 || K <= 0 || d->opA != 0 || d->opB != 1 || d->batch > 1 || (K & 31) || (d->lda & 7) ||
       (d->ldb & 7) || (wplane & 7) || (aplane & 7) || d->lda < K || d->ldb < K || d->ldc < N ||
-      ((uintptr_t)d->A & 15) || ((uintptr_t)d->B & 15) || (form != 2 && form != 3))
+      ((uintptr_t)d->A & 15) || ((uintptr_t)d->B & 15) || form < 2 || form > 5)
     return (int)hipErrorInvalidValue;
   GemmP p{};
   p.M = M; p.N = N; p.K = K; p.batch = 1; p.splitk = 1; p.kchunk = K;
@@ -163,14 +175,18 @@ extern "C" int dasa_gemm_f32x6_pp(const dasa_gemm_desc* d, int64_t wplane, int64
   p.bias = d->bias; p.act = d->act;
   p.aux = d->aux; p.ld_aux = d->ld_aux;
   p.colscale = d->colscale; p.alpha = d->alpha; p.beta = d->beta;
-  const int bm = form == 2 ? 256 : 128;
+  const int bm = (form == 2 || form == 5) ? 256 : 128;
   p.group_m = cdiv(M, bm) >= 8 ? -8 : 1;
   const dim3 grid((unsigned)cdiv(N, 128), (unsigned)cdiv(M, bm), 1);
   hipStream_t st = (hipStream_t)stream;
   if (form == 2)
     hipLaunchKernelGGL((gemm_f32x6_pp_kernel<256, 128, 4, 2, 2>), grid, dim3(512), 0, st, p, (long)wplane, (long)aplane);
-  else
+  else if (form == 3)
     hipLaunchKernelGGL((gemm_f32x6_pp_kernel<128, 128, 4, 2, 3>), grid, dim3(512), 0, st, p, (long)wplane, (long)aplane);
+  else if (form == 5)
+    hipLaunchKernelGGL((gemm_f32x6_pp_kernel<256, 128, 4, 2, 2, 1>), grid, dim3(512), 0, st, p, (long)wplane, (long)aplane);
+  else
+    hipLaunchKernelGGL((gemm_f32x6_pp_kernel<128, 128, 4, 2, 3, 1>), grid, dim3(512), 0, st, p, (long)wplane, (long)aplane);
   DASA_CHECK_LAUNCH();
   return 0;
 }

@@ -56,7 +56,7 @@ def main():
         line = f"{M:>5}x{N:>5}x{K:>5}"
         res = {}
         for name, fn in (("default", run_default), ("f8", forced(8)), ("f20", forced(20)), ("f7", forced(7)),
-                         ("pp3", pp(3)), ("pp2", pp(2))):
+                         ("pp3", pp(3)), ("pp2", pp(2)), ("pp4", pp(4)), ("pp5", pp(5))):
             us = _time_graph(fn, reps)
             fn()
             torch.cuda.synchronize()
@@ -64,7 +64,7 @@ def main():
             line += f" | {name} {us:7.1f}us {fl / us / 1e6:5.1f}TF"
         us_split = _time_graph(lambda: ops.split3_bf16(A), reps)
         line += f" | splitA {us_split:6.1f}us"
-        eq = {k: torch.equal(res[k], res["f8"]) for k in ("pp3", "pp2", "f20")}
+        eq = {k: torch.equal(res[k], res["f8"]) for k in ("pp3", "pp2", "pp4", "pp5", "f20")}
         print(line + f" | bitwise==f8 {eq}", flush=True)
         del A, W, wp, ap, y
         torch.cuda.empty_cache()
