@@ -340,6 +340,42 @@ def _graph_leaves(outs):
     return leaves
 
 
+_PARAM_WALK = os.environ.get("DASA_PARAM_WALK", "0") == "1"   # A/B: the flat-key regions walk every call
+
+
+class _ParamWatch:
+    """The identity / storage key of the parameters a captured region reads without walking the module
+    tree per call (`module.parameters()` recurses through every submodule: ~0.3 ms for the ~130 parameters of
+    the finetune's VisionEncoder + LXRT region, per decision step). The tree is flattened once into
+    (container dict, name) entries - every module's `_parameters` and `_modules` - and re-flattened when one
+    of those dicts changed size or a child module was replaced, so a Parameter or submodule assigned anywhere
+    in the tree, or a storage swap (p.data = ...), still changes the key."""
+
+    def __init__(self, modules):
+        self.modules = list(modules)
+        self._flat = None
+
+    def _flatten(self):
+        mods = [mod for m in self.modules for mod in m.modules()]
+        self._edges = [(mod._modules, name, child) for mod in mods for name, child in mod._modules.items()]
+        self._dicts = [(d, len(d)) for mod in mods for d in (mod._modules, mod._parameters)]
+        self._flat = [(mod._parameters, name) for mod in mods for name, p in mod._parameters.items() if p is not None]
+
+    def _stale(self):
+        for d, n in self._dicts:
+            if len(d) != n:
+                return True
+        for d, name, child in self._edges:
+            if d.get(name) is not child:
+                return True
+        return False
+
+    def key(self):
+        if self._flat is None or self._stale():
+            self._flatten()
+        return tuple((id(p), p.data_ptr()) for p in (d[n] for d, n in self._flat) if p is not None)
+
+
 class AutogradGraphs:
     """Training-mode decision steps (agent_dg.py:725-936 with autograd on) as hipGraph
     replays. A region — e.g. the decoder step + the one-kernel policy head — is captured once per slot
@@ -353,9 +389,11 @@ class AutogradGraphs:
     updates need no re-capture); a re-assigned parameter (new storage) re-captures. Host cost of a
     step: the input copies and one graph launch instead of ~30 Python-level launches."""
 
-    def __init__(self, modules):
+    def __init__(self, modules, flat_key=False):
         self.modules = list(modules)
-        self._params = None
+        # flat_key: the parameter key without a module walk per call (the finetune's VL region; the decision
+        # step's decoder region keeps the walk: a faster host there slowed cfg2, DESIGN §4 r06)
+        self._watch = _ParamWatch(self.modules) if flat_key and not _PARAM_WALK else None
         self.slots = {}
         self.uses = {}
         self.stream = None
@@ -365,8 +403,10 @@ class AutogradGraphs:
         self.replays = 0
 
     def _param_key(self):
-        # walked every call (a few dozen parameters): a Parameter object replaced on a module
-        # (module.weight = nn.Parameter(...)) changes the key as well as a storage swap (p.data = ...)
+        # a Parameter object replaced on a module (module.weight = nn.Parameter(...)) changes the key as well
+        # as a storage swap (p.data = ...); in-place updates are read by the replays
+        if self._watch is not None:
+            return self._watch.key()
         return tuple((id(p), p.data_ptr()) for m in self.modules for p in m.parameters())
 
     @contextlib.contextmanager

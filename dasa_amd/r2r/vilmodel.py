@@ -447,7 +447,7 @@ class DicModel(nn.Module):
         parameters get their gradients when the caller's backward reaches it."""
         if self._tgraphs is None:
             mods = [self.vision_encoder, self.addlayer] + ([self.vlayer] if args.d_v_layers > 0 else [])
-            self._tgraphs = graph.AutogradGraphs(mods)
+            self._tgraphs = graph.AutogradGraphs(mods, flat_key=True)
         dev = img_feats.device
         if self._dummy is None or self._dummy.device != dev:
             self._dummy = torch.zeros(0, device=dev, requires_grad=True)

@@ -372,3 +372,36 @@ def test_graph_captures_run_with_gc_disabled(monkeypatch):
                 bad.append((fn, node.lineno, "capture_begin outside graph._graph"))
     assert sites >= 4, sites
     assert not bad, bad
+
+
+def test_graph_param_watch_tracks_parameter_changes():
+    """graph._ParamWatch (the finetune VL region's parameter key, flattened once instead of a module walk per
+    call) equals the walk's key and changes with a re-assigned Parameter, a storage swap, a replaced
+    submodule and a parameter added to a submodule - not with an in-place update (read by the replays)."""
+    import torch.nn as nn
+    from dasa_amd.graph import _ParamWatch
+
+    class Att(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.q, self.k, self.ln = nn.Linear(8, 8), nn.Linear(8, 8), nn.LayerNorm(8)
+
+    mods = [nn.ModuleList([Att() for _ in range(3)]), nn.Linear(4, 4)]
+    walk = lambda: tuple((id(p), p.data_ptr()) for m in mods for p in m.parameters())   # noqa: E731
+    w = _ParamWatch(mods)
+    k0 = w.key()
+    assert k0 == walk() and w.key() == k0
+    with torch.no_grad():
+        mods[0][0].q.weight.add_(1.0)
+    assert w.key() == k0
+    mods[0][1].q.weight = nn.Parameter(torch.randn(8, 8))
+    k1 = w.key()
+    assert k1 != k0 and k1 == walk()
+    mods[0][2] = Att()
+    k2 = w.key()
+    assert k2 != k1 and k2 == walk()
+    mods[0][2].extra = nn.Parameter(torch.randn(3))
+    k3 = w.key()
+    assert len(k3) == len(k2) + 1 and sorted(k3) == sorted(walk())
+    mods[0][0].q.weight.data = torch.randn(8, 8)
+    assert w.key() != k3
