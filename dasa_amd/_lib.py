@@ -99,6 +99,7 @@ SIGNATURES = {
     "dasa_bilstm_bptt_x6": (i32, [i32]),
     "dasa_bilstm_bptt_one_tile": (i32, [i32]),
     "dasa_mha_bwd_split": (i32, [i32]),
+    "dasa_mha_bwd_stamps": (i32, [vp]),
     "dasa_bilstm_fwd_x6": (i32, [i32]),
     "dasa_bilstm_fwd_bf16": (i32, [i32]),
     "dasa_set_error_word": (i32, [vp]),

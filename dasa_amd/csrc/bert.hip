@@ -518,8 +518,25 @@ __device__ __forceinline__ void lds_tn_blocks(const float* A, int lda, const flo
   }
 }
 
+// Diagnosis (dasa_mha_bwd_stamps): workgroup 0's clock (s_memtime, shader cycles) at
+// each phase boundary; one record of kBwdStamps per launch, overwritten by the next.
+constexpr int kBwdStamps = 9;
+template <bool STAMP>
+__device__ __forceinline__ void bwd_stamp(unsigned long long* buf, int i) {
+  if (!STAMP) return;   // the product instantiation carries no stamp code (no scheduling barriers)
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    buf[i] = t;
+  }
+}
+
+template <bool STAMP>
 __global__ __launch_bounds__(256) void mha_bwd_lds_kernel(MhaArgs a, const float* dO, long lddo, float* dQ, float* dK,
-                                                          float* dV, int parts) {
+                                                          float* dV, int parts, unsigned long long* stamps) {
+  bwd_stamp<STAMP>(stamps, 0);
   __shared__ float bufA[kBwdBufA];   // dO^T [64][Lq]; then Q [Lq][64]
   __shared__ float bufB[kBwdBufA];   // V^T [64][Lk]; then K [Lk][64]
   __shared__ float sP[kBwdBufL];     // P [Lq][Lk]; then P_dropped
@@ -567,6 +584,7 @@ __global__ __launch_bounds__(256) void mha_bwd_lds_kernel(MhaArgs a, const float
     }
   }
   __syncthreads();
+  bwd_stamp<STAMP>(stamps, 1);
   // dP (masked by the forward's dropout scale) into sdS
   lds_tn_blocks(bufA, kBwdLd, bufB, kBwdLd, kDh, 0, Lq4 / 4, Lk4 / 4, [&](int m0, int n0, float (&acc)[4][4]) {
 #pragma unroll
@@ -581,12 +599,14 @@ __global__ __launch_bounds__(256) void mha_bwd_lds_kernel(MhaArgs a, const float
       }
   });
   __syncthreads();
+  bwd_stamp<STAMP>(stamps, 2);
   for (int i = t; i < Lq; i += blockDim.x) {
     float s = 0.f;
     for (int j = 0; j < Lk; ++j) s = fmaf(sP[i * kBwdLd + j], sdS[i * kBwdLd + j], s);
     rowdot[i] = s;
   }
   __syncthreads();
+  bwd_stamp<STAMP>(stamps, 3);
   for (int idx = t; idx < Lq4 * Lk4; idx += blockDim.x) {
     const int i = idx / Lk4, j = idx % Lk4;
     float g = 0.f;
@@ -595,6 +615,7 @@ __global__ __launch_bounds__(256) void mha_bwd_lds_kernel(MhaArgs a, const float
     sdST[j * kBwdLd + i] = g;
   }
   __syncthreads();
+  bwd_stamp<STAMP>(stamps, 4);
   // the dropped probabilities feed dV; Q and K replace dO^T / V^T
   if (drop)
     for (int idx = t; idx < Lq * Lk; idx += blockDim.x) {
@@ -617,6 +638,7 @@ __global__ __launch_bounds__(256) void mha_bwd_lds_kernel(MhaArgs a, const float
     }
   }
   __syncthreads();
+  bwd_stamp<STAMP>(stamps, 5);
   // dV[j][d] = sum_i Pd[i][j] dO[i][d]
   lds_tn_blocks(sP, kBwdLd, sdO, kBwdLdD, Lq, kb0, kbn, kDh / 4, [&](int m0, int n0, float (&acc)[4][4]) {
 #pragma unroll
@@ -625,6 +647,7 @@ __global__ __launch_bounds__(256) void mha_bwd_lds_kernel(MhaArgs a, const float
         *reinterpret_cast<float4*>(dV + ((long)b * Lk + m0 + r) * a.ldv + h * kDh + n0) =
             make_float4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
   });
+  bwd_stamp<STAMP>(stamps, 6);
   // dQ[i][d] = sum_j dS[i][j] K[j][d]
   lds_tn_blocks(sdST, kBwdLd, bufB, kBwdLdD, Lk, qb0, qbn, kDh / 4, [&](int m0, int n0, float (&acc)[4][4]) {
 #pragma unroll
@@ -633,6 +656,7 @@ __global__ __launch_bounds__(256) void mha_bwd_lds_kernel(MhaArgs a, const float
         *reinterpret_cast<float4*>(dQ + ((long)b * Lq + m0 + r) * a.ldq + h * kDh + n0) =
             make_float4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
   });
+  bwd_stamp<STAMP>(stamps, 7);
   // dK[j][d] = sum_i dS[i][j] Q[i][d]
   lds_tn_blocks(sdS, kBwdLd, bufA, kBwdLdD, Lq, kb0, kbn, kDh / 4, [&](int m0, int n0, float (&acc)[4][4]) {
 #pragma unroll
@@ -641,6 +665,10 @@ __global__ __launch_bounds__(256) void mha_bwd_lds_kernel(MhaArgs a, const float
         *reinterpret_cast<float4*>(dK + ((long)b * Lk + m0 + r) * a.ldk + h * kDh + n0) =
             make_float4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
   });
+  if (STAMP) {   // (stamp 8: this thread's stores drained)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bwd_stamp<STAMP>(stamps, 8);
+  }
 }
 
 // ------------------------------------------------------------------ misc
@@ -1042,6 +1070,11 @@ extern "C" int dasa_mha_fwd_bf16(const void* Q, int64_t ldq, const void* K, int6
 
 // workgroups per (batch, head) of the Lq, Lk <= 80 attention backward: 0 = automatic, n >= 1 forced
 static int g_mha_bwd_parts = 0;
+static unsigned long long* g_mha_stamps = nullptr;   // dasa_mha_bwd_stamps (diagnosis)
+extern "C" int dasa_mha_bwd_stamps(void* buf) {
+  g_mha_stamps = (unsigned long long*)buf;
+  return kBwdStamps;
+}
 extern "C" int dasa_mha_bwd_split(int32_t parts) {
   const int prev = g_mha_bwd_parts;
   if (parts >= 0) g_mha_bwd_parts = parts > 16 ? 16 : parts;
@@ -1063,8 +1096,12 @@ extern "C" int dasa_mha_bwd(const float* Q, int64_t ldq, const float* K, int64_t
       parts = 256 / (B * heads);
       parts = parts < 1 ? 1 : parts > 4 ? 4 : parts;
     }
-    hipLaunchKernelGGL(mha_bwd_lds_kernel, dim3(B * heads * parts), dim3(256), 0, (hipStream_t)stream, a, dout,
-                       (long)lddo, dQ, dK, dV, parts);
+    if (g_mha_stamps)
+      hipLaunchKernelGGL(mha_bwd_lds_kernel<true>, dim3(B * heads * parts), dim3(256), 0, (hipStream_t)stream, a, dout,
+                         (long)lddo, dQ, dK, dV, parts, g_mha_stamps);
+    else
+      hipLaunchKernelGGL(mha_bwd_lds_kernel<false>, dim3(B * heads * parts), dim3(256), 0, (hipStream_t)stream, a,
+                         dout, (long)lddo, dQ, dK, dV, parts, nullptr);
   } else
     hipLaunchKernelGGL(mha_bwd_kernel, dim3(B * heads), dim3(256), 0, (hipStream_t)stream, a, dout, (long)lddo, dQ, dK,
                        dV);

@@ -198,6 +198,9 @@ int dasa_mha_bwd(const float* Q, int64_t ldq, const float* K, int64_t ldk, const
  * while B x heads x parts <= 256; the finetune's B = 2), n >= 1 forced (at most 16), < 0 only
  * queries. Returns the previous setting. Host-only.                                               */
 int dasa_mha_bwd_split(int32_t parts);
+/* Diagnosis: the LDS-staged backward records workgroup 0's shader clock (s_memtime) at its 9 phase boundaries
+ * into buf (9 uint64, device memory; NULL stops). Returns the record length. Host-only.                    */
+int dasa_mha_bwd_stamps(void* buf);
 
 /* ---- SoftDot / ShiftSoftDot attention (model.py:253-353) ------------------------------------
  * q [B][D] is linear_in(h) (computed by dasa_gemm_f32); ctx [B][N][ldn] (ldn >= D, batch stride
