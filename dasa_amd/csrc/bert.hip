@@ -537,8 +537,8 @@ template <bool STAMP>
 __global__ __launch_bounds__(256) void mha_bwd_lds_kernel(MhaArgs a, const float* dO, long lddo, float* dQ, float* dK,
                                                           float* dV, int parts, unsigned long long* stamps) {
   bwd_stamp<STAMP>(stamps, 0);
-  __shared__ float bufA[kBwdBufA];   // dO^T [64][Lq]; then Q [Lq][64]
-  __shared__ float bufB[kBwdBufA];   // V^T [64][Lk]; then K [Lk][64]
+  __shared__ float bufA[kBwdBufA];   // Q [Lq][64] (after dS)
+  __shared__ float bufB[kBwdBufA];   // V [Lk][64]; then K [Lk][64]
   __shared__ float sP[kBwdBufL];     // P [Lq][Lk]; then P_dropped
   __shared__ float sdO[kBwdMaxL * kBwdLdD];   // dO [Lq][64]
   __shared__ float sdS[kBwdBufL];    // dP, then dS [Lq][Lk]
@@ -571,11 +571,8 @@ __global__ __launch_bounds__(256) void mha_bwd_lds_kernel(MhaArgs a, const float
 #pragma unroll
     for (int it = 0; it < NR; ++it) {
       const int idx = t + 256 * it, i = idx / kDh, d = idx % kDh;
-      if (i < Lq4) {
-        sdO[i * kBwdLdD + d] = vo[it];
-        bufA[d * kBwdLd + i] = vo[it];
-      }
-      if (i < Lk4) bufB[d * kBwdLd + i] = vv[it];
+      if (i < Lq4) sdO[i * kBwdLdD + d] = vo[it];
+      if (i < Lk4) bufB[i * kBwdLdD + d] = vv[it];   // V row-major: the dP MFMA's B fragments
     }
 #pragma unroll
     for (int it = 0; it < NP; ++it) {
@@ -585,19 +582,43 @@ __global__ __launch_bounds__(256) void mha_bwd_lds_kernel(MhaArgs a, const float
   }
   __syncthreads();
   bwd_stamp<STAMP>(stamps, 1);
-  // dP (masked by the forward's dropout scale) into sdS
-  lds_tn_blocks(bufA, kBwdLd, bufB, kBwdLd, kDh, 0, Lq4 / 4, Lk4 / 4, [&](int m0, int n0, float (&acc)[4][4]) {
+  // dP = dO V^T (masked by the forward's dropout scale) into sdS, on v_mfma_f32_32x32x2_f32 (r06: on the VALU
+  // 4x4 blocks it was the kernel's longest phase, 14-29 k cycles, tools/mha_bwd_stamps.py): 32x32 tiles of
+  // (query i, key j) dealt round-robin to the 4 waves; A = dO rows, B = V rows, lane (j, half hh) feeding
+  // dims 8g + 4hh + e to MFMA e (the forward's K-permutation); rows past the staged ones clamp to row 79
+  // (their outputs are never stored)
+  {
+    const int lane = t & 63, w = t >> 6, jl = lane & 31, hh = lane >> 5;
+    const int ntj = (Lk4 + 31) / 32, ntiles = ((Lq4 + 31) / 32) * ntj;
+    for (int tile = w; tile < ntiles; tile += 4) {
+      const int i0 = (tile / ntj) * 32, j0 = (tile % ntj) * 32;
+      const float* ap = sdO + min(i0 + jl, kBwdMaxL - 1) * kBwdLdD + 4 * hh;
+      const float* bp = bufB + min(j0 + jl, kBwdMaxL - 1) * kBwdLdD + 4 * hh;
+      floatx16 acc;
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int i = m0 + r, j = n0 + c;
-        float v = 0.f;
-        if (i < Lq && j < Lk)
-          v = drop ? acc[r][c] * dasa_dropout_scale(a.p, sdk, (uint64_t)(pbase + (long)i * Lk + j)) : acc[r][c];
-        sdS[i * kBwdLd + j] = v;
+      for (int g = 0; g < 8; ++g) {
+        const float4 af = *reinterpret_cast<const float4*>(ap + 8 * g);
+        const float4 bf = *reinterpret_cast<const float4*>(bp + 8 * g);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af.x, bf.x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af.y, bf.y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af.z, bf.z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af.w, bf.w, acc, 0, 0, 0);
       }
-  });
+      const int j = j0 + jl;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = i0 + acc_row(r, hh);
+        if (i < Lq4 && j < Lk4) {
+          float v = 0.f;
+          if (i < Lq && j < Lk)
+            v = drop ? acc[r] * dasa_dropout_scale(a.p, sdk, (uint64_t)(pbase + (long)i * Lk + j)) : acc[r];
+          sdS[i * kBwdLd + j] = v;
+        }
+      }
+    }
+  }
   __syncthreads();
   bwd_stamp<STAMP>(stamps, 2);
   for (int i = t; i < Lq; i += blockDim.x) {
