@@ -521,6 +521,41 @@ __device__ __forceinline__ void lds_tn_blocks(const float* A, int lda, const flo
 // Diagnosis (dasa_mha_bwd_stamps): workgroup 0's clock (s_memtime, shader cycles) at
 // each phase boundary; one record of kBwdStamps per launch, overwritten by the next.
 constexpr int kBwdStamps = 9;
+
+// C[m][n] = sum_{k < K} A[k][m] B[k][n] (A, B row-major in LDS) on v_mfma_f32_32x32x2_f32, for rows m in
+// [mlo, mhi) and the 64 columns n: 32 x 32 tiles dealt round-robin to the workgroup's 4 waves; lane (col jl,
+// half hh) supplies k = kk + 4 hh + e to MFMA e of each 8-deep k step (A column / B column reads per k row),
+// k >= K masked to zero. epi(m, n, v) per output of the tile (m may exceed mhi: the caller checks).
+template <typename Epi>
+__device__ __forceinline__ void lds_tn_mfma(const float* A, int lda, const float* B, int ldb, int K, int mlo, int mhi,
+                                            Epi epi) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, jl = lane & 31, hh = lane >> 5;
+  const int ntm = (mhi - mlo + 31) / 32, ntiles = ntm * (kDh / 32);
+  for (int tile = w; tile < ntiles; tile += 4) {
+    const int m0 = mlo + (tile >> 1) * 32, n0 = (tile & 1) * 32;
+    const float* ap = A + min(m0 + jl, lda - 1);
+    const float* bp = B + n0 + jl;
+    floatx16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    for (int kk = 0; kk < K; kk += 8) {
+      float av[4], bv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = kk + 4 * hh + e, kc = min(k, K - 1);
+        const float z = k < K ? 1.f : 0.f;
+        av[e] = z * ap[kc * lda];
+        bv[e] = bp[kc * ldb];
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[e], bv[e], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) epi(m0 + acc_row(r, hh), n0 + jl, acc[r]);
+  }
+}
+
+
 template <bool STAMP>
 __device__ __forceinline__ void bwd_stamp(unsigned long long* buf, int i) {
   if (!STAMP) return;   // the product instantiation carries no stamp code (no scheduling barriers)
@@ -660,31 +695,21 @@ __global__ __launch_bounds__(256) void mha_bwd_lds_kernel(MhaArgs a, const float
   }
   __syncthreads();
   bwd_stamp<STAMP>(stamps, 5);
-  // dV[j][d] = sum_i Pd[i][j] dO[i][d]
-  lds_tn_blocks(sP, kBwdLd, sdO, kBwdLdD, Lq, kb0, kbn, kDh / 4, [&](int m0, int n0, float (&acc)[4][4]) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (m0 + r < Lk)
-        *reinterpret_cast<float4*>(dV + ((long)b * Lk + m0 + r) * a.ldv + h * kDh + n0) =
-            make_float4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
+  // dV / dQ / dK on v_mfma_f32_32x32x2_f32 (lds_tn_mfma; r06: each was ~9 % of the kernel on the VALU blocks).
+  // dV[j][d] = sum_i Pd[i][j] dO[i][d], rows j of this part
+  const int jlo = 4 * kb0, jhi = 4 * (kb0 + kbn), ilo = 4 * qb0, ihi = 4 * (qb0 + qbn);
+  lds_tn_mfma(sP, kBwdLd, sdO, kBwdLdD, Lq, jlo, jhi, [&](int j, int d, float v) {
+    if (j < jhi && j < Lk) dV[((long)b * Lk + j) * a.ldv + h * kDh + d] = v;
   });
   bwd_stamp<STAMP>(stamps, 6);
-  // dQ[i][d] = sum_j dS[i][j] K[j][d]
-  lds_tn_blocks(sdST, kBwdLd, bufB, kBwdLdD, Lk, qb0, qbn, kDh / 4, [&](int m0, int n0, float (&acc)[4][4]) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (m0 + r < Lq)
-        *reinterpret_cast<float4*>(dQ + ((long)b * Lq + m0 + r) * a.ldq + h * kDh + n0) =
-            make_float4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
+  // dQ[i][d] = sum_j dS[i][j] K[j][d], rows i of this part
+  lds_tn_mfma(sdST, kBwdLd, bufB, kBwdLdD, Lk, ilo, ihi, [&](int i, int d, float v) {
+    if (i < ihi && i < Lq) dQ[((long)b * Lq + i) * a.ldq + h * kDh + d] = v;
   });
   bwd_stamp<STAMP>(stamps, 7);
-  // dK[j][d] = sum_i dS[i][j] Q[i][d]
-  lds_tn_blocks(sdS, kBwdLd, bufA, kBwdLdD, Lq, kb0, kbn, kDh / 4, [&](int m0, int n0, float (&acc)[4][4]) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (m0 + r < Lk)
-        *reinterpret_cast<float4*>(dK + ((long)b * Lk + m0 + r) * a.ldk + h * kDh + n0) =
-            make_float4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
+  // dK[j][d] = sum_i dS[i][j] Q[i][d], rows j of this part
+  lds_tn_mfma(sdS, kBwdLd, bufA, kBwdLdD, Lq, jlo, jhi, [&](int j, int d, float v) {
+    if (j < jhi && j < Lk) dK[((long)b * Lk + j) * a.ldk + h * kDh + d] = v;
   });
   if (STAMP) {   // (stamp 8: this thread's stores drained)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
