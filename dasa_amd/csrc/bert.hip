@@ -492,6 +492,9 @@ constexpr int kBwdLd = kBwdMaxL + 4;   // row stride of [.][Lq] / [.][Lk] tiles
 constexpr int kBwdLdD = kDh + 4;       // row stride of [.][64] tiles
 constexpr int kBwdBufA = (kDh * kBwdLd > kBwdMaxL * kBwdLdD) ? kDh * kBwdLd : kBwdMaxL * kBwdLdD;
 constexpr int kBwdBufL = kBwdMaxL * kBwdLd;
+// 8 waves: the LDS footprint (~146 KB) allows one workgroup per CU, so the MFMA tiles and elementwise phases
+// are spread over 8 waves rather than 4 (r06)
+constexpr int kBwdThreads = 512, kBwdWaves = kBwdThreads / 64;
 
 // C[m][n] = sum_k A[k][m] B[k][n] over 4x4 register blocks (A, B row-major in LDS, m / n multiples of 4),
 // m-blocks mb0 .. mb0 + MB - 1.
@@ -523,7 +526,7 @@ __device__ __forceinline__ void lds_tn_blocks(const float* A, int lda, const flo
 constexpr int kBwdStamps = 9;
 
 // C[m][n] = sum_{k < K} A[k][m] B[k][n] (A, B row-major in LDS) on v_mfma_f32_32x32x2_f32, for rows m in
-// [mlo, mhi) and the 64 columns n: 32 x 32 tiles dealt round-robin to the workgroup's 4 waves; lane (col jl,
+// [mlo, mhi) and the 64 columns n: 32 x 32 tiles dealt round-robin to the workgroup's waves; lane (col jl,
 // half hh) supplies k = kk + 4 hh + e to MFMA e of each 8-deep k step (A column / B column reads per k row),
 // k >= K masked to zero. epi(m, n, v) per output of the tile (m may exceed mhi: the caller checks).
 template <typename Epi>
@@ -531,7 +534,7 @@ __device__ __forceinline__ void lds_tn_mfma(const float* A, int lda, const float
                                             Epi epi) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, jl = lane & 31, hh = lane >> 5;
   const int ntm = (mhi - mlo + 31) / 32, ntiles = ntm * (kDh / 32);
-  for (int tile = w; tile < ntiles; tile += 4) {
+  for (int tile = w; tile < ntiles; tile += kBwdWaves) {
     const int m0 = mlo + (tile >> 1) * 32, n0 = (tile & 1) * 32;
     const float* ap = A + min(m0 + jl, lda - 1);
     const float* bp = B + n0 + jl;
@@ -569,7 +572,7 @@ __device__ __forceinline__ void bwd_stamp(unsigned long long* buf, int i) {
 }
 
 template <bool STAMP>
-__global__ __launch_bounds__(256) void mha_bwd_lds_kernel(MhaArgs a, const float* dO, long lddo, float* dQ, float* dK,
+__global__ __launch_bounds__(kBwdThreads) void mha_bwd_lds_kernel(MhaArgs a, const float* dO, long lddo, float* dQ, float* dK,
                                                           float* dV, int parts, unsigned long long* stamps) {
   bwd_stamp<STAMP>(stamps, 0);
   __shared__ float bufA[kBwdBufA];   // Q [Lq][64] (after dS)
@@ -587,31 +590,31 @@ __global__ __launch_bounds__(256) void mha_bwd_lds_kernel(MhaArgs a, const float
   const long pbase = ((long)b * a.heads + h) * Lq * Lk;
   const bool drop = a.p > 0.f;
   // staging: every global load of dO, V and P issued before the first LDS store (fixed trip counts, fully
-  // unrolled: 65 loads in flight per thread, one memory round trip instead of one per loop iteration)
-  constexpr int NR = kBwdMaxL * kDh / 256, NP = kBwdMaxL * kBwdMaxL / 256;
-  static_assert(NR * 256 == kBwdMaxL * kDh && NP * 256 == kBwdMaxL * kBwdMaxL, "staging trip counts");
+  // unrolled: 33 loads in flight per thread, one memory round trip instead of one per loop iteration)
+  constexpr int NR = kBwdMaxL * kDh / kBwdThreads, NP = (kBwdMaxL * kBwdMaxL + kBwdThreads - 1) / kBwdThreads;
+  static_assert(NR * kBwdThreads == kBwdMaxL * kDh, "staging trip counts");
   {
     float vo[NR], vv[NR], vp[NP];
 #pragma unroll
     for (int it = 0; it < NR; ++it) {
-      const int idx = t + 256 * it, i = idx / kDh, d = idx % kDh;
+      const int idx = t + kBwdThreads * it, i = idx / kDh, d = idx % kDh;
       vo[it] = i < Lq ? dO[((long)b * Lq + i) * lddo + h * kDh + d] : 0.f;
       vv[it] = i < Lk ? a.V[((long)b * Lk + i) * a.ldv + h * kDh + d] : 0.f;
     }
 #pragma unroll
     for (int it = 0; it < NP; ++it) {
-      const int idx = t + 256 * it, i = idx / Lk4, j = idx % Lk4;
+      const int idx = t + kBwdThreads * it, i = idx / Lk4, j = idx % Lk4;
       vp[it] = (i < Lq && j < Lk) ? a.probs[pbase + (long)i * Lk + j] : 0.f;
     }
 #pragma unroll
     for (int it = 0; it < NR; ++it) {
-      const int idx = t + 256 * it, i = idx / kDh, d = idx % kDh;
+      const int idx = t + kBwdThreads * it, i = idx / kDh, d = idx % kDh;
       if (i < Lq4) sdO[i * kBwdLdD + d] = vo[it];
       if (i < Lk4) bufB[i * kBwdLdD + d] = vv[it];   // V row-major: the dP MFMA's B fragments
     }
 #pragma unroll
     for (int it = 0; it < NP; ++it) {
-      const int idx = t + 256 * it, i = idx / Lk4, j = idx % Lk4;
+      const int idx = t + kBwdThreads * it, i = idx / Lk4, j = idx % Lk4;
       if (idx < Lq4 * Lk4) sP[i * kBwdLd + j] = vp[it];
     }
   }
@@ -619,13 +622,13 @@ __global__ __launch_bounds__(256) void mha_bwd_lds_kernel(MhaArgs a, const float
   bwd_stamp<STAMP>(stamps, 1);
   // dP = dO V^T (masked by the forward's dropout scale) into sdS, on v_mfma_f32_32x32x2_f32 (r06: on the VALU
   // 4x4 blocks it was the kernel's longest phase, 14-29 k cycles, tools/mha_bwd_stamps.py): 32x32 tiles of
-  // (query i, key j) dealt round-robin to the 4 waves; A = dO rows, B = V rows, lane (j, half hh) feeding
+  // (query i, key j) dealt round-robin to the waves; A = dO rows, B = V rows, lane (j, half hh) feeding
   // dims 8g + 4hh + e to MFMA e (the forward's K-permutation); rows past the staged ones clamp to row 79
   // (their outputs are never stored)
   {
     const int lane = t & 63, w = t >> 6, jl = lane & 31, hh = lane >> 5;
     const int ntj = (Lk4 + 31) / 32, ntiles = ((Lq4 + 31) / 32) * ntj;
-    for (int tile = w; tile < ntiles; tile += 4) {
+    for (int tile = w; tile < ntiles; tile += kBwdWaves) {
       const int i0 = (tile / ntj) * 32, j0 = (tile % ntj) * 32;
       const float* ap = sdO + min(i0 + jl, kBwdMaxL - 1) * kBwdLdD + 4 * hh;
       const float* bp = bufB + min(j0 + jl, kBwdMaxL - 1) * kBwdLdD + 4 * hh;
@@ -682,13 +685,13 @@ __global__ __launch_bounds__(256) void mha_bwd_lds_kernel(MhaArgs a, const float
     float vq[NR], vk[NR];
 #pragma unroll
     for (int it = 0; it < NR; ++it) {
-      const int idx = t + 256 * it, i = idx / kDh, d = idx % kDh;
+      const int idx = t + kBwdThreads * it, i = idx / kDh, d = idx % kDh;
       vq[it] = i < Lq ? a.Q[((long)b * Lq + i) * a.ldq + h * kDh + d] : 0.f;
       vk[it] = i < Lk ? a.K[((long)b * Lk + i) * a.ldk + h * kDh + d] : 0.f;
     }
 #pragma unroll
     for (int it = 0; it < NR; ++it) {
-      const int idx = t + 256 * it, i = idx / kDh, d = idx % kDh;
+      const int idx = t + kBwdThreads * it, i = idx / kDh, d = idx % kDh;
       if (i < Lq4) bufA[i * kBwdLdD + d] = vq[it];
       if (i < Lk4) bufB[i * kBwdLdD + d] = vk[it];
     }
@@ -1143,10 +1146,10 @@ extern "C" int dasa_mha_bwd(const float* Q, int64_t ldq, const float* K, int64_t
       parts = parts < 1 ? 1 : parts > 4 ? 4 : parts;
     }
     if (g_mha_stamps)
-      hipLaunchKernelGGL(mha_bwd_lds_kernel<true>, dim3(B * heads * parts), dim3(256), 0, (hipStream_t)stream, a, dout,
+      hipLaunchKernelGGL(mha_bwd_lds_kernel<true>, dim3(B * heads * parts), dim3(kBwdThreads), 0, (hipStream_t)stream, a, dout,
                          (long)lddo, dQ, dK, dV, parts, g_mha_stamps);
     else
-      hipLaunchKernelGGL(mha_bwd_lds_kernel<false>, dim3(B * heads * parts), dim3(256), 0, (hipStream_t)stream, a,
+      hipLaunchKernelGGL(mha_bwd_lds_kernel<false>, dim3(B * heads * parts), dim3(kBwdThreads), 0, (hipStream_t)stream, a,
                          dout, (long)lddo, dQ, dK, dV, parts, nullptr);
   } else
     hipLaunchKernelGGL(mha_bwd_kernel, dim3(B * heads), dim3(256), 0, (hipStream_t)stream, a, dout, (long)lddo, dQ, dK,
